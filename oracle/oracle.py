@@ -1,0 +1,238 @@
+"""ctypes wrapper around the CPU oracle (oracle/_build/libsts_oracle.so).
+
+TEST INFRASTRUCTURE ONLY.  Only tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline leg may import this module, and only as the checker or the CPU
+baseline.  The product path (spark-timeseries_amd/sparkts -> libsts_hip.so)
+never imports it.
+
+Every wrapped function restates a reference loop; see sts_oracle.c for the
+file:line citations (S/ = /root/reference/src/main/scala/com/cloudera/sparkts/).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "_build", "libsts_oracle.so")
+
+OK, ERR_BAD_ARG, ERR_ALL_NAN, ERR_UNSUPPORTED_METHOD = 0, 1, 2, 3
+ERR_REQUIREMENT, ERR_NOT_ENOUGH_DATA, ERR_SINGULAR = 5, 7, 8
+FILL_METHODS = {"linear": 0, "nearest": 1, "next": 2, "previous": 3}
+
+_lib = None
+_dp = ctypes.POINTER(ctypes.c_double)
+_i64 = ctypes.c_int64
+
+
+def build() -> None:
+    subprocess.check_call(["make", "-s", "-C", HERE])
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = ctypes.CDLL(LIB_PATH)
+        i32p = ctypes.POINTER(ctypes.c_int32)
+        sig = {
+            "orc_fill_previous": (None, [_dp, _dp, _i64]),
+            "orc_fill_next": (None, [_dp, _dp, _i64]),
+            "orc_fill_nearest": (ctypes.c_int, [_dp, _dp, _i64]),
+            "orc_fill_linear": (None, [_dp, _dp, _i64]),
+            "orc_fillts": (ctypes.c_int, [_dp, _dp, _i64, ctypes.c_int]),
+            "orc_autocorr": (None, [_dp, _i64, ctypes.c_int, _dp]),
+            "orc_lag_mat_trim_both": (ctypes.c_int, [_dp, _i64, ctypes.c_int, ctypes.c_int, _dp]),
+            "orc_differences_at_lag": (ctypes.c_int, [_dp, _dp, _i64, ctypes.c_int, ctypes.c_int]),
+            "orc_inverse_differences_at_lag": (ctypes.c_int, [_dp, _dp, _i64, ctypes.c_int, ctypes.c_int]),
+            "orc_differences_of_order_d": (None, [_dp, _dp, _i64, ctypes.c_int]),
+            "orc_ewma_add": (None, [_dp, _dp, _i64, ctypes.c_double]),
+            "orc_ewma_remove": (None, [_dp, _dp, _i64, ctypes.c_double]),
+            "orc_ar_remove": (None, [_dp, _dp, _i64, ctypes.c_double, _dp, ctypes.c_int]),
+            "orc_ar_add": (None, [_dp, _dp, _i64, ctypes.c_double, _dp, ctypes.c_int]),
+            "orc_ar_fit": (ctypes.c_int, [_dp, _i64, ctypes.c_int, ctypes.c_int, _dp, _dp]),
+            "orc_panel_fill": (ctypes.c_int, [_dp, _dp, _i64, _i64, _i64, ctypes.c_int, i32p, ctypes.c_int]),
+            "orc_panel_fill_autocorr": (ctypes.c_int, [_dp, _dp, _i64, _i64, _i64, ctypes.c_int, ctypes.c_int, _dp, i32p, ctypes.c_int]),
+            "orc_panel_fill_diff_ewma": (ctypes.c_int, [_dp, _dp, _i64, _i64, _i64, ctypes.c_double, ctypes.c_int]),
+            "orc_panel_ar_fit_remove": (ctypes.c_int, [_dp, _dp, _i64, _i64, _i64, ctypes.c_int, ctypes.c_int, _dp, _dp, ctypes.c_int]),
+            "orc_gen_value": (ctypes.c_double, [ctypes.c_uint64, _i64, _i64, _i64]),
+            "orc_nan_threshold": (ctypes.c_uint32, [ctypes.c_double]),
+            "orc_gen_panel": (None, [ctypes.c_uint64, _i64, _i64, _i64, _i64, ctypes.c_double, _dp]),
+            "orc_gen_ar_panel": (None, [ctypes.c_uint64, _i64, _i64, _i64, _i64, ctypes.c_int, _dp]),
+            "orc_gen_ar_params": (None, [ctypes.c_uint64, _i64, ctypes.c_int, _dp, _dp]),
+        }
+        for name, (res, args) in sig.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+def _p(a: np.ndarray):
+    assert a.dtype == np.float64 and a.flags["C_CONTIGUOUS"]
+    return a.ctypes.data_as(_dp)
+
+
+def _vec(x) -> np.ndarray:
+    return np.ascontiguousarray(np.asarray(x, dtype=np.float64))
+
+
+class OracleError(Exception):
+    def __init__(self, code: int, msg: str):
+        super().__init__(msg)
+        self.code = code
+
+
+# ---------------- single-series restatements ----------------
+
+def fill_previous(x):
+    x = _vec(x); r = np.empty_like(x); lib().orc_fill_previous(_p(x), _p(r), x.size); return r
+
+
+def fill_next(x):
+    x = _vec(x); r = np.empty_like(x); lib().orc_fill_next(_p(x), _p(r), x.size); return r
+
+
+def fill_nearest(x):
+    x = _vec(x); r = np.empty_like(x)
+    st = lib().orc_fill_nearest(_p(x), _p(r), x.size)
+    if st == ERR_ALL_NAN:
+        raise OracleError(st, "Input is all NaNs!")
+    return r
+
+
+def fill_linear(x):
+    x = _vec(x); r = np.empty_like(x); lib().orc_fill_linear(_p(x), _p(r), x.size); return r
+
+
+def fillts(x, method: str):
+    if method not in FILL_METHODS:
+        raise OracleError(ERR_UNSUPPORTED_METHOD, "unsupported fill method %r" % method)
+    return {"linear": fill_linear, "nearest": fill_nearest, "next": fill_next,
+            "previous": fill_previous}[method](x)
+
+
+def autocorr(x, num_lags: int):
+    x = _vec(x); out = np.empty(num_lags); lib().orc_autocorr(_p(x), x.size, num_lags, _p(out)); return out
+
+
+def lag(x, max_lag: int, include_original: bool):
+    """Breeze DenseMatrix (n - max_lag) x ncols, returned as a 2-D numpy array
+    (rows, cols); the column-major buffer is out.T.ravel()."""
+    x = _vec(x)
+    ncols = max_lag + (1 if include_original else 0)
+    rows = x.size - max_lag
+    buf = np.empty(max(rows, 0) * ncols)
+    st = lib().orc_lag_mat_trim_both(_p(x), x.size, max_lag, int(include_original), _p(buf))
+    if st != OK:
+        raise OracleError(st, "bad lag arguments")
+    return buf.reshape(ncols, rows).T.copy()
+
+
+def differences_at_lag(ts, lag_: int, dest=None, start=None, inplace=False):
+    ts = _vec(ts)
+    start = lag_ if start is None else start
+    if inplace:
+        d = ts
+    else:
+        d = ts.copy() if dest is None else _vec(dest).copy()
+    st = lib().orc_differences_at_lag(_p(ts), _p(d), ts.size, lag_, start)
+    if st != OK:
+        raise OracleError(st, "requirement failed: starting index cannot be less than lag")
+    return d
+
+
+def inverse_differences_at_lag(d, lag_: int, start=None):
+    d = _vec(d); out = d.copy()
+    start = lag_ if start is None else start
+    st = lib().orc_inverse_differences_at_lag(_p(d), _p(out), d.size, lag_, start)
+    if st != OK:
+        raise OracleError(st, "requirement failed: starting index cannot be less than lag")
+    return out
+
+
+def differences_of_order_d(ts, d: int):
+    ts = _vec(ts); out = np.empty_like(ts); lib().orc_differences_of_order_d(_p(ts), _p(out), ts.size, d); return out
+
+
+def ewma_add(ts, s: float, dest=None):
+    ts = _vec(ts); out = np.empty_like(ts) if dest is None else dest
+    lib().orc_ewma_add(_p(ts), _p(out), ts.size, s); return out
+
+
+def ewma_remove(ts, s: float, dest=None):
+    ts = _vec(ts); out = np.empty_like(ts) if dest is None else dest
+    lib().orc_ewma_remove(_p(ts), _p(out), ts.size, s); return out
+
+
+def ar_remove(ts, c: float, coef):
+    ts = _vec(ts); coef = _vec(coef); out = np.empty_like(ts)
+    lib().orc_ar_remove(_p(ts), _p(out), ts.size, c, _p(coef), coef.size); return out
+
+
+def ar_add(ts, c: float, coef, inplace=False):
+    ts = _vec(ts); coef = _vec(coef); out = ts if inplace else np.empty_like(ts)
+    lib().orc_ar_add(_p(ts), _p(out), ts.size, c, _p(coef), coef.size); return out
+
+
+def ar_fit(ts, p: int, no_intercept: bool = False):
+    ts = _vec(ts); c = np.zeros(1); coef = np.zeros(p)
+    st = lib().orc_ar_fit(_p(ts), ts.size, p, int(no_intercept), _p(c), _p(coef))
+    if st != OK:
+        raise OracleError(st, "AR fit failed (status %d)" % st)
+    return float(c[0]), coef
+
+
+# ---------------- panel drivers ----------------
+
+def _panel(x):
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    assert x.ndim == 2
+    return x
+
+
+def panel_fill(x, method: str, threads: int = 1):
+    x = _panel(x); S, T = x.shape; out = np.empty_like(x); err = np.zeros(S, np.int32)
+    lib().orc_panel_fill(_p(x), _p(out), S, T, T, FILL_METHODS[method],
+                         err.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), threads)
+    return out, err
+
+
+def panel_fill_autocorr(x, method, K: int, threads: int = 1):
+    x = _panel(x); S, T = x.shape; filled = np.empty_like(x); acf = np.empty((S, K))
+    err = np.zeros(S, np.int32)
+    m = -1 if method is None else FILL_METHODS[method]
+    lib().orc_panel_fill_autocorr(_p(x), _p(filled), S, T, T, m, K, _p(acf),
+                                  err.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), threads)
+    return filled, acf, err
+
+
+def panel_fill_diff_ewma(x, s: float, threads: int = 1):
+    x = _panel(x); S, T = x.shape; out = np.empty_like(x)
+    lib().orc_panel_fill_diff_ewma(_p(x), _p(out), S, T, T, s, threads); return out
+
+
+def panel_ar_fit_remove(x, p: int, no_intercept=False, threads: int = 1):
+    x = _panel(x); S, T = x.shape; out = np.empty_like(x); c = np.empty(S); coef = np.empty((S, p))
+    lib().orc_panel_ar_fit_remove(_p(x), _p(out), S, T, T, p, int(no_intercept), _p(c), _p(coef), threads)
+    return out, c, coef
+
+
+# ---------------- generator ----------------
+
+def gen_panel(seed: int, S: int, T: int, nan_p: float, s0: int = 0):
+    out = np.empty((S, T)); lib().orc_gen_panel(seed, s0, S, T, T, nan_p, _p(out)); return out
+
+
+def gen_ar_panel(seed: int, S: int, T: int, p: int, s0: int = 0):
+    out = np.empty((S, T)); lib().orc_gen_ar_panel(seed, s0, S, T, T, p, _p(out)); return out
+
+
+def gen_ar_params(seed: int, s: int, p: int):
+    c = np.zeros(1); phi = np.zeros(p); lib().orc_gen_ar_params(seed, s, p, _p(c), _p(phi))
+    return float(c[0]), phi

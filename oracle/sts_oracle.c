@@ -1,0 +1,495 @@
+/*
+ * sts_oracle.c -- CPU restatement of the spark-timeseries hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY (see sts_oracle.h): the parity checker and the
+ * CPU baseline.  Nothing in the shipped library links or calls this file.
+ *
+ * Reference: mjayantkumar/spark-timeseries (Scala 2.10, Breeze 0.10,
+ * commons-math3 3.4.1).  S/ = src/main/scala/com/cloudera/sparkts/.
+ * Build flags: -O2 -ffp-contract=off (JVM double semantics: IEEE binary64,
+ * round-to-nearest, no fused multiply-add).
+ */
+#include "sts_oracle.h"
+
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+/* S/UnivariateTimeSeries.scala:194-204 (fillPrevious) */
+void orc_fill_previous(const double* x, double* r, int64_t n) {
+    double filler = NAN; /* initial value, :196 */
+    for (int64_t i = 0; i < n; i++) {
+        filler = isnan(x[i]) ? filler : x[i];
+        r[i] = filler;
+    }
+}
+
+/* S/UnivariateTimeSeries.scala:214-224 (fillNext) */
+void orc_fill_next(const double* x, double* r, int64_t n) {
+    double filler = NAN;
+    for (int64_t i = n - 1; i >= 0; i--) {
+        filler = isnan(x[i]) ? filler : x[i];
+        r[i] = filler;
+    }
+}
+
+/* S/UnivariateTimeSeries.scala:156-184 (fillNearest), statement by statement.
+ * The loop starts at i = 1: index 0 is never modified and never becomes
+ * lastExisting; ties go to the next value; throws
+ * IllegalArgumentException("Input is all NaNs!") at :170-171. */
+int orc_fill_nearest(const double* x, double* r, int64_t n) {
+    if (r != x) memcpy(r, x, (size_t)n * sizeof(double));
+    int64_t lastExisting = -1;
+    int64_t nextExisting = -1;
+    int64_t i = 1;
+    while (i < n) {
+        if (isnan(r[i])) {
+            if (nextExisting < i) {
+                nextExisting = i + 1;
+                while (nextExisting < n && isnan(r[nextExisting])) nextExisting++;
+            }
+            if (lastExisting < 0 && nextExisting >= n) {
+                return ORC_ERR_ALL_NAN;
+            } else if (nextExisting >= n || (lastExisting >= 0 && i - lastExisting < nextExisting - i)) {
+                r[i] = r[lastExisting];
+            } else {
+                r[i] = r[nextExisting];
+            }
+        } else {
+            lastExisting = i;
+        }
+        i++;
+    }
+    return ORC_OK;
+}
+
+/* S/UnivariateTimeSeries.scala:247-266 (fillLinear).  Interior runs are filled
+ * by a SEQUENTIAL accumulation r[j] = r[j-1] + increment (:259-261), not by
+ * before + k*increment; the two differ in the last bits. */
+void orc_fill_linear(const double* x, double* r, int64_t n) {
+    if (r != x) memcpy(r, x, (size_t)n * sizeof(double));
+    int64_t i = 1;
+    while (i < n - 1) {
+        int64_t rangeStart = i;
+        while (i < n - 1 && isnan(r[i])) i++;
+        double before = r[rangeStart - 1];
+        double after = r[i];
+        if (i != rangeStart && !isnan(before) && !isnan(after)) {
+            /* Double / Int: the Int distance is widened to double */
+            double increment = (after - before) / (double)(int32_t)(i - (rangeStart - 1));
+            for (int64_t j = rangeStart; j < i; j++) r[j] = r[j - 1] + increment;
+        }
+        i++;
+    }
+}
+
+/* S/UnivariateTimeSeries.scala:141-150 (fillts dispatch).  "spline" (commons-
+ * math3 SplineInterpolator) is outside the north_star path and is reported as
+ * unsupported here, exactly as the device library does. */
+int orc_fillts(const double* x, double* r, int64_t n, int method) {
+    switch (method) {
+    case ORC_FILL_LINEAR: orc_fill_linear(x, r, n); return ORC_OK;
+    case ORC_FILL_NEAREST: return orc_fill_nearest(x, r, n);
+    case ORC_FILL_NEXT: orc_fill_next(x, r, n); return ORC_OK;
+    case ORC_FILL_PREVIOUS: orc_fill_previous(x, r, n); return ORC_OK;
+    default: return ORC_ERR_UNSUPPORTED_METHOD;
+    }
+}
+
+/* Breeze 0.10 breeze.stats.mean over a DenseVector slice: sum left to right,
+ * divide by the count (Breeze source is not vendored in /root/reference; the
+ * summation order is an assumption, any other order differs by << 1e-10). */
+static double breeze_mean(const double* v, int64_t len) {
+    double sum = 0.0;
+    for (int64_t k = 0; k < len; k++) sum += v[k];
+    return sum / (double)len;
+}
+
+/* S/UnivariateTimeSeries.scala:68-93 (autocorr).  For lag i >= n the slices are
+ * empty (or inverted); the result is NaN (0/0), see DESIGN.md. */
+void orc_autocorr(const double* ts, int64_t n, int numLags, double* corrs) {
+    for (int i = 1; i <= numLags; i++) {
+        if ((int64_t)i >= n) { corrs[i - 1] = NAN; continue; }
+        const double* slice1 = ts + i;       /* ts(i until n)   :72 */
+        const double* slice2 = ts;           /* ts(0 until n-i) :73 */
+        int64_t len = n - i;
+        double mean1 = breeze_mean(slice1, len);
+        double mean2 = breeze_mean(slice2, len);
+        double variance1 = 0.0, variance2 = 0.0, covariance = 0.0;
+        for (int64_t j = 0; j < len; j++) {
+            double diff1 = slice1[j] - mean1;
+            double diff2 = slice2[j] - mean2;
+            variance1 += diff1 * diff1;
+            variance2 += diff2 * diff2;
+            covariance += diff1 * diff2;
+        }
+        corrs[i - 1] = covariance / (sqrt(variance1) * sqrt(variance2));
+    }
+}
+
+/* S/Lag.scala:62-77 (lagMatTrimBoth, Vector variant): Breeze DenseMatrix of
+ * (n - maxLag) rows x (maxLag + inc) columns, column-major:
+ * M(r, c - init) = x(r + maxLag - c), c = init..maxLag. */
+int orc_lag_mat_trim_both(const double* x, int64_t n, int maxLag, int includeOriginal,
+                          double* out) {
+    int64_t numRows = n - maxLag;
+    if (maxLag < 0 || numRows < 0) return ORC_ERR_BAD_ARG;
+    int initialLag = includeOriginal ? 0 : 1;
+    for (int64_t r = 0; r < numRows; r++)
+        for (int c = initialLag; c <= maxLag; c++)
+            out[(int64_t)(c - initialLag) * numRows + r] = x[r + maxLag - c];
+    return ORC_OK;
+}
+
+/* S/UnivariateTimeSeries.scala:356-376 (differencesAtLag with an explicit dest).
+ * dest may alias ts: the loop then reads values it has already overwritten,
+ * exactly as the JVM loop does.  lag == 0 returns dest untouched (:363-364). */
+int orc_differences_at_lag(const double* ts, double* dest, int64_t n, int lag, int start) {
+    if (!(start >= lag)) return ORC_ERR_REQUIREMENT; /* require(), :361 */
+    if (lag == 0) return ORC_OK;
+    for (int64_t i = 0; i < n; i++)
+        dest[i] = (i < start) ? ts[i] : ts[i] - ts[i - lag];
+    return ORC_OK;
+}
+
+/* S/UnivariateTimeSeries.scala:397-417 (inverseDifferencesAtLag) */
+int orc_inverse_differences_at_lag(const double* d, double* dest, int64_t n, int lag, int start) {
+    if (!(start >= lag)) return ORC_ERR_REQUIREMENT;
+    if (lag == 0) return ORC_OK;
+    for (int64_t i = 0; i < n; i++)
+        dest[i] = (i < start) ? d[i] : d[i] + dest[i - lag];
+    return ORC_OK;
+}
+
+/* S/UnivariateTimeSeries.scala:438-450 (differencesOfOrderD): ping-pong of two
+ * copies so that no call sees its own output. */
+void orc_differences_of_order_d(const double* ts, double* out, int64_t n, int d) {
+    double* a = (double*)malloc((size_t)(n > 0 ? n : 1) * sizeof(double));
+    double* b = (double*)malloc((size_t)(n > 0 ? n : 1) * sizeof(double));
+    memcpy(a, ts, (size_t)n * sizeof(double)); /* diffedTs */
+    memcpy(b, ts, (size_t)n * sizeof(double)); /* origTs */
+    double* diffed = a;
+    double* orig = b;
+    for (int i = 1; i <= d; i++) {
+        double* swap = orig;
+        orig = diffed;
+        diffed = swap;
+        orc_differences_at_lag(orig, diffed, n, 1, i);
+    }
+    memcpy(out, diffed, (size_t)n * sizeof(double));
+    free(a);
+    free(b);
+}
+
+/* S/models/EWMA.scala:135-142 (EWMAModel.addTimeDependentEffects):
+ * dest(0) = ts(0); dest(i) = s*ts(i) + (1 - s)*dest(i-1).  In-place is safe. */
+void orc_ewma_add(const double* ts, double* dest, int64_t n, double s) {
+    if (n <= 0) return;
+    dest[0] = ts[0];
+    for (int64_t i = 1; i < n; i++) dest[i] = s * ts[i] + (1.0 - s) * dest[i - 1];
+}
+
+/* S/models/EWMA.scala:125-133 (removeTimeDependentEffects):
+ * dest(i) = (ts(i) - (1 - s)*ts(i-1)) / s.  In-place is NOT equivalent
+ * (reads the overwritten ts(i-1)); the loop below reproduces that too. */
+void orc_ewma_remove(const double* ts, double* dest, int64_t n, double s) {
+    if (n <= 0) return;
+    dest[0] = ts[0];
+    for (int64_t i = 1; i < n; i++) dest[i] = (ts[i] - (1.0 - s) * ts[i - 1]) / s;
+}
+
+/* S/models/Autoregression.scala:60-73 (ARModel.removeTimeDependentEffects) */
+void orc_ar_remove(const double* ts, double* dest, int64_t n, double c, const double* coef, int p) {
+    for (int64_t i = 0; i < n; i++) {
+        dest[i] = ts[i] - c;
+        for (int j = 0; j < p && i - j - 1 >= 0; j++) dest[i] -= ts[i - j - 1] * coef[j];
+    }
+}
+
+/* S/models/Autoregression.scala:75-88 (ARModel.addTimeDependentEffects, IIR) */
+void orc_ar_add(const double* ts, double* dest, int64_t n, double c, const double* coef, int p) {
+    for (int64_t i = 0; i < n; i++) {
+        dest[i] = c + ts[i];
+        for (int j = 0; j < p && i - j - 1 >= 0; j++) dest[i] += dest[i - j - 1] * coef[j];
+    }
+}
+
+/* commons-math3 3.4.1 OLSMultipleLinearRegression (not vendored in
+ * /root/reference; restated from its published source):
+ *   newSampleData -> validateSampleData (x[0].length + 1 > x.length throws
+ *   NOT_ENOUGH_DATA_FOR_NUMBER_OF_PREDICTORS), intercept column of 1.0 first
+ *   unless noIntercept, QRDecomposition(X, threshold = 0) on X^T rows
+ *   (Householder, performHouseholderReflection), Solver.solve(y): apply the
+ *   reflections to y, back-substitute R; SingularMatrixException when any
+ *   |rDiag| <= 0.  Called from S/models/Autoregression.scala:47-50. */
+int orc_ols_householder(const double* y, const double* x, int64_t m, int k, int no_intercept,
+                        double* beta) {
+    int ncol = k + (no_intercept ? 0 : 1);
+    if (m == 0) return ORC_ERR_NOT_ENOUGH_DATA;
+    if ((int64_t)k + 1 > m) return ORC_ERR_NOT_ENOUGH_DATA;
+    /* qrt = X^T: qrt[col][row] */
+    double* qrt = (double*)malloc((size_t)ncol * (size_t)m * sizeof(double));
+    double* rDiag = (double*)malloc((size_t)ncol * sizeof(double));
+    double* yy = (double*)malloc((size_t)m * sizeof(double));
+    for (int64_t r = 0; r < m; r++) {
+        int cc = 0;
+        if (!no_intercept) qrt[(int64_t)(cc++) * m + r] = 1.0;
+        for (int c = 0; c < k; c++) qrt[(int64_t)(cc++) * m + r] = x[r * k + c];
+        yy[r] = y[r];
+    }
+    int64_t minmn = (int64_t)ncol < m ? ncol : m;
+    for (int64_t minor = 0; minor < minmn; minor++) {
+        double* qrtMinor = qrt + minor * m;
+        double xNormSqr = 0.0;
+        for (int64_t row = minor; row < m; row++) {
+            double c = qrtMinor[row];
+            xNormSqr += c * c;
+        }
+        double a = (qrtMinor[minor] > 0) ? -sqrt(xNormSqr) : sqrt(xNormSqr);
+        rDiag[minor] = a;
+        if (a != 0.0) {
+            qrtMinor[minor] -= a;
+            for (int64_t col = minor + 1; col < ncol; col++) {
+                double* qrtCol = qrt + col * m;
+                double alpha = 0.0;
+                for (int64_t row = minor; row < m; row++) alpha -= qrtCol[row] * qrtMinor[row];
+                alpha /= a * qrtMinor[minor];
+                for (int64_t row = minor; row < m; row++) qrtCol[row] -= alpha * qrtMinor[row];
+            }
+        }
+    }
+    int status = ORC_OK;
+    for (int64_t d = 0; d < minmn; d++)
+        if (fabs(rDiag[d]) <= 0.0) status = ORC_ERR_SINGULAR;
+    if (status == ORC_OK) {
+        for (int64_t minor = 0; minor < minmn; minor++) {
+            const double* qrtMinor = qrt + minor * m;
+            double dotProduct = 0.0;
+            for (int64_t row = minor; row < m; row++) dotProduct += yy[row] * qrtMinor[row];
+            dotProduct /= rDiag[minor] * qrtMinor[minor];
+            for (int64_t row = minor; row < m; row++) yy[row] += dotProduct * qrtMinor[row];
+        }
+        for (int64_t row = minmn - 1; row >= 0; --row) {
+            yy[row] /= rDiag[row];
+            double yRow = yy[row];
+            const double* qrtRow = qrt + row * m;
+            beta[row] = yRow;
+            for (int64_t i = 0; i < row; i++) yy[i] -= yRow * qrtRow[i];
+        }
+    }
+    free(qrt);
+    free(rDiag);
+    free(yy);
+    return status;
+}
+
+/* S/models/Autoregression.scala:38-53 (Autoregression.fitModel):
+ * Y = ts(maxLag until n), X = Lag.lagMatTrimBoth(ts, maxLag) (row r =
+ * [x(r+p-1), ..., x(r)]), OLS with intercept unless noIntercept;
+ * c = params.head (0 if noIntercept), coefficients = params.tail. */
+int orc_ar_fit(const double* ts, int64_t n, int p, int no_intercept, double* c, double* coef) {
+    int64_t m = n - p;
+    if (p < 1 || m <= 0) return ORC_ERR_NOT_ENOUGH_DATA;
+    double* X = (double*)malloc((size_t)m * (size_t)p * sizeof(double));
+    for (int64_t r = 0; r < m; r++)
+        for (int cc = 1; cc <= p; cc++) X[r * p + (cc - 1)] = ts[r + p - cc];
+    double beta[64];
+    if (p + 1 > 64) { free(X); return ORC_ERR_BAD_ARG; }
+    int st = orc_ols_householder(ts + p, X, m, p, no_intercept, beta);
+    free(X);
+    if (st != ORC_OK) return st;
+    if (no_intercept) {
+        *c = 0.0;
+        for (int j = 0; j < p; j++) coef[j] = beta[j];
+    } else {
+        *c = beta[0];
+        for (int j = 0; j < p; j++) coef[j] = beta[j + 1];
+    }
+    return ORC_OK;
+}
+
+/* ---------------- panel drivers: one "partition" per thread (local[N]) ---------------- */
+
+static int clamp_threads(int threads) { return threads > 0 ? threads : 1; }
+
+int orc_panel_fill(const double* in, double* out, int64_t S, int64_t T, int64_t ld, int method,
+                   int32_t* err, int threads) {
+    if (method < 0 || method > 3) return ORC_ERR_UNSUPPORTED_METHOD;
+    int any = 0;
+#pragma omp parallel for schedule(static) num_threads(clamp_threads(threads)) reduction(| : any)
+    for (int64_t s = 0; s < S; s++) {
+        int st = orc_fillts(in + s * ld, out + s * ld, T, method);
+        if (err) err[s] = st;
+        any |= (st != ORC_OK);
+    }
+    return any ? ORC_ERR_ALL_NAN : ORC_OK;
+}
+
+int orc_panel_fill_autocorr(const double* in, double* filled, int64_t S, int64_t T, int64_t ld,
+                            int method, int K, double* acf, int32_t* err, int threads) {
+    if (method < -1 || method > 3) return ORC_ERR_UNSUPPORTED_METHOD;
+    int any = 0;
+#pragma omp parallel for schedule(static) num_threads(clamp_threads(threads)) reduction(| : any)
+    for (int64_t s = 0; s < S; s++) {
+        int st = ORC_OK;
+        if (method >= 0) st = orc_fillts(in + s * ld, filled + s * ld, T, method);
+        else memcpy(filled + s * ld, in + s * ld, (size_t)T * sizeof(double));
+        if (err) err[s] = st;
+        if (st != ORC_OK) {
+            for (int k = 0; k < K; k++) acf[s * K + k] = NAN;
+            any = 1;
+        } else {
+            orc_autocorr(filled + s * ld, T, K, acf + s * K);
+        }
+    }
+    return any ? ORC_ERR_ALL_NAN : ORC_OK;
+}
+
+/* C2 pipeline: fillPrevious -> differencesAtLag(1) -> EWMAModel(s).add */
+int orc_panel_fill_diff_ewma(const double* in, double* out, int64_t S, int64_t T, int64_t ld,
+                             double s, int threads) {
+#pragma omp parallel num_threads(clamp_threads(threads))
+    {
+        double* tmp = (double*)malloc((size_t)(T > 0 ? T : 1) * sizeof(double));
+        double* dif = (double*)malloc((size_t)(T > 0 ? T : 1) * sizeof(double));
+#pragma omp for schedule(static)
+        for (int64_t q = 0; q < S; q++) {
+            orc_fill_previous(in + q * ld, tmp, T);
+            memcpy(dif, tmp, (size_t)T * sizeof(double));
+            orc_differences_at_lag(tmp, dif, T, 1, 1);
+            orc_ewma_add(dif, out + q * ld, T, s);
+        }
+        free(tmp);
+        free(dif);
+    }
+    return ORC_OK;
+}
+
+/* C4 pipeline: Autoregression.fitModel(ts, p) -> ARModel.removeTimeDependentEffects(ts) */
+int orc_panel_ar_fit_remove(const double* in, double* out, int64_t S, int64_t T, int64_t ld,
+                            int p, int no_intercept, double* c, double* coef, int threads) {
+    int any = 0;
+#pragma omp parallel for schedule(static) num_threads(clamp_threads(threads)) reduction(| : any)
+    for (int64_t q = 0; q < S; q++) {
+        int st = orc_ar_fit(in + q * ld, T, p, no_intercept, c + q, coef + q * p);
+        if (st != ORC_OK) {
+            any = 1;
+            c[q] = NAN;
+            for (int j = 0; j < p; j++) coef[q * p + j] = NAN;
+        }
+        orc_ar_remove(in + q * ld, out + q * ld, T, c[q], coef + q * p, p);
+    }
+    return any ? ORC_ERR_SINGULAR : ORC_OK;
+}
+
+/* ---------------- synthetic generator ---------------- */
+
+void orc_philox4x32_10(const uint32_t ctr_in[4], const uint32_t key_in[2], uint32_t out[4]) {
+    uint32_t c0 = ctr_in[0], c1 = ctr_in[1], c2 = ctr_in[2], c3 = ctr_in[3];
+    uint32_t k0 = key_in[0], k1 = key_in[1];
+    for (int r = 0; r < 10; r++) {
+        uint64_t p0 = (uint64_t)0xD2511F53u * c0;
+        uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
+        uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+        uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
+        uint32_t n0 = hi1 ^ c1 ^ k0;
+        uint32_t n2 = hi0 ^ c3 ^ k1;
+        c0 = n0;
+        c1 = lo1;
+        c2 = n2;
+        c3 = lo0;
+        k0 += 0x9E3779B9u;
+        k1 += 0xBB67AE85u;
+    }
+    out[0] = c0;
+    out[1] = c1;
+    out[2] = c2;
+    out[3] = c3;
+}
+
+static inline double u53(uint32_t a, uint32_t b) {
+    uint64_t m = ((uint64_t)(a >> 5) << 26) | (uint64_t)(b >> 6);
+    return (double)m * 0x1p-53;
+}
+
+static inline void gen_words(uint64_t seed, int64_t s, uint64_t t, uint32_t out[4]) {
+    uint32_t ctr[4] = {(uint32_t)t, (uint32_t)(t >> 32), (uint32_t)(uint64_t)s,
+                       (uint32_t)((uint64_t)s >> 32)};
+    uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
+    orc_philox4x32_10(ctr, key, out);
+}
+
+static double gen_series_u(uint64_t seed, int64_t s) {
+    uint32_t w[4];
+    gen_words(seed, s, ~(uint64_t)0, w);
+    return u53(w[0], w[1]);
+}
+
+/* x[s,t] = 100 + 10*u_s + t/T + (u_{s,t} - 0.5) */
+double orc_gen_value(uint64_t seed, int64_t s, int64_t t, int64_t T) {
+    uint32_t w[4];
+    gen_words(seed, s, (uint64_t)t, w);
+    double us = gen_series_u(seed, s);
+    double ust = u53(w[0], w[1]);
+    return ((100.0 + 10.0 * us) + (double)t / (double)T) + (ust - 0.5);
+}
+
+uint32_t orc_nan_threshold(double p) {
+    if (!(p > 0.0)) return 0;
+    if (p >= 1.0) return 0xFFFFFFFFu;
+    return (uint32_t)floor(p * 4294967296.0);
+}
+
+int orc_gen_is_nan(uint64_t seed, int64_t s, int64_t t, uint32_t thr) {
+    uint32_t w[4];
+    gen_words(seed, s, (uint64_t)t, w);
+    return w[2] < thr;
+}
+
+void orc_gen_panel(uint64_t seed, int64_t s0, int64_t S, int64_t T, int64_t ld, double nan_p,
+                   double* out) {
+    uint32_t thr = orc_nan_threshold(nan_p);
+    for (int64_t q = 0; q < S; q++) {
+        int64_t s = s0 + q;
+        double us = gen_series_u(seed, s);
+        for (int64_t t = 0; t < T; t++) {
+            uint32_t w[4];
+            gen_words(seed, s, (uint64_t)t, w);
+            double v = ((100.0 + 10.0 * us) + (double)t / (double)T) + (u53(w[0], w[1]) - 0.5);
+            out[q * ld + t] = (w[2] < thr) ? NAN : v;
+        }
+    }
+}
+
+/* C4: AR(p) series, phi = base * (1 + 0.1*(u_s - 0.5)), c = 1, innovations
+ * u_{s,t} - 0.5, built with ARModel.addTimeDependentEffects semantics. */
+static const double kArBase[8] = {0.3, -0.2, 0.1, 0.05, -0.05, 0.02, -0.02, 0.01};
+
+void orc_gen_ar_params(uint64_t seed, int64_t s, int p, double* c, double* phi) {
+    double us = gen_series_u(seed, s);
+    double scale = 1.0 + 0.1 * (us - 0.5);
+    *c = 1.0;
+    for (int j = 0; j < p; j++) phi[j] = kArBase[j & 7] * scale;
+}
+
+void orc_gen_ar_panel(uint64_t seed, int64_t s0, int64_t S, int64_t T, int64_t ld, int p,
+                      double* out) {
+    double phi[64];
+    for (int64_t q = 0; q < S; q++) {
+        int64_t s = s0 + q;
+        double c;
+        orc_gen_ar_params(seed, s, p, &c, phi);
+        double* d = out + q * ld;
+        for (int64_t t = 0; t < T; t++) {
+            uint32_t w[4];
+            gen_words(seed, s, (uint64_t)t, w);
+            double e = u53(w[0], w[1]) - 0.5;
+            d[t] = c + e;
+            for (int j = 0; j < p && t - j - 1 >= 0; j++) d[t] += d[t - j - 1] * phi[j];
+        }
+    }
+}
