@@ -1,0 +1,231 @@
+#!/usr/bin/env python3
+"""bench.py -- series-elements/s and % HBM roofline of the fused fill + ACF hot path.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c3|c2|c4|c5|c1]
+
+Default workload (the BASELINE.json metric "fill+lag+ACF", config C3): every rank owns
+a C3 shard of 12,500 series x 982,800 minute bars (fp64, 5 % NaN, Philox synthetic,
+generated in HBM); one step = TimeSeriesRDD.fill("linear") + autocorr(numLags = 60)
+of every series (fused: one pass over HBM) + the RCCL all-gather of the per-series
+ACF results when N > 1.  Weak scaling: at N = 8 the job is exactly C3 (100k series,
+786 GB).  Rank 0 prints ONE JSON line.
+
+Multi-GPU: launched by the driver as torch.distributed.run (one process per GPU,
+RANK / LOCAL_RANK / WORLD_SIZE from the env, backend "nccl" = RCCL).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "spark-timeseries_amd"))
+
+HBM_PEAK_GBPS = 8000.0   # MI355X_MICROARCH.md: 8.0 TB/s spec
+
+WORKLOADS = {
+    # name: (series per GPU, steps per series, nan_p, seed, description)
+    "c3": (12_500, 982_800, 0.05, 3,
+           "C3 shard: fill('linear') + autocorr(60), 12,500 series x 982,800 steps per GPU "
+           "(N=8 -> C3's 100k x 982,800, 786 GB)"),
+    "c1": (10_000, 2_520, 0.05, 1, "C1: fill('linear') + autocorr(20), 10,000 series x 2,520 steps"),
+    "c2": (1_000_000, 390, 0.05, 2,
+           "C2: fillPrevious -> differencesAtLag(1) -> EWMA(0.2).add, 1,000,000 series x 390 steps"),
+    "c4": (500_000, 2_520, 0.0, 4, "C4: AR(5) fit + removeTimeDependentEffects, 500,000 series x 2,520 steps"),
+}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--workload", default="c3", choices=sorted(WORKLOADS))
+    ap.add_argument("--series", type=int, default=0, help="override series per GPU (testing)")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU baseline sample")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    from sparkts import _native
+    from sparkts.errors import raise_for_status
+    from sparkts.timeseriesrdd import all_gather_results
+    _native.ensure_device(local)
+    lib = _native.lib()
+
+    S, T, nan_p, seed, desc = WORKLOADS[args.workload]
+    if args.series:
+        S = args.series
+    K, p_ar = 60, 5
+    if args.workload == "c1":
+        K = 20
+    s0 = rank * S                      # this rank's partition of the keyed panel
+    stream = torch.cuda.current_stream(dev)
+    sp = stream.cuda_stream
+
+    x = torch.empty((S, T), dtype=torch.float64, device=dev)
+    out = torch.empty_like(x)
+    acf = torch.empty((S, K), dtype=torch.float64, device=dev)
+    err = torch.zeros(S, dtype=torch.int32, device=dev)
+    if args.workload == "c4":
+        cgen = torch.empty(S, dtype=torch.float64, device=dev)
+        pgen = torch.empty((S, p_ar), dtype=torch.float64, device=dev)
+        raise_for_status(lib.sts_gen_ar_panel(x.data_ptr(), cgen.data_ptr(), pgen.data_ptr(), s0, S, T, T, seed, p_ar,
+                                              sp), "gen")
+        c_fit = torch.empty(S, dtype=torch.float64, device=dev)
+        coef_fit = torch.empty((S, p_ar), dtype=torch.float64, device=dev)
+    else:
+        raise_for_status(lib.sts_gen_panel(x.data_ptr(), s0, S, T, T, seed, nan_p, sp), "gen")
+    smooth = torch.full((S,), 0.2, dtype=torch.float64, device=dev)
+
+    def step():
+        if args.workload in ("c3", "c1"):
+            raise_for_status(lib.sts_fill_autocorr(x.data_ptr(), out.data_ptr(), S, T, T, T, 0, K, acf.data_ptr(),
+                                                   err.data_ptr(), sp), "fill_autocorr")
+            if world > 1:
+                all_gather_results(acf)
+        elif args.workload == "c2":
+            raise_for_status(lib.sts_fill_diff_ewma(x.data_ptr(), out.data_ptr(), S, T, T, T, 3, 1, smooth.data_ptr(),
+                                                    err.data_ptr(), sp), "fill_diff_ewma")
+        elif args.workload == "c4":
+            raise_for_status(lib.sts_ar_fit_remove(x.data_ptr(), out.data_ptr(), S, T, T, T, p_ar, 0,
+                                                   c_fit.data_ptr(), coef_fit.data_ptr(), err.data_ptr(), sp),
+                             "ar_fit_remove")
+            if world > 1:
+                all_gather_results(torch.cat([c_fit[:, None], coef_fit], 1))
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    lib.sts_profile_begin()
+    t0 = time.perf_counter()
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    ev0.record(stream)
+    for _ in range(args.steps):
+        step()
+    ev1.record(stream)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    wall = time.perf_counter() - t0
+    kern_ms = np.zeros(1, dtype=np.float64)
+    launches = np.zeros(1, dtype=np.int64)
+    lib.sts_profile_end(kern_ms.ctypes.data, launches.ctypes.data)
+    elapsed = wall
+    if world > 1:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+
+    elems = float(S) * T * world * args.steps
+    value = elems / elapsed
+    ms_per_step = elapsed / args.steps * 1e3
+    # dominant kernel: the fused series-tile kernel (fill + ACF partials / fill only)
+    bytes_per_launch = 16.0 * S * T      # 8 B read + 8 B filled write per element
+    roofline = None
+    if args.workload in ("c3", "c1") and launches[0] > 0:
+        avg_ms = kern_ms[0] / launches[0]
+        achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9
+        roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                    "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": None,
+                    "kernel": "sts::tile_kernel<4096,5> (fill linear + ACF partials, FP64 MFMA)",
+                    "avg_kernel_ms": round(avg_ms, 4), "bytes_per_launch": bytes_per_launch}
+    elif launches[0] == 0:
+        step_bytes = 16.0 * S * T
+        achieved = step_bytes / (ms_per_step * 1e-3) / 1e9 / 1.0
+        roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                    "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": None,
+                    "note": "whole-step time (single kernel per step)"}
+
+    cpu = None
+    if rank == 0 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args, S, T, K, seed, nan_p, out, acf, p_ar)
+
+    if rank == 0:
+        line = {
+            "metric": "series-elements/sec + % HBM roofline (fill+lag+ACF) at 1/2/4/8 MI355X",
+            "value": value, "unit": "series-elements/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic: Philox4x32-10 counter-based panel generated in HBM (SURVEY.md 8(d)), %g NaN" % nan_p,
+            "config": {"workload": desc, "series_per_gpu": S, "steps_per_series": T,
+                       "numLags": K if args.workload in ("c3", "c1") else None,
+                       "fill": {"c3": "linear", "c1": "linear", "c2": "previous", "c4": None}[args.workload],
+                       "parallelism": "dp%d (series sharded by key, one process per GPU)" % world},
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(args, S, T, K, seed, nan_p, out, acf, p_ar):
+    """The oracle (CPU restatement of the reference loops, oracle/) on a bounded sample of
+    the same workload, one series per thread like Spark local[N].  The sample series are
+    the rank-0 series 0..n-1, so their GPU results are also checked here."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    threads = max(1, min(16, os.cpu_count() or 1))
+    per_round = threads
+    done, elapsed, s_next = 0, 0.0, 0
+    worst_rel, exact = 0.0, True
+    while elapsed < args.cpu_seconds and s_next < S:
+        n = min(per_round, S - s_next)
+        if args.workload == "c4":
+            xs = oracle.gen_ar_panel(seed, n, T, p_ar, s0=s_next)
+        else:
+            xs = oracle.gen_panel(seed, n, T, nan_p, s0=s_next)
+        t0 = time.perf_counter()
+        if args.workload in ("c3", "c1"):
+            rf, racf, _ = oracle.panel_fill_autocorr(xs, "linear", K, threads=threads)
+        elif args.workload == "c2":
+            rf = oracle.panel_fill_diff_ewma(xs, 0.2, threads=threads)
+        else:
+            rf, _, _ = oracle.panel_ar_fit_remove(xs, p_ar, threads=threads)
+        elapsed += time.perf_counter() - t0
+        if s_next == 0:
+            g = out[:n].cpu().numpy()
+            if args.workload != "c4":
+                exact = bool(np.array_equal(np.isnan(g), np.isnan(rf)) and
+                             np.array_equal(np.nan_to_num(g), np.nan_to_num(rf)))
+            if args.workload in ("c3", "c1"):
+                ga = acf[:n].cpu().numpy()
+                fin = ~np.isnan(racf)
+                if fin.any():
+                    worst_rel = float((np.abs(ga[fin] - racf[fin]) / np.abs(racf[fin])).max())
+        done += n
+        s_next += n
+    rate = done * T / elapsed if elapsed > 0 else None
+    return {"value": rate, "unit": "series-elements/s", "cores": threads, "kind": "port",
+            "sample": "%d of the rank-0 series x %d steps (%.1f s of CPU work), oracle/sts_oracle.c restatement of "
+                      "the reference loops, one series per thread (Spark local[%d] analogue); the JVM reference "
+                      "cannot run here" % (done, T, elapsed, threads),
+            "sample_check": {"filled_bit_exact": exact, "acf_max_rel_err": worst_rel}}
+
+
+if __name__ == "__main__":
+    main()

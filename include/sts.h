@@ -1,0 +1,196 @@
+/*
+ * sts.h -- C ABI of libsts_hip.so, the MI355X (gfx950) engine for the
+ * spark-timeseries series-wise hot path.
+ *
+ * Every entry point below replaces a reference operator that Spark calls once
+ * per (key, series) record inside a narrow map task
+ * (TimeSeriesRDD.mapSeries, S/TimeSeriesRDD.scala:188-199).  Here one call
+ * processes a whole PANEL of series (a partition's records gathered into one
+ * buffer), which is the batching the JNI shim performs.
+ *
+ *   S/ = src/main/scala/com/cloudera/sparkts/ in the reference.
+ *
+ * Panel layout: S series x T time steps, fp64, series-contiguous: element
+ * (s, t) of a panel with leading dimension ld (ld >= T) is at p[s*ld + t].
+ * This is Breeze DenseMatrix(T, S) column-major as built by
+ * TimeSeriesRDD.collectAsTimeSeries (S/TimeSeriesRDD.scala:66-71) and each
+ * record's DenseVector.data.  NaN marks a missing observation.
+ *
+ * Memory: functions without a `_host` suffix take DEVICE pointers (HBM,
+ * e.g. hipMalloc'd) and are stream-ordered on `stream` (a hipStream_t; NULL
+ * means hipStreamPerThread, so concurrent executor threads never serialise
+ * on the legacy null stream).  `_host` variants take host pointers, stage
+ * through HBM on the calling thread's stream and return when the results
+ * are back on the host (the JNI path).
+ *
+ * Errors: every function returns an sts_status; sts_last_error() gives a
+ * thread-local message.  Per-series data errors (fillNearest on an all-NaN
+ * series, singular AR designs) are written to an optional device int32
+ * array err_per_series[S] (0 = ok, else an sts_status); when that pointer is
+ * NULL the call synchronises its stream and returns the first failing status,
+ * which is the reference's exception semantics (a task exception).
+ *
+ * Arithmetic: IEEE binary64, no FMA contraction on the bit-exact paths
+ * (fills, differencing, lag matrices, EWMA/AR add and remove); the
+ * reductions (autocorr, AR fit) match the reference within 1e-10 relative.
+ */
+#ifndef STS_H
+#define STS_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define STS_ABI_VERSION 1
+
+/* Status codes.  The comment names the JVM exception the reference throws. */
+typedef enum sts_status {
+    STS_OK = 0,
+    STS_ERR_BAD_ARG = 1,            /* IllegalArgumentException (argument validation)      */
+    STS_ERR_ALL_NAN = 2,            /* IllegalArgumentException("Input is all NaNs!"),
+                                       S/UnivariateTimeSeries.scala:170-171                */
+    STS_ERR_UNSUPPORTED_METHOD = 3, /* UnsupportedOperationException, :148                  */
+    STS_ERR_HIP = 4,                /* device / runtime failure                             */
+    STS_ERR_REQUIREMENT = 5,        /* IllegalArgumentException("requirement failed: ..."),
+                                       :361 / :402                                          */
+    STS_ERR_NULL_DEST = 6,          /* NullPointerException (EWMAModel with dest = null,
+                                       S/models/EWMA.scala:125-127,135-136)                 */
+    STS_ERR_NOT_ENOUGH_DATA = 7,    /* commons-math3 MathIllegalArgumentException
+                                       NOT_ENOUGH_DATA_FOR_NUMBER_OF_PREDICTORS              */
+    STS_ERR_SINGULAR = 8,           /* commons-math3 SingularMatrixException                 */
+    STS_ERR_NO_DEVICE = 9           /* no gfx950 device visible                              */
+} sts_status;
+
+/* Fill methods of UnivariateTimeSeries.fillts (S/UnivariateTimeSeries.scala:141-150). */
+typedef enum sts_fill_method {
+    STS_FILL_NONE = -1,     /* identity (no imputation); fused kernels only */
+    STS_FILL_LINEAR = 0,    /* fillLinear   :247-266 */
+    STS_FILL_NEAREST = 1,   /* fillNearest  :156-184 */
+    STS_FILL_NEXT = 2,      /* fillNext     :214-224 */
+    STS_FILL_PREVIOUS = 3,  /* fillPrevious :194-204 */
+    STS_FILL_SPLINE = 4     /* fillSpline   :277-297 -- not on the device path: returns
+                               STS_ERR_UNSUPPORTED_METHOD (out of scope) */
+} sts_fill_method;
+
+/* ---- library / runtime ---- */
+int         sts_abi_version(void);
+/* Select the HIP device for the calling thread (idempotent). */
+int         sts_init(int device);
+/* Thread-local description of the last non-OK status on this thread. */
+const char* sts_last_error(void);
+/* Map a fillts method string ("linear", "nearest", "next", "previous", "spline")
+ * to sts_fill_method; returns -2 for anything else (the reference's
+ * UnsupportedOperationException, S/UnivariateTimeSeries.scala:148). */
+int         sts_fill_method_from_name(const char* name);
+/* Wait for all work this library queued on `stream`. */
+int         sts_stream_synchronize(void* stream);
+/* Measurement hooks (bench.py): while on, HIP events are recorded on the launch stream
+ * around every series-tile kernel launched by the calling thread; sts_profile_end waits
+ * for them and returns the summed kernel time and the number of launches. */
+int         sts_profile_begin(void);
+int         sts_profile_end(double* kernel_ms, int64_t* launches);
+
+/* ---- a1-a5: TimeSeriesRDD.fill(method) -> UnivariateTimeSeries.fillts
+ *      (S/TimeSeriesRDD.scala:180-182, S/UnivariateTimeSeries.scala:141-266).
+ * out must not alias in (the reference always fills a fresh copy, :157/:195/:215/:248).
+ * Bit-exact. */
+int sts_fill(const double* in, double* out, int64_t S, int64_t T, int64_t ld_in, int64_t ld_out,
+             int method, int32_t* err_per_series, void* stream);
+
+/* ---- a6: UnivariateTimeSeries.differencesAtLag(ts, dest, lag, startIndex)
+ *      (S/UnivariateTimeSeries.scala:356-376; the (ts, lag) wrapper :384-386 is start = lag).
+ * out == in (same pointer and ld) reproduces the reference's in-place (dest eq ts)
+ * semantics, where later elements read already-differenced values.  lag == 0
+ * leaves out untouched (:363-364).  start < lag -> STS_ERR_REQUIREMENT.  Bit-exact. */
+int sts_diff_at_lag(const double* in, double* out, int64_t S, int64_t T, int64_t ld_in,
+                    int64_t ld_out, int lag, int start, void* stream);
+
+/* ---- a7: UnivariateTimeSeries.lag(ts, maxLag, includeOriginal) -> Lag.lagMatTrimBoth
+ *      (S/UnivariateTimeSeries.scala:37-39, S/Lag.scala:62-77).
+ * Series s's (T - maxLag) x (maxLag + inc) column-major block is written at
+ * out + s * (T - maxLag) * (maxLag + inc), i.e. the panel form of TimeSeries.lags
+ * (S/TimeSeries.scala:50-73).  Bit-exact. */
+int sts_lag_matrix(const double* in, double* out, int64_t S, int64_t T, int64_t ld_in,
+                   int max_lag, int include_original, void* stream);
+
+/* ---- a8: UnivariateTimeSeries.autocorr(ts, numLags) (S/UnivariateTimeSeries.scala:68-93).
+ * acf[s*K + (i-1)] = lag-i sample autocorrelation, i = 1..K (K <= 63).  1e-10 relative. */
+int sts_autocorr(const double* in, int64_t S, int64_t T, int64_t ld, int K, double* acf,
+                 void* stream);
+
+/* ---- a9 / a10: EWMAModel.add/removeTimeDependentEffects (S/models/EWMA.scala:125-142).
+ * smoothing[s] is series s's model parameter (device array of S doubles).
+ * out == in is allowed for add (safe in the reference) and for remove (reproduces the
+ * reference's read-after-overwrite).  out == NULL -> STS_ERR_NULL_DEST.  Bit-exact. */
+int sts_ewma_add(const double* in, double* out, int64_t S, int64_t T, int64_t ld_in,
+                 int64_t ld_out, const double* smoothing, void* stream);
+int sts_ewma_remove(const double* in, double* out, int64_t S, int64_t T, int64_t ld_in,
+                    int64_t ld_out, const double* smoothing, void* stream);
+
+/* ---- a11: Autoregression.fitModel(ts, p, noIntercept) (S/models/Autoregression.scala:38-53).
+ * c[s] and coef[s*p + j] receive the model; 1 <= p <= 31.  T - p < p + 1 ->
+ * STS_ERR_NOT_ENOUGH_DATA.  1e-10 relative to a Householder-QR OLS. */
+int sts_ar_fit(const double* in, int64_t S, int64_t T, int64_t ld, int p, int no_intercept,
+               double* c, double* coef, int32_t* err_per_series, void* stream);
+
+/* ---- a12 / a13: ARModel.remove/addTimeDependentEffects (S/models/Autoregression.scala:60-88).
+ * out == in reproduces the reference's aliasing semantics.  Bit-exact. */
+int sts_ar_remove(const double* in, double* out, int64_t S, int64_t T, int64_t ld_in,
+                  int64_t ld_out, const double* c, const double* coef, int p, void* stream);
+int sts_ar_add(const double* in, double* out, int64_t S, int64_t T, int64_t ld_in,
+               int64_t ld_out, const double* c, const double* coef, int p, void* stream);
+
+/* ---- fused mapSeries pipelines (one pass over HBM; each returned output written once) ---- */
+
+/* C1/C3: fill(method) then autocorr(K) of the filled series.  filled may be NULL when
+ * method == STS_FILL_NONE. */
+int sts_fill_autocorr(const double* in, double* filled, int64_t S, int64_t T, int64_t ld_in,
+                      int64_t ld_out, int method, int K, double* acf, int32_t* err_per_series,
+                      void* stream);
+/* C2: fill(method) -> differencesAtLag(lag) -> EWMAModel(smoothing[s]).addTimeDependentEffects */
+int sts_fill_diff_ewma(const double* in, double* out, int64_t S, int64_t T, int64_t ld_in,
+                       int64_t ld_out, int method, int lag, const double* smoothing,
+                       int32_t* err_per_series, void* stream);
+/* C5: fill(method) -> lag(maxLag, includeOriginal); filled may be NULL (not returned). */
+int sts_fill_lag_matrix(const double* in, double* filled, double* lagmat, int64_t S, int64_t T,
+                        int64_t ld_in, int64_t ld_out, int method, int max_lag,
+                        int include_original, int32_t* err_per_series, void* stream);
+/* C4: Autoregression.fitModel(ts, p, noIntercept) -> model.removeTimeDependentEffects(ts) */
+int sts_ar_fit_remove(const double* in, double* out, int64_t S, int64_t T, int64_t ld_in,
+                      int64_t ld_out, int p, int no_intercept, double* c, double* coef,
+                      int32_t* err_per_series, void* stream);
+
+/* ---- synthetic panels: counter-based Philox4x32-10, bit-identical
+ * to the CPU generator in oracle/, so any shard can be regenerated anywhere. ---- */
+int sts_gen_panel(double* out, int64_t s0, int64_t S, int64_t T, int64_t ld, uint64_t seed,
+                  double nan_p, void* stream);
+int sts_gen_ar_panel(double* out, double* c, double* phi, int64_t s0, int64_t S, int64_t T,
+                     int64_t ld, uint64_t seed, int p, void* stream);
+
+/* ---- host-buffer variants (JNI path): stage host arrays through HBM on the calling
+ * thread's stream; err_per_series, c, coef, acf are host arrays.  Return after the
+ * results are back on the host. ---- */
+int sts_fill_host(const double* in, double* out, int64_t S, int64_t T, int64_t ld, int method,
+                  int32_t* err_per_series);
+int sts_autocorr_host(const double* in, int64_t S, int64_t T, int64_t ld, int K, double* acf);
+int sts_diff_at_lag_host(const double* in, double* out, int64_t S, int64_t T, int64_t ld,
+                         int lag, int start);
+int sts_lag_matrix_host(const double* in, double* out, int64_t S, int64_t T, int64_t ld,
+                        int max_lag, int include_original);
+int sts_ewma_add_host(const double* in, double* out, int64_t S, int64_t T, int64_t ld,
+                      const double* smoothing);
+int sts_ewma_remove_host(const double* in, double* out, int64_t S, int64_t T, int64_t ld,
+                         const double* smoothing);
+int sts_ar_fit_host(const double* in, int64_t S, int64_t T, int64_t ld, int p, int no_intercept,
+                    double* c, double* coef, int32_t* err_per_series);
+int sts_ar_remove_host(const double* in, double* out, int64_t S, int64_t T, int64_t ld,
+                       const double* c, const double* coef, int p);
+int sts_ar_add_host(const double* in, double* out, int64_t S, int64_t T, int64_t ld,
+                    const double* c, const double* coef, int p);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* STS_H */

@@ -1,0 +1,528 @@
+// sts_api.cpp -- the C ABI (include/sts.h): argument validation with the reference's
+// error semantics, stream/workspace handling, kernel dispatch, host-buffer staging.
+//
+// Reentrancy: no mutable global state after first use except the per-device
+// memory-pool setup (guarded by std::call_once); every call runs on the caller's
+// stream (NULL -> hipStreamPerThread) and allocates its scratch stream-ordered
+// (hipMallocAsync / hipFreeAsync), so Spark's N executor threads can call
+// concurrently.  Errors are reported through a thread-local message.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "sts_internal.hpp"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int status, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return status;
+}
+
+int hip_fail(hipError_t e, const char* where) {
+    return fail(STS_ERR_HIP, "%s: %s", where, hipGetErrorString(e));
+}
+
+#define HIP_TRY(call, where)                       \
+    do {                                           \
+        hipError_t e_ = (call);                    \
+        if (e_ != hipSuccess) return hip_fail(e_, where); \
+    } while (0)
+
+hipStream_t as_stream(void* s) { return s ? reinterpret_cast<hipStream_t>(s) : hipStreamPerThread; }
+
+std::once_flag g_pool_once[64];
+
+int ensure_device() {
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return hip_fail(e, "hipGetDevice");
+    int n = 0;
+    e = hipGetDeviceCount(&n);
+    if (e != hipSuccess || n == 0) return fail(STS_ERR_NO_DEVICE, "no HIP device visible");
+    if (dev >= 0 && dev < 64) {
+        std::call_once(g_pool_once[dev], [dev] {
+            hipMemPool_t pool;
+            if (hipDeviceGetDefaultMemPool(&pool, dev) == hipSuccess) {
+                uint64_t thr = UINT64_MAX;
+                (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &thr);
+            }
+        });
+    }
+    return STS_OK;
+}
+
+// stream-ordered scratch
+struct Scratch {
+    void* p = nullptr;
+    hipStream_t st;
+    explicit Scratch(hipStream_t s) : st(s) {}
+    hipError_t alloc(size_t bytes) { return hipMallocAsync(&p, bytes ? bytes : 16, st); }
+    ~Scratch() {
+        if (p) (void)hipFreeAsync(p, st);
+    }
+};
+
+int check_panel(const void* in, int64_t S, int64_t T, int64_t ld, const char* name) {
+    if (S < 0 || T < 0) return fail(STS_ERR_BAD_ARG, "%s: negative panel shape (S=%lld, T=%lld)", name,
+                                    (long long)S, (long long)T);
+    if (T > 0x7fffffffLL) return fail(STS_ERR_BAD_ARG, "%s: T=%lld exceeds the reference's Int index range",
+                                      name, (long long)T);
+    if (ld < T) return fail(STS_ERR_BAD_ARG, "%s: leading dimension %lld < T=%lld", name, (long long)ld,
+                            (long long)T);
+    if (S * T > 0 && !in) return fail(STS_ERR_BAD_ARG, "%s: null panel pointer", name);
+    return STS_OK;
+}
+
+// err handling: caller array (async) or internal buffer checked synchronously
+struct ErrSink {
+    int32_t* dev = nullptr;
+    bool owned = false;
+    Scratch scratch;
+    int64_t S;
+    ErrSink(int32_t* user, int64_t S_, hipStream_t st) : dev(user), scratch(st), S(S_) {}
+    int prepare() {
+        if (!dev) {
+            hipError_t e = scratch.alloc((size_t)(S > 0 ? S : 1) * sizeof(int32_t));
+            if (e != hipSuccess) return hip_fail(e, "hipMallocAsync(err)");
+            dev = static_cast<int32_t*>(scratch.p);
+            owned = true;
+        }
+        if (S > 0) {
+            hipError_t e = hipMemsetAsync(dev, 0, (size_t)S * sizeof(int32_t), scratch.st);
+            if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync(err)");
+        }
+        return STS_OK;
+    }
+    // for the internal buffer: wait and turn the first failing series into a status
+    int finish(const char* what) {
+        if (!owned || S == 0) return STS_OK;
+        std::vector<int32_t> h((size_t)S);
+        hipError_t e = hipMemcpyAsync(h.data(), dev, (size_t)S * sizeof(int32_t), hipMemcpyDeviceToHost, scratch.st);
+        if (e == hipSuccess) e = hipStreamSynchronize(scratch.st);
+        if (e != hipSuccess) return hip_fail(e, what);
+        for (int64_t s = 0; s < S; s++) {
+            if (h[(size_t)s] == STS_ERR_ALL_NAN) return fail(STS_ERR_ALL_NAN, "Input is all NaNs! (series %lld)", (long long)s);
+            if (h[(size_t)s] == STS_ERR_SINGULAR) return fail(STS_ERR_SINGULAR, "singular AR design matrix (series %lld)", (long long)s);
+            if (h[(size_t)s] != 0) return fail(h[(size_t)s], "%s failed for series %lld", what, (long long)s);
+        }
+        return STS_OK;
+    }
+};
+
+int method_ok(int method, bool allow_none, const char* name) {
+    if (method == STS_FILL_SPLINE)
+        return fail(STS_ERR_UNSUPPORTED_METHOD,
+                    "%s: fill method \"spline\" (commons-math3 SplineInterpolator) is not on the device path", name);
+    if (method < (allow_none ? STS_FILL_NONE : STS_FILL_LINEAR) || method > STS_FILL_PREVIOUS)
+        return fail(STS_ERR_UNSUPPORTED_METHOD, "%s: unsupported fill method %d", name, method);
+    return STS_OK;
+}
+
+int tile_width(int64_t T) { return T <= 512 ? 512 : 4096; }
+
+// Measurement hook (bench.py): HIP events recorded on the launch stream around every
+// tile-kernel launch of this thread while profiling is on.
+struct ProfileState {
+    bool on = false;
+    std::vector<hipEvent_t> pool;
+    size_t used = 0;
+};
+thread_local ProfileState g_prof;
+
+void prof_mark(hipStream_t st) {
+    if (!g_prof.on) return;
+    if (g_prof.used == g_prof.pool.size()) {
+        hipEvent_t e;
+        if (hipEventCreate(&e) != hipSuccess) return;
+        g_prof.pool.push_back(e);
+    }
+    (void)hipEventRecord(g_prof.pool[g_prof.used++], st);
+}
+
+// fill (+ optional ACF partials / lag matrix) through the tile kernel
+int run_tile(const double* in, double* out, double* lagmat, int64_t S, int64_t T, int64_t ld_in, int64_t ld_out,
+             int method, int K, double* acf, int max_lag, int inc, int32_t* err, hipStream_t st, const char* name) {
+    if (S == 0 || T == 0) return STS_OK;
+    const int tw = (K > 0) ? 4096 : tile_width(T);
+    sts::TileArgs a{};
+    a.in = in;
+    a.out = out;
+    a.lagmat = lagmat;
+    a.err = err;
+    a.S = S;
+    a.T = T;
+    a.ld_in = ld_in;
+    a.ld_out = ld_out;
+    a.tiles_per_series = (T + tw - 1) / tw;
+    a.K = K;
+    a.max_lag = max_lag;
+    a.include_original = inc;
+    if (S * a.tiles_per_series > 0x7fffffffLL) return fail(STS_ERR_BAD_ARG, "%s: panel too large for one launch", name);
+    Scratch part(st);
+    if (K > 0) {
+        hipError_t e = part.alloc((size_t)(S * a.tiles_per_series) * sts::kPartStride * sizeof(double));
+        if (e != hipSuccess) return hip_fail(e, "hipMallocAsync(partials)");
+        a.partials = static_cast<double*>(part.p);
+    }
+    prof_mark(st);
+    hipError_t e = sts::launch_tile(method, tw, a, st);
+    prof_mark(st);
+    if (e != hipSuccess) return hip_fail(e, name);
+    if (K > 0) {
+        sts::FinalizeArgs f{};
+        f.F = out ? out : in;
+        f.partials = a.partials;
+        f.acf = acf;
+        f.S = S;
+        f.T = T;
+        f.ldF = out ? ld_out : ld_in;
+        f.tiles_per_series = a.tiles_per_series;
+        f.K = K;
+        e = sts::launch_acf_finalize(f, st);
+        if (e != hipSuccess) return hip_fail(e, "acf finalize");
+    }
+    return STS_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int sts_abi_version(void) { return STS_ABI_VERSION; }
+
+int sts_init(int device) {
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess || n == 0) return fail(STS_ERR_NO_DEVICE, "no HIP device visible");
+    if (device < 0 || device >= n) return fail(STS_ERR_BAD_ARG, "device %d out of range (%d devices)", device, n);
+    HIP_TRY(hipSetDevice(device), "hipSetDevice");
+    hipDeviceProp_t prop;
+    HIP_TRY(hipGetDeviceProperties(&prop, device), "hipGetDeviceProperties");
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+        return fail(STS_ERR_NO_DEVICE, "device %d is %s; this library is built for gfx950 only", device, prop.gcnArchName);
+    return ensure_device();
+}
+
+const char* sts_last_error(void) { return g_err.c_str(); }
+
+int sts_fill_method_from_name(const char* name) {
+    if (!name) return -2;
+    if (!std::strcmp(name, "linear")) return STS_FILL_LINEAR;
+    if (!std::strcmp(name, "nearest")) return STS_FILL_NEAREST;
+    if (!std::strcmp(name, "next")) return STS_FILL_NEXT;
+    if (!std::strcmp(name, "previous")) return STS_FILL_PREVIOUS;
+    if (!std::strcmp(name, "spline")) return STS_FILL_SPLINE;
+    return -2;
+}
+
+int sts_profile_begin(void) {
+    g_prof.on = true;
+    g_prof.used = 0;
+    return STS_OK;
+}
+
+int sts_profile_end(double* kernel_ms, int64_t* launches) {
+    g_prof.on = false;
+    double total = 0.0;
+    int64_t n = 0;
+    for (size_t i = 0; i + 1 < g_prof.used; i += 2) {
+        HIP_TRY(hipEventSynchronize(g_prof.pool[i + 1]), "hipEventSynchronize");
+        float ms = 0.f;
+        HIP_TRY(hipEventElapsedTime(&ms, g_prof.pool[i], g_prof.pool[i + 1]), "hipEventElapsedTime");
+        total += ms;
+        n++;
+    }
+    g_prof.used = 0;
+    if (kernel_ms) *kernel_ms = total;
+    if (launches) *launches = n;
+    return STS_OK;
+}
+
+int sts_stream_synchronize(void* stream) {
+    HIP_TRY(hipStreamSynchronize(as_stream(stream)), "hipStreamSynchronize");
+    return STS_OK;
+}
+
+int sts_fill(const double* in, double* out, int64_t S, int64_t T, int64_t ld_in, int64_t ld_out, int method,
+             int32_t* err_per_series, void* stream) {
+    int r;
+    if ((r = method_ok(method, false, "fill"))) return r;
+    if ((r = check_panel(in, S, T, ld_in, "fill"))) return r;
+    if ((r = check_panel(out, S, T, ld_out, "fill"))) return r;
+    if (S * T > 0 && in == out) return fail(STS_ERR_BAD_ARG, "fill: out must not alias in (fillts returns a new vector)");
+    if ((r = ensure_device())) return r;
+    hipStream_t st = as_stream(stream);
+    ErrSink es(err_per_series, S, st);
+    if ((r = es.prepare())) return r;
+    if ((r = run_tile(in, out, nullptr, S, T, ld_in, ld_out, method, 0, nullptr, 0, 0, es.dev, st, "fill"))) return r;
+    return es.finish("fill");
+}
+
+int sts_fill_autocorr(const double* in, double* filled, int64_t S, int64_t T, int64_t ld_in, int64_t ld_out,
+                      int method, int K, double* acf, int32_t* err_per_series, void* stream) {
+    int r;
+    if ((r = method_ok(method, true, "fill_autocorr"))) return r;
+    if ((r = check_panel(in, S, T, ld_in, "fill_autocorr"))) return r;
+    if (method != STS_FILL_NONE) {
+        if ((r = check_panel(filled, S, T, ld_out, "fill_autocorr"))) return r;
+        if (S * T > 0 && in == filled) return fail(STS_ERR_BAD_ARG, "fill_autocorr: filled must not alias in");
+    } else if (filled) {
+        return fail(STS_ERR_BAD_ARG, "fill_autocorr: filled must be NULL for STS_FILL_NONE");
+    }
+    if (K < 0 || K > 63) return fail(STS_ERR_BAD_ARG, "autocorr: numLags %d outside [0, 63]", K);
+    if (S > 0 && K > 0 && !acf) return fail(STS_ERR_BAD_ARG, "autocorr: null output");
+    if ((r = ensure_device())) return r;
+    hipStream_t st = as_stream(stream);
+    ErrSink es(err_per_series, S, st);
+    if ((r = es.prepare())) return r;
+    if (T == 0 && S > 0 && K > 0) {
+        std::vector<double> nan((size_t)(S * K), NAN);
+        HIP_TRY(hipMemcpyAsync(acf, nan.data(), nan.size() * sizeof(double), hipMemcpyHostToDevice, st), "acf");
+        HIP_TRY(hipStreamSynchronize(st), "acf");
+        return es.finish("fill_autocorr");
+    }
+    if (K == 0) {
+        if (method != STS_FILL_NONE && (r = run_tile(in, filled, nullptr, S, T, ld_in, ld_out, method, 0, nullptr, 0, 0,
+                                                    es.dev, st, "fill"))) return r;
+        return es.finish("fill_autocorr");
+    }
+    if ((r = run_tile(in, method == STS_FILL_NONE ? nullptr : filled, nullptr, S, T, ld_in, ld_out, method, K, acf, 0,
+                      0, es.dev, st, "fill_autocorr"))) return r;
+    return es.finish("fill_autocorr");
+}
+
+int sts_autocorr(const double* in, int64_t S, int64_t T, int64_t ld, int K, double* acf, void* stream) {
+    return sts_fill_autocorr(in, nullptr, S, T, ld, ld, STS_FILL_NONE, K, acf, nullptr, stream);
+}
+
+int sts_diff_at_lag(const double* in, double* out, int64_t S, int64_t T, int64_t ld_in, int64_t ld_out, int lag,
+                    int start, void* stream) {
+    int r;
+    if (!(start >= lag)) return fail(STS_ERR_REQUIREMENT, "requirement failed: starting index cannot be less than lag");
+    if (lag < 0) return fail(STS_ERR_BAD_ARG, "differencesAtLag: negative lag %d", lag);
+    if ((r = check_panel(in, S, T, ld_in, "differencesAtLag"))) return r;
+    if ((r = check_panel(out, S, T, ld_out, "differencesAtLag"))) return r;
+    if (lag == 0 || S * T == 0) return STS_OK;  // dest returned untouched (:363-364)
+    if ((r = ensure_device())) return r;
+    hipStream_t st = as_stream(stream);
+    if (in == out) {
+        if (ld_in != ld_out) return fail(STS_ERR_BAD_ARG, "differencesAtLag: in-place call with different ld");
+        HIP_TRY(sts::launch_diff_inplace(out, S, T, ld_out, lag, start, st), "differencesAtLag(in place)");
+    } else {
+        HIP_TRY(sts::launch_diff(in, out, S, T, ld_in, ld_out, lag, start, st), "differencesAtLag");
+    }
+    return STS_OK;
+}
+
+int sts_lag_matrix(const double* in, double* out, int64_t S, int64_t T, int64_t ld_in, int max_lag,
+                   int include_original, void* stream) {
+    int r;
+    if ((r = check_panel(in, S, T, ld_in, "lag"))) return r;
+    if (max_lag < 0 || max_lag > T) return fail(STS_ERR_BAD_ARG, "lag: maxLag %d outside [0, T=%lld]", max_lag, (long long)T);
+    const int64_t n = S * (T - max_lag) * (max_lag + (include_original ? 1 : 0));
+    if (n > 0 && !out) return fail(STS_ERR_BAD_ARG, "lag: null output");
+    if (n == 0) return STS_OK;
+    if ((r = ensure_device())) return r;
+    HIP_TRY(sts::launch_lagmat(in, out, S, T, ld_in, max_lag, include_original, as_stream(stream)), "lag");
+    return STS_OK;
+}
+
+int sts_fill_lag_matrix(const double* in, double* filled, double* lagmat, int64_t S, int64_t T, int64_t ld_in,
+                        int64_t ld_out, int method, int max_lag, int include_original, int32_t* err_per_series,
+                        void* stream) {
+    int r;
+    if ((r = method_ok(method, true, "fill_lag_matrix"))) return r;
+    if ((r = check_panel(in, S, T, ld_in, "fill_lag_matrix"))) return r;
+    if (filled && (r = check_panel(filled, S, T, ld_out, "fill_lag_matrix"))) return r;
+    if (filled && S * T > 0 && filled == in) return fail(STS_ERR_BAD_ARG, "fill_lag_matrix: filled must not alias in");
+    if (max_lag < 0 || max_lag > T) return fail(STS_ERR_BAD_ARG, "lag: maxLag %d outside [0, T=%lld]", max_lag, (long long)T);
+    const int64_t n = S * (T - max_lag) * (max_lag + (include_original ? 1 : 0));
+    if (n > 0 && !lagmat) return fail(STS_ERR_BAD_ARG, "lag: null output");
+    if ((r = ensure_device())) return r;
+    hipStream_t st = as_stream(stream);
+    ErrSink es(err_per_series, S, st);
+    if ((r = es.prepare())) return r;
+    if ((r = run_tile(in, filled, n > 0 ? lagmat : nullptr, S, T, ld_in, ld_out, method, 0, nullptr, max_lag,
+                      include_original ? 1 : 0, es.dev, st, "fill_lag_matrix"))) return r;
+    return es.finish("fill_lag_matrix");
+}
+
+int sts_ewma_add(const double* in, double* out, int64_t S, int64_t T, int64_t ld_in, int64_t ld_out,
+                 const double* smoothing, void* stream) {
+    int r;
+    if (!out) return fail(STS_ERR_NULL_DEST, "EWMAModel.addTimeDependentEffects: dest is null (NullPointerException)");
+    if ((r = check_panel(in, S, T, ld_in, "ewma_add"))) return r;
+    if ((r = check_panel(out, S, T, ld_out, "ewma_add"))) return r;
+    if (S > 0 && !smoothing) return fail(STS_ERR_BAD_ARG, "ewma_add: null smoothing");
+    if (S * T == 0) return STS_OK;
+    if ((r = ensure_device())) return r;
+    sts::RecurArgs a{};
+    a.in = in; a.out = out; a.S = S; a.T = T; a.ld_in = ld_in; a.ld_out = ld_out; a.sm = smoothing;
+    HIP_TRY(sts::launch_recur(sts::kEwmaAdd, a, as_stream(stream)), "ewma_add");
+    return STS_OK;
+}
+
+int sts_ewma_remove(const double* in, double* out, int64_t S, int64_t T, int64_t ld_in, int64_t ld_out,
+                    const double* smoothing, void* stream) {
+    int r;
+    if (!out) return fail(STS_ERR_NULL_DEST, "EWMAModel.removeTimeDependentEffects: dest is null (NullPointerException)");
+    if ((r = check_panel(in, S, T, ld_in, "ewma_remove"))) return r;
+    if ((r = check_panel(out, S, T, ld_out, "ewma_remove"))) return r;
+    if (S > 0 && !smoothing) return fail(STS_ERR_BAD_ARG, "ewma_remove: null smoothing");
+    if (S * T == 0) return STS_OK;
+    if ((r = ensure_device())) return r;
+    hipStream_t st = as_stream(stream);
+    if (in == out) {
+        sts::RecurArgs a{};
+        a.in = in; a.out = out; a.S = S; a.T = T; a.ld_in = ld_in; a.ld_out = ld_out; a.sm = smoothing;
+        HIP_TRY(sts::launch_recur(sts::kEwmaRemoveInplace, a, st), "ewma_remove(in place)");
+    } else {
+        HIP_TRY(sts::launch_ewma_remove(in, out, S, T, ld_in, ld_out, smoothing, st), "ewma_remove");
+    }
+    return STS_OK;
+}
+
+int sts_ar_remove(const double* in, double* out, int64_t S, int64_t T, int64_t ld_in, int64_t ld_out,
+                  const double* c, const double* coef, int p, void* stream) {
+    int r;
+    if ((r = check_panel(in, S, T, ld_in, "ar_remove"))) return r;
+    if ((r = check_panel(out, S, T, ld_out, "ar_remove"))) return r;
+    if (p < 0) return fail(STS_ERR_BAD_ARG, "ar_remove: negative order");
+    if (S > 0 && (!c || (p > 0 && !coef))) return fail(STS_ERR_BAD_ARG, "ar_remove: null model");
+    if (S * T == 0) return STS_OK;
+    if ((r = ensure_device())) return r;
+    hipStream_t st = as_stream(stream);
+    if (in == out) {
+        sts::RecurArgs a{};
+        a.in = in; a.out = out; a.S = S; a.T = T; a.ld_in = ld_in; a.ld_out = ld_out; a.c = c; a.coef = coef; a.p = p;
+        HIP_TRY(sts::launch_recur(sts::kArRemoveInplace, a, st), "ar_remove(in place)");
+    } else {
+        HIP_TRY(sts::launch_ar_remove(in, out, S, T, ld_in, ld_out, c, coef, p, st), "ar_remove");
+    }
+    return STS_OK;
+}
+
+int sts_ar_add(const double* in, double* out, int64_t S, int64_t T, int64_t ld_in, int64_t ld_out, const double* c,
+               const double* coef, int p, void* stream) {
+    int r;
+    if ((r = check_panel(in, S, T, ld_in, "ar_add"))) return r;
+    if ((r = check_panel(out, S, T, ld_out, "ar_add"))) return r;
+    if (p < 0) return fail(STS_ERR_BAD_ARG, "ar_add: negative order");
+    if (S > 0 && (!c || (p > 0 && !coef))) return fail(STS_ERR_BAD_ARG, "ar_add: null model");
+    if (S * T == 0) return STS_OK;
+    if ((r = ensure_device())) return r;
+    sts::RecurArgs a{};
+    a.in = in; a.out = out; a.S = S; a.T = T; a.ld_in = ld_in; a.ld_out = ld_out; a.c = c; a.coef = coef; a.p = p;
+    HIP_TRY(sts::launch_recur(sts::kArAdd, a, as_stream(stream)), "ar_add");
+    return STS_OK;
+}
+
+static int ar_fit_common(const double* in, double* out, int64_t S, int64_t T, int64_t ld_in, int64_t ld_out, int p,
+                         int no_intercept, double* c, double* coef, int32_t* err_per_series, void* stream,
+                         const char* name) {
+    int r;
+    if ((r = check_panel(in, S, T, ld_in, name))) return r;
+    if (out && (r = check_panel(out, S, T, ld_out, name))) return r;
+    if (p < 1 || p > 31) return fail(STS_ERR_BAD_ARG, "%s: AR order %d outside [1, 31]", name, p);
+    if (T - p < (int64_t)p + 1)
+        return fail(STS_ERR_NOT_ENOUGH_DATA, "%s: not enough data (%lld rows) for the number of predictors (%d)", name,
+                    (long long)(T - p), p);
+    if (S > 0 && (!c || !coef)) return fail(STS_ERR_BAD_ARG, "%s: null model output", name);
+    if (out && in == out) return fail(STS_ERR_BAD_ARG, "%s: out must not alias in", name);
+    if (S == 0) return STS_OK;
+    if ((r = ensure_device())) return r;
+    hipStream_t st = as_stream(stream);
+    ErrSink es(err_per_series, S, st);
+    if ((r = es.prepare())) return r;
+    sts::ArArgs a{};
+    a.in = in; a.out = out; a.c = c; a.coef = coef; a.err = es.dev;
+    a.S = S; a.T = T; a.ld_in = ld_in; a.ld_out = ld_out; a.p = p; a.no_intercept = no_intercept ? 1 : 0;
+    HIP_TRY(sts::launch_ar_fit(a, st), name);
+    return es.finish(name);
+}
+
+int sts_ar_fit(const double* in, int64_t S, int64_t T, int64_t ld, int p, int no_intercept, double* c, double* coef,
+               int32_t* err_per_series, void* stream) {
+    return ar_fit_common(in, nullptr, S, T, ld, ld, p, no_intercept, c, coef, err_per_series, stream, "ar_fit");
+}
+
+int sts_ar_fit_remove(const double* in, double* out, int64_t S, int64_t T, int64_t ld_in, int64_t ld_out, int p,
+                      int no_intercept, double* c, double* coef, int32_t* err_per_series, void* stream) {
+    if (!out) return fail(STS_ERR_BAD_ARG, "ar_fit_remove: null output");
+    return ar_fit_common(in, out, S, T, ld_in, ld_out, p, no_intercept, c, coef, err_per_series, stream,
+                         "ar_fit_remove");
+}
+
+int sts_fill_diff_ewma(const double* in, double* out, int64_t S, int64_t T, int64_t ld_in, int64_t ld_out, int method,
+                       int lag, const double* smoothing, int32_t* err_per_series, void* stream) {
+    int r;
+    if ((r = method_ok(method, true, "fill_diff_ewma"))) return r;
+    if ((r = check_panel(in, S, T, ld_in, "fill_diff_ewma"))) return r;
+    if ((r = check_panel(out, S, T, ld_out, "fill_diff_ewma"))) return r;
+    if (lag < 0) return fail(STS_ERR_BAD_ARG, "fill_diff_ewma: negative lag");
+    if (S > 0 && !smoothing) return fail(STS_ERR_BAD_ARG, "fill_diff_ewma: null smoothing");
+    if (S * T > 0 && in == out) return fail(STS_ERR_BAD_ARG, "fill_diff_ewma: out must not alias in");
+    if (S * T == 0) return STS_OK;
+    if ((r = ensure_device())) return r;
+    hipStream_t st = as_stream(stream);
+    ErrSink es(err_per_series, S, st);
+    if ((r = es.prepare())) return r;
+    if ((method == STS_FILL_PREVIOUS || method == STS_FILL_NONE) && lag >= 1 && lag <= 32 && method == STS_FILL_PREVIOUS) {
+        sts::RecurArgs a{};
+        a.in = in; a.out = out; a.S = S; a.T = T; a.ld_in = ld_in; a.ld_out = ld_out; a.sm = smoothing;
+        a.lag = lag; a.start = lag; a.method = method;
+        HIP_TRY(sts::launch_recur(sts::kFillDiffEwma, a, st), "fill_diff_ewma");
+        return es.finish("fill_diff_ewma");
+    }
+    // general composition: fill -> (in place) differences -> (in place) EWMA add, all on `out`
+    if (method != STS_FILL_NONE) {
+        if ((r = run_tile(in, out, nullptr, S, T, ld_in, ld_out, method, 0, nullptr, 0, 0, es.dev, st, "fill"))) return r;
+    } else {
+        HIP_TRY(hipMemcpy2DAsync(out, ld_out * sizeof(double), in, ld_in * sizeof(double), T * sizeof(double), S,
+                                 hipMemcpyDeviceToDevice, st), "copy");
+    }
+    if (lag > 0) HIP_TRY(sts::launch_diff_inplace(out, S, T, ld_out, lag, lag, st), "differencesAtLag");
+    sts::RecurArgs a{};
+    a.in = out; a.out = out; a.S = S; a.T = T; a.ld_in = ld_out; a.ld_out = ld_out; a.sm = smoothing;
+    HIP_TRY(sts::launch_recur(sts::kEwmaAdd, a, st), "ewma_add");
+    return es.finish("fill_diff_ewma");
+}
+
+int sts_gen_panel(double* out, int64_t s0, int64_t S, int64_t T, int64_t ld, uint64_t seed, double nan_p,
+                  void* stream) {
+    int r;
+    if ((r = check_panel(out, S, T, ld, "gen_panel"))) return r;
+    if ((r = ensure_device())) return r;
+    uint32_t thr = 0;
+    if (nan_p >= 1.0) thr = 0xFFFFFFFFu;
+    else if (nan_p > 0.0) thr = (uint32_t)std::floor(nan_p * 4294967296.0);
+    HIP_TRY(sts::launch_gen_panel(out, s0, S, T, ld, seed, thr, as_stream(stream)), "gen_panel");
+    return STS_OK;
+}
+
+int sts_gen_ar_panel(double* out, double* c, double* phi, int64_t s0, int64_t S, int64_t T, int64_t ld, uint64_t seed,
+                     int p, void* stream) {
+    int r;
+    if ((r = check_panel(out, S, T, ld, "gen_ar_panel"))) return r;
+    if (p < 1 || p > 32) return fail(STS_ERR_BAD_ARG, "gen_ar_panel: order %d outside [1, 32]", p);
+    if (S > 0 && (!c || !phi)) return fail(STS_ERR_BAD_ARG, "gen_ar_panel: null parameter outputs");
+    if ((r = ensure_device())) return r;
+    HIP_TRY(sts::launch_gen_ar(out, c, phi, s0, S, T, ld, seed, p, as_stream(stream)), "gen_ar_panel");
+    return STS_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,90 @@
+// sts_internal.hpp -- shared declarations between the C-ABI layer (sts_api.cpp) and
+// the HIP kernel translation units.  Host-side launchers only: no kernel bodies here.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "sts.h"
+
+namespace sts {
+
+// Tile geometry of the imputation / autocorrelation tile kernel (sts_tile.hip).
+// A tile is TW consecutive steps of ONE series plus HB steps of look-back and HA
+// steps of look-ahead (ACF pairs reach 16*NT-1 <= 79 steps past the tile).
+constexpr int kHB = 64;
+constexpr int kHA = 128;
+constexpr int kPartStride = 66;  // per-tile partials: lags 0..63, sum(y), pad
+
+struct TileArgs {
+    const double* in;
+    double* out;          // filled output (may be null when not written)
+    double* lagmat;       // lag-matrix output (may be null)
+    double* partials;     // ACF partial sums [tiles][kPartStride] (may be null)
+    int32_t* err;         // per-series error flags (may be null)
+    int64_t S, T, ld_in, ld_out;
+    int64_t tiles_per_series;
+    int K;                // ACF lags (0 = no ACF)
+    int max_lag;          // lag matrix p
+    int include_original; // lag matrix inc
+};
+
+struct FinalizeArgs {
+    const double* F;      // filled series (or raw input when no fill), ld = ldF
+    const double* partials;
+    double* acf;          // S x K
+    int64_t S, T, ldF, tiles_per_series;
+    int K;
+};
+
+// launchers (return hipError_t of the launch)
+hipError_t launch_tile(int method, int tw, const TileArgs& a, hipStream_t st);
+hipError_t launch_acf_finalize(const FinalizeArgs& a, hipStream_t st);
+
+hipError_t launch_diff(const double* in, double* out, int64_t S, int64_t T, int64_t ld_in,
+                       int64_t ld_out, int lag, int start, hipStream_t st);
+hipError_t launch_diff_inplace(double* x, int64_t S, int64_t T, int64_t ld, int lag, int start,
+                               hipStream_t st);
+hipError_t launch_lagmat(const double* in, double* out, int64_t S, int64_t T, int64_t ld_in,
+                         int max_lag, int include_original, hipStream_t st);
+hipError_t launch_ewma_remove(const double* in, double* out, int64_t S, int64_t T, int64_t ld_in,
+                              int64_t ld_out, const double* sm, hipStream_t st);
+hipError_t launch_ar_remove(const double* in, double* out, int64_t S, int64_t T, int64_t ld_in,
+                            int64_t ld_out, const double* c, const double* coef, int p,
+                            hipStream_t st);
+
+// series-per-lane recurrences (sts_recur.hip)
+enum RecurOp { kEwmaAdd = 0, kEwmaRemoveInplace = 1, kArAdd = 2, kArRemoveInplace = 3,
+               kFillDiffEwma = 4, kDiffInplace = 5 };
+struct RecurArgs {
+    const double* in;
+    double* out;
+    int64_t S, T, ld_in, ld_out;
+    const double* sm;     // EWMA smoothing per series
+    const double* c;      // AR intercept per series
+    const double* coef;   // AR coefficients [S][p]
+    int p;                // AR order
+    int lag, start;       // differencing
+    int method;           // fill method for kFillDiffEwma
+};
+hipError_t launch_recur(RecurOp op, const RecurArgs& a, hipStream_t st);
+
+// AR fit (sts_ar.hip)
+struct ArArgs {
+    const double* in;
+    double* out;          // remove output (null -> fit only)
+    double* c;
+    double* coef;
+    int32_t* err;
+    int64_t S, T, ld_in, ld_out;
+    int p, no_intercept;
+};
+hipError_t launch_ar_fit(const ArArgs& a, hipStream_t st);
+
+// generators (sts_gen.hip)
+hipError_t launch_gen_panel(double* out, int64_t s0, int64_t S, int64_t T, int64_t ld,
+                            uint64_t seed, uint32_t nan_thr, hipStream_t st);
+hipError_t launch_gen_ar(double* out, double* c, double* phi, int64_t s0, int64_t S, int64_t T,
+                         int64_t ld, uint64_t seed, int p, hipStream_t st);
+
+}  // namespace sts

@@ -1,0 +1,216 @@
+// sts_recur.hip -- first-order and p-th order recurrences along time, one LANE per
+// series, bit-exact by construction (the reference's own sequential order):
+//   EWMAModel.addTimeDependentEffects     S/models/EWMA.scala:135-142
+//   EWMAModel.removeTimeDependentEffects  S/models/EWMA.scala:125-133 (dest eq ts)
+//   ARModel.addTimeDependentEffects       S/models/Autoregression.scala:75-88 (IIR)
+//   ARModel.removeTimeDependentEffects    S/models/Autoregression.scala:60-73 (dest eq ts)
+//   differencesAtLag                      S/UnivariateTimeSeries.scala:356-376 (dest eq ts)
+//   C2 pipeline fillPrevious -> differencesAtLag(lag) -> EWMA add, fused (one HBM pass)
+//
+// A wave owns 64 series.  Time is processed in chunks of kCH steps: the wave loads a
+// 64 x kCH block through LDS (each load instruction covers 2 series x 256 contiguous
+// bytes, so HBM sees whole lines), transposes it (row stride kCH+1 doubles: the
+// per-lane row reads hit 64 distinct banks), runs each lane's recurrence over the
+// chunk in registers, and stores the block back the same way.
+#include "sts_internal.hpp"
+
+#include <hip/hip_runtime.h>
+
+namespace sts {
+namespace {
+
+constexpr int kCH = 32;
+constexpr int kRow = kCH + 1;
+
+template <int OP, int H>
+__global__ __launch_bounds__(64) void recur_kernel(RecurArgs a) {
+    __shared__ double tile[64 * kRow];
+    const int lane = threadIdx.x;
+    const int64_t s0 = (int64_t)blockIdx.x * 64;
+    const int64_t sl = s0 + lane;                 // this lane's series
+    const bool live = sl < a.S;
+    const int ns = (a.S - s0 < 64) ? (int)(a.S - s0) : 64;
+    const int64_t T = a.T;
+
+    // per-series parameters
+    double sm = 0.0, oms = 0.0, cc = 0.0;
+    double cf[H];
+#pragma unroll
+    for (int j = 0; j < H; j++) cf[j] = 0.0;
+    const int hp = (OP == kArAdd || OP == kArRemoveInplace) ? a.p : a.lag;  // history length used
+    if (live) {
+        if (OP == kEwmaAdd || OP == kEwmaRemoveInplace || OP == kFillDiffEwma) {
+            sm = a.sm[sl];
+            oms = 1.0 - sm;
+        }
+        if (OP == kArAdd || OP == kArRemoveInplace) {
+            cc = a.c[sl];
+#pragma unroll
+            for (int j = 0; j < H; j++) cf[j] = (j < a.p) ? a.coef[sl * a.p + j] : 0.0;
+        }
+    }
+    // state: h[j] = value at t-1-j (outputs, or filled values for kFillDiffEwma)
+    double h[H];
+#pragma unroll
+    for (int j = 0; j < H; j++) h[j] = 0.0;
+    double e = 0.0;                                // EWMA state
+    double carry = __builtin_nan("");              // fillPrevious carry
+
+    for (int64_t tc = 0; tc < T; tc += kCH) {
+        const int len = (T - tc < kCH) ? (int)(T - tc) : kCH;
+        // load block: lanes 0-31 row r, lanes 32-63 row r+1
+        {
+            const int col = lane & 31;
+            for (int r = 0; r < ns; r += 2) {
+                const int row = r + (lane >> 5);
+                if (row < ns && col < len) tile[row * kRow + col] = a.in[(s0 + row) * a.ld_in + tc + col];
+            }
+        }
+        __syncthreads();
+        if (live) {
+            double* myrow = tile + lane * kRow;
+            for (int c = 0; c < len; c++) {
+                const int64_t t = tc + c;
+                const double x = myrow[c];
+                double y;
+                if (OP == kEwmaAdd) {
+                    // dest(i) = smoothing * ts(i) + (1 - smoothing) * dest(i - 1)
+                    e = (t == 0) ? x : sm * x + oms * e;
+                    y = e;
+                } else if (OP == kEwmaRemoveInplace) {
+                    // ts(i - 1) already overwritten by dest(i - 1)
+                    y = (t == 0) ? x : (x - oms * h[0]) / sm;
+                } else if (OP == kArAdd) {
+                    y = cc + x;
+#pragma unroll
+                    for (int j = 0; j < H; j++)
+                        if (j < hp && t - j - 1 >= 0) y += h[j] * cf[j];
+                } else if (OP == kArRemoveInplace) {
+                    y = x - cc;
+#pragma unroll
+                    for (int j = 0; j < H; j++)
+                        if (j < hp && t - j - 1 >= 0) y -= h[j] * cf[j];
+                } else if (OP == kDiffInplace) {
+                    // ts(i - lag) already overwritten when i - lag >= start; for i - lag < start it
+                    // equals the original, so h (the outputs) is right in both cases
+                    double hl = 0.0;
+#pragma unroll
+                    for (int j = 0; j < H; j++) hl = (j == hp - 1) ? h[j] : hl;   // static indexing
+                    y = (t < a.start) ? x : x - hl;
+                } else {  // kFillDiffEwma: fillPrevious -> differencesAtLag(lag, start=lag) -> EWMA add
+                    carry = (x != x) ? carry : x;
+                    const double f = carry;
+                    double hl = 0.0;
+#pragma unroll
+                    for (int j = 0; j < H; j++) hl = (j == hp - 1) ? h[j] : hl;   // static indexing
+                    const double d = (t < a.lag) ? f : f - hl;
+                    e = (t == 0) ? d : sm * d + oms * e;
+                    y = e;
+                    // history of FILLED values
+#pragma unroll
+                    for (int j = H - 1; j > 0; j--) h[j] = h[j - 1];
+                    h[0] = f;
+                    myrow[c] = y;
+                    continue;
+                }
+#pragma unroll
+                for (int j = H - 1; j > 0; j--) h[j] = h[j - 1];
+                h[0] = y;
+                myrow[c] = y;
+            }
+        }
+        __syncthreads();
+        {
+            const int col = lane & 31;
+            for (int r = 0; r < ns; r += 2) {
+                const int row = r + (lane >> 5);
+                if (row < ns && col < len) a.out[(s0 + row) * a.ld_out + tc + col] = tile[row * kRow + col];
+            }
+        }
+        __syncthreads();
+    }
+}
+
+// Fallbacks for histories longer than 32 steps (correct, not tuned):
+// in-place differencing decomposes into `lag` independent chains t = r, r+lag, ...
+__global__ __launch_bounds__(256) void diff_chain_kernel(double* x, int64_t S, int64_t T, int64_t ld, int lag,
+                                                         int start) {
+    const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (g >= S * lag) return;
+    const int64_t s = g / lag;
+    const int r = (int)(g - s * lag);
+    double* v = x + s * ld;
+    for (int64_t t = r; t < T; t += lag)
+        if (t >= start) v[t] = v[t] - v[t - lag];
+}
+
+// AR add / in-place AR remove of order p > 32: one thread per series on global memory
+template <int OP>
+__global__ __launch_bounds__(256) void ar_naive_kernel(RecurArgs a) {
+    const int64_t s = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (s >= a.S) return;
+    const double* x = a.in + s * a.ld_in;
+    double* d = a.out + s * a.ld_out;
+    const double* cf = a.coef + s * a.p;
+    const double c = a.c[s];
+    for (int64_t i = 0; i < a.T; i++) {
+        if (OP == kArAdd) {
+            double v = c + x[i];
+            for (int j = 0; j < a.p && i - j - 1 >= 0; j++) v += d[i - j - 1] * cf[j];
+            d[i] = v;
+        } else {
+            double v = x[i] - c;
+            for (int j = 0; j < a.p && i - j - 1 >= 0; j++) v -= d[i - j - 1] * cf[j];
+            d[i] = v;
+        }
+    }
+}
+
+template <int OP>
+hipError_t launch_h(const RecurArgs& a, int need, hipStream_t st) {
+    dim3 grid((unsigned)((a.S + 63) / 64)), block(64);
+    if (need <= 1) hipLaunchKernelGGL((recur_kernel<OP, 1>), grid, block, 0, st, a);
+    else if (need <= 2) hipLaunchKernelGGL((recur_kernel<OP, 2>), grid, block, 0, st, a);
+    else if (need <= 4) hipLaunchKernelGGL((recur_kernel<OP, 4>), grid, block, 0, st, a);
+    else if (need <= 8) hipLaunchKernelGGL((recur_kernel<OP, 8>), grid, block, 0, st, a);
+    else if (need <= 16) hipLaunchKernelGGL((recur_kernel<OP, 16>), grid, block, 0, st, a);
+    else if (need <= 32) hipLaunchKernelGGL((recur_kernel<OP, 32>), grid, block, 0, st, a);
+    else if (OP == kArAdd || OP == kArRemoveInplace)
+        hipLaunchKernelGGL((ar_naive_kernel<OP>), dim3((unsigned)((a.S + 255) / 256)), dim3(256), 0, st, a);
+    else if (OP == kDiffInplace)
+        hipLaunchKernelGGL(diff_chain_kernel, dim3((unsigned)((a.S * a.lag + 255) / 256)), dim3(256), 0, st,
+                           a.out, a.S, a.T, a.ld_out, a.lag, a.start);
+    else return hipErrorInvalidValue;
+    return hipGetLastError();
+}
+
+}  // namespace
+
+hipError_t launch_recur(RecurOp op, const RecurArgs& a, hipStream_t st) {
+    if (a.S <= 0 || a.T <= 0) return hipSuccess;
+    switch (op) {
+    case kEwmaAdd: return launch_h<kEwmaAdd>(a, 1, st);
+    case kEwmaRemoveInplace: return launch_h<kEwmaRemoveInplace>(a, 1, st);
+    case kArAdd: return launch_h<kArAdd>(a, a.p, st);
+    case kArRemoveInplace: return launch_h<kArRemoveInplace>(a, a.p, st);
+    case kDiffInplace: return launch_h<kDiffInplace>(a, a.lag, st);
+    case kFillDiffEwma: return launch_h<kFillDiffEwma>(a, a.lag, st);
+    }
+    return hipErrorInvalidValue;
+}
+
+hipError_t launch_diff_inplace(double* x, int64_t S, int64_t T, int64_t ld, int lag, int start,
+                               hipStream_t st) {
+    RecurArgs a{};
+    a.in = x;
+    a.out = x;
+    a.S = S;
+    a.T = T;
+    a.ld_in = ld;
+    a.ld_out = ld;
+    a.lag = lag;
+    a.start = start;
+    return launch_recur(kDiffInplace, a, st);
+}
+
+}  // namespace sts

@@ -1,0 +1,447 @@
+// sts_tile.hip -- the series-tile kernel: NaN imputation (fillts), optional fused
+// multi-lag autocorrelation partial sums on FP64 MFMA, optional lag-matrix output.
+//
+// Reference operators (S/ = src/main/scala/com/cloudera/sparkts/):
+//   fillPrevious   S/UnivariateTimeSeries.scala:194-204
+//   fillNext       S/UnivariateTimeSeries.scala:214-224
+//   fillNearest    S/UnivariateTimeSeries.scala:156-184
+//   fillLinear     S/UnivariateTimeSeries.scala:247-266
+//   autocorr       S/UnivariateTimeSeries.scala:68-93
+//   lagMatTrimBoth S/Lag.scala:62-77
+//
+// One workgroup (4 waves) owns one TILE: TW consecutive steps [t0, t1) of one series,
+// staged in LDS together with kHB steps before and kHA steps after it (extended range
+// E).  Imputation is index driven: a 64-bit validity ballot per 64 steps plus a
+// word-level max/min scan give, in O(1) per step, the last valid index L(t) <= t and
+// the first valid index N(t) >= t.  From (L, N) every method is a copy except linear,
+// whose reference loop accumulates r[j] = r[j-1] + inc SEQUENTIALLY from the run
+// start: each NaN step replays that chain from L (t - L adds), which reproduces the
+// reference bit for bit (no FMA: the library is built with -ffp-contract=off).
+// Runs longer than the halos fall back to a wave-wide scan of global memory.
+//
+// Autocorrelation: with y = F - F(0) (a shift; exact algebra for a correlation),
+// the kernel accumulates per tile P_i = sum_j y_j * y_{j+i} (i = 0..63) and
+// sum_j y_j for j in the tile, with y = 0 past the series end.  The lag products are
+// FP64 MFMA rank-4 updates: viewing the series as rows of 16, U_t = sum_a A_a^T A_{a+t}
+// (A_a = 16 consecutive steps) holds every pair at lag 16t + c - b; lane l of a wave
+// feeds element j0 + l as the A operand and j0 + 16t + l as the B operand of
+// v_mfma_f64_16x16x4_f64, so both operands are contiguous LDS reads.  A finalize
+// kernel (sts_acf_finalize) combines the tiles in a fixed order (deterministic).
+#include "sts_internal.hpp"
+
+#include <hip/hip_runtime.h>
+
+namespace sts {
+namespace {
+
+typedef double d4 __attribute__((ext_vector_type(4)));
+
+constexpr int kThreads = 256;
+constexpr int kWaves = kThreads / 64;
+constexpr int kBig = 1 << 30;
+
+__device__ __forceinline__ bool isnan_d(double v) { return __builtin_isnan(v); }
+
+// Bijective XCD-aware remap (cdna_hip_programming.md §5 "XCD swizzle must be
+// bijective"): consecutive tile ids -> one XCD, so neighbour tiles of one series
+// share the L2 that holds their overlapping halos.
+__device__ __forceinline__ int64_t xcd_remap(int64_t b, int64_t n) {
+    int64_t q = n / 8, r = n % 8, x = b % 8;
+    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
+}
+
+// Wave-wide search of global memory for the last valid index < from (stop at 0).
+__device__ int64_t scan_back(const double* src, int64_t from, int lane) {
+    for (int64_t base = from - 64;; base -= 64) {
+        int64_t t = base + lane;
+        bool v = (t >= 0 && t < from) ? !isnan_d(src[t]) : false;
+        unsigned long long m = __ballot(v);
+        if (m) return base + 63 - __clzll(m);
+        if (base <= 0) return -1;
+    }
+}
+
+// Wave-wide search for the first valid index >= from (stop at T).
+__device__ int64_t scan_fwd(const double* src, int64_t from, int64_t T, int lane) {
+    for (int64_t base = from;; base += 64) {
+        int64_t t = base + lane;
+        bool v = (t < T) ? !isnan_d(src[t]) : false;
+        unsigned long long m = __ballot(v);
+        if (m) return base + __ffsll(m) - 1;
+        if (base + 64 >= T) return T;
+    }
+}
+
+template <int TW, int NT>
+__global__ __launch_bounds__(kThreads) void tile_kernel(TileArgs a, int method) {
+    constexpr int EW = kHB + TW + kHA;
+    constexpr int NW = EW / 64;
+    static_assert(EW % 64 == 0, "extended tile must be whole words");
+    static_assert(NW <= 128, "word scan handles at most 128 words");
+    __shared__ __attribute__((aligned(16))) double vals[EW];
+    __shared__ unsigned long long mask[NW];
+    __shared__ int lastUpTo[NW];
+    __shared__ int firstFrom[NW];
+    __shared__ int64_t sh_i[2];
+    __shared__ double sh_d[3];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
+    const int64_t ntiles = a.S * a.tiles_per_series;
+    const int64_t tile = xcd_remap(blockIdx.x, ntiles);
+    const int64_t s = tile / a.tiles_per_series;
+    const int64_t k = tile - s * a.tiles_per_series;
+    const int64_t T = a.T;
+    const int64_t t0 = k * TW;
+    const int64_t t1 = (t0 + TW < T) ? t0 + TW : T;
+    const int64_t e0 = t0 - kHB;
+    const double* src = a.in + s * a.ld_in;
+
+    // ---- 1. stage E = [e0, e0 + EW) in LDS (NaN outside the series) ----
+    {
+        const bool interior = (e0 >= 0) && (e0 + EW <= T) && ((reinterpret_cast<uintptr_t>(src) & 15) == 0);
+        if (interior) {
+            const double2* s2 = reinterpret_cast<const double2*>(src + e0);
+            double2* v2 = reinterpret_cast<double2*>(vals);
+            constexpr int kFull = (EW / 2) / kThreads;      // whole rounds
+#pragma unroll
+            for (int j = 0; j < kFull; j++) v2[tid + j * kThreads] = s2[tid + j * kThreads];
+            if (kFull * kThreads + tid < EW / 2) v2[kFull * kThreads + tid] = s2[kFull * kThreads + tid];
+        } else {
+            for (int q = tid; q < EW; q += kThreads) {
+                int64_t t = e0 + q;
+                vals[q] = (t >= 0 && t < T) ? src[t] : __builtin_nan("");
+            }
+        }
+    }
+    __syncthreads();
+
+    // ---- 2. validity ballots, one 64-bit word per 64 steps ----
+    for (int w = wave; w < NW; w += kWaves) {
+        unsigned long long m = __ballot(!isnan_d(vals[w * 64 + lane]));
+        if (lane == 0) mask[w] = m;
+    }
+    __syncthreads();
+
+    // positions to produce: [qA, qB) (E-relative); ACF needs 16*NT steps past the tile
+    const int qA = kHB;
+    const int qW = kHB + (int)(t1 - t0);                       // end of the written range
+    int qB = qW + (NT > 0 ? 16 * NT : 0);
+    if (e0 + qB > T) qB = (int)(T - e0);
+    const bool needL = (method == STS_FILL_LINEAR || method == STS_FILL_PREVIOUS || method == STS_FILL_NEAREST);
+    const bool needN = (method == STS_FILL_LINEAR || method == STS_FILL_NEXT || method == STS_FILL_NEAREST);
+
+    // ---- 3. word-level scans (wave 0) + slow paths + ACF shift ----
+    if (wave == 0) {
+        const int w0 = 2 * lane, w1 = 2 * lane + 1;
+        unsigned long long m0 = (w0 < NW) ? mask[w0] : 0ull;
+        unsigned long long m1 = (w1 < NW) ? mask[w1] : 0ull;
+        int l0 = m0 ? w0 * 64 + 63 - __clzll(m0) : -1;
+        int l1 = m1 ? w1 * 64 + 63 - __clzll(m1) : -1;
+        int f0 = m0 ? w0 * 64 + __ffsll(m0) - 1 : kBig;
+        int f1 = m1 ? w1 * 64 + __ffsll(m1) - 1 : kBig;
+        int incl = l1 > l0 ? l1 : l0;         // max over my two words
+        int fmin = f0 < f1 ? f0 : f1;         // min over my two words
+        // inclusive prefix max over lanes
+        int pm = incl;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            int o = __shfl_up(pm, d);
+            if (lane >= d) pm = o > pm ? o : pm;
+        }
+        int ex = __shfl_up(pm, 1);
+        if (lane == 0) ex = -1;
+        // inclusive suffix min over lanes
+        int sm = fmin;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            int o = __shfl_down(sm, d);
+            if (lane + d < 64) sm = o < sm ? o : sm;
+        }
+        int exs = __shfl_down(sm, 1);
+        if (lane == 63) exs = kBig;
+        if (w0 < NW) {
+            lastUpTo[w0] = ex > l0 ? ex : l0;
+            int a0 = f1 < exs ? f1 : exs;
+            firstFrom[w0] = f0 < a0 ? f0 : a0;
+        }
+        if (w1 < NW) {
+            int a1 = ex > l0 ? ex : l0;
+            lastUpTo[w1] = a1 > l1 ? a1 : l1;
+            firstFrom[w1] = f1 < exs ? f1 : exs;
+        }
+        const int firstValidE = __shfl(sm, 0);     // min over all words
+        const int lastValidE = __shfl(pm, 63);     // max over all words
+        int64_t lext = -1, next = T;
+        if (needL && e0 > 0 && firstValidE > qA) lext = scan_back(src, e0, lane);
+        if (needN && e0 + EW < T && qB > qA && lastValidE < qB - 1) next = scan_fwd(src, e0 + EW, T, lane);
+        double c0 = 0.0;
+        if (NT > 0) {
+            double x0 = src[0];
+            if (method == STS_FILL_NEXT && isnan_d(x0)) {
+                int64_t f = scan_fwd(src, 0, T, lane);
+                x0 = (f < T) ? src[f] : __builtin_nan("");
+            }
+            c0 = x0;
+        }
+        if (lane == 0) {
+            sh_i[0] = lext;
+            sh_i[1] = next;
+            sh_d[0] = (lext >= 0) ? src[lext] : 0.0;
+            sh_d[1] = (next < T) ? src[next] : 0.0;
+            sh_d[2] = c0;
+        }
+    }
+    __syncthreads();
+
+    const int64_t lext = sh_i[0], next = sh_i[1];
+    const double lextv = sh_d[0], nextv = sh_d[1], c0 = sh_d[2];
+    bool series_err = false;
+
+    // value of the filled series at E-position q (t = e0 + q < T)
+    auto fill_at = [&](int q) -> double {
+        double v = vals[q];
+        if (method == STS_FILL_NONE || !isnan_d(v)) return v;
+        const int64_t t = e0 + q;
+        const int w = q >> 6, b = q & 63;
+        int64_t Lt = -1, Nt = T;
+        double Lv = 0.0, Nv = 0.0;
+        if (needL) {
+            unsigned long long m = mask[w] & (((2ull << b)) - 1ull);
+            int Lq = m ? w * 64 + 63 - __clzll(m) : (w > 0 ? lastUpTo[w - 1] : -1);
+            if (Lq >= 0) { Lt = e0 + Lq; Lv = vals[Lq]; }
+            else { Lt = lext; Lv = lextv; }
+        }
+        if (needN) {
+            unsigned long long m = mask[w] & (~0ull << b);
+            int Nq = m ? w * 64 + __ffsll(m) - 1 : (w + 1 < NW ? firstFrom[w + 1] : kBig);
+            if (Nq < kBig) { Nt = e0 + Nq; Nv = vals[Nq]; }
+            else { Nt = next; Nv = nextv; }
+        }
+        switch (method) {
+        case STS_FILL_PREVIOUS:
+            return Lt >= 0 ? Lv : __builtin_nan("");
+        case STS_FILL_NEXT:
+            return Nt < T ? Nv : __builtin_nan("");
+        case STS_FILL_NEAREST: {
+            if (t == 0) return v;                     // index 0 is never modified
+            const int64_t P = (Lt >= 1) ? Lt : -1;    // index 0 is never a previous source
+            if (P < 0 && Nt >= T) { series_err = true; return v; }
+            if (Nt >= T || (P >= 0 && t - P < Nt - t)) return Lv;   // ties go to next
+            return Nv;
+        }
+        case STS_FILL_LINEAR: {
+            if (Lt < 0 || Nt >= T) return v;          // runs touching index 0 or n-1 stay NaN
+            const double inc = (Nv - Lv) / (double)(int)(Nt - Lt);
+            double r = Lv;
+            for (int64_t j = Lt + 1; j <= t; j++) r = r + inc;   // sequential, as :259-261
+            return r;
+        }
+        default:
+            return v;
+        }
+    };
+
+    // ---- 4. produce F on [qA, qB): write filled output / lag matrix ----
+    // F is written back into vals IN PLACE at NaN positions only: every (L, N) source
+    // read by another thread is a valid position, whose value never changes.
+    double* dst = a.out ? a.out + s * a.ld_out : nullptr;
+    const bool dst_al = dst && ((reinterpret_cast<uintptr_t>(dst) & 15) == 0);
+    const int64_t lrows = T - a.max_lag;
+    const int ncols = a.max_lag + (a.include_original ? 1 : 0);
+    const int init = a.include_original ? 0 : 1;
+    for (int q = qA + 2 * tid; q < qB; q += 2 * kThreads) {
+        const double v0 = vals[q];
+        const double v1 = (q + 1 < qB) ? vals[q + 1] : 0.0;
+        const double f0 = isnan_d(v0) ? fill_at(q) : v0;
+        const double f1 = (q + 1 < qB && isnan_d(v1)) ? fill_at(q + 1) : v1;
+        const int64_t t = e0 + q;
+        if (dst && q < qW) {
+            if (dst_al && q + 1 < qW) {
+                *reinterpret_cast<double2*>(dst + t) = make_double2(f0, f1);
+            } else {
+                dst[t] = f0;
+                if (q + 1 < qW) dst[t + 1] = f1;
+            }
+        }
+        if (a.lagmat && q < qW) {
+            double* lm = a.lagmat + s * lrows * ncols;
+            for (int c = init; c <= a.max_lag; c++) {
+                double* col = lm + (int64_t)(c - init) * lrows;
+                const int64_t r0 = t - a.max_lag + c;
+                if (r0 >= 0 && r0 < lrows) col[r0] = f0;
+                if (q + 1 < qW && r0 + 1 >= 0 && r0 + 1 < lrows) col[r0 + 1] = f1;
+            }
+        }
+        if (NT > 0) {
+            if (isnan_d(v0)) vals[q] = f0;
+            if (q + 1 < qB && isnan_d(v1)) vals[q + 1] = f1;
+        }
+    }
+    if (series_err && a.err) a.err[s] = STS_ERR_ALL_NAN;
+
+    if constexpr (NT > 0) {
+        // ---- 5. y = F - F(0) in place (0 past the series end) ----
+        __syncthreads();
+        // every index the MFMA loop can touch must hold y (0 past the data): the last
+        // chunk may read 63 + 16*(NT-1) steps past qW
+        const int qBfull = (qW + 64 + 16 * NT < EW) ? qW + 64 + 16 * NT : EW;
+        for (int q = qA + tid; q < qBfull; q += kThreads) vals[q] = (q < qB) ? vals[q] - c0 : 0.0;
+        __syncthreads();
+
+        // ---- 6. lag products on MFMA: U_t += A(j0 + l) x B(j0 + 16t + l) ----
+        constexpr int CPW = TW / 64 / kWaves;   // 64-step chunks per wave
+        const int nchunks = (int)((t1 - t0 + 63) / 64);
+        int c = wave * CPW;
+        int cend = c + CPW;
+        if (cend > nchunks) cend = nchunks;
+        d4 U[NT];
+#pragma unroll
+        for (int t = 0; t < NT; t++) U[t] = d4{0.0, 0.0, 0.0, 0.0};
+        double sy = 0.0;
+        const int tlen = (int)(t1 - t0);
+        for (; c < cend; c++) {
+            const int jrel = 64 * c + lane;
+            const double* yb = vals + qA + jrel;
+            const double av = (jrel < tlen) ? yb[0] : 0.0;
+            double bv[NT];
+            bv[0] = av;
+#pragma unroll
+            for (int t = 1; t < NT; t++) bv[t] = yb[16 * t];
+#pragma unroll
+            for (int t = 0; t < NT; t++) U[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv[t], U[t], 0, 0, 0);
+            sy += av;
+        }
+        __syncthreads();   // every wave is done reading y
+
+        // ---- 7. diagonal extraction: lane i accumulates lag i in a fixed order ----
+        double* scr = vals + wave * 256;
+        double lagacc = 0.0;
+#pragma unroll
+        for (int t = 0; t < NT; t++) {
+#pragma unroll
+            for (int r = 0; r < 4; r++) scr[((lane >> 4) + 4 * r) * 16 + (lane & 15)] = U[t][r];
+            __syncthreads();
+#pragma unroll
+            for (int b = 0; b < 16; b++)
+                if (((b + lane) >> 4) == t) lagacc += scr[b * 16 + ((b + lane) & 15)];
+            __syncthreads();
+        }
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) sy += __shfl_xor(sy, d);
+        double* wsum = vals + kWaves * 256;
+        wsum[wave * kPartStride + lane] = lagacc;
+        if (lane == 0) wsum[wave * kPartStride + 64] = sy;
+        __syncthreads();
+        if (wave == 0) {
+            double* part = a.partials + tile * kPartStride;
+            double tot = 0.0;
+#pragma unroll
+            for (int w = 0; w < kWaves; w++) tot += wsum[w * kPartStride + lane];
+            part[lane] = tot;
+            if (lane == 0) {
+                double ts = 0.0;
+#pragma unroll
+                for (int w = 0; w < kWaves; w++) ts += wsum[w * kPartStride + 64];
+                part[64] = ts;
+            }
+        }
+    }
+}
+
+// One wave per series: combine tile partials in tile order (deterministic), apply the
+// head/tail corrections, and form the reference's correlation
+//   cov / (sqrt(var1) * sqrt(var2))            (S/UnivariateTimeSeries.scala:80-89)
+// from shifted moments.  Lane l computes lag i = l + 1.  Series with T <= 2K run the
+// reference's two-pass loop directly (reproduces its NaN pattern exactly when a NaN sits
+// in the middle of a short series).
+__global__ __launch_bounds__(256) void acf_finalize_kernel(FinalizeArgs a) {
+    const int lane = threadIdx.x & 63;
+    const int64_t s = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (s >= a.S) return;
+    const int K = a.K;
+    const int i = lane + 1;
+    const int64_t T = a.T;
+    const double* F = a.F + s * a.ldF;
+    if (lane >= K) return;
+    double out;
+    if (i >= T) {
+        out = __builtin_nan("");
+    } else if (T <= 2 * (int64_t)K) {
+        const int64_t len = T - i;
+        double s1 = 0.0, s2 = 0.0;
+        for (int64_t j = 0; j < len; j++) s1 += F[i + j];
+        for (int64_t j = 0; j < len; j++) s2 += F[j];
+        const double m1 = s1 / (double)len, m2 = s2 / (double)len;
+        double v1 = 0.0, v2 = 0.0, cv = 0.0;
+        for (int64_t j = 0; j < len; j++) {
+            double d1 = F[i + j] - m1, d2 = F[j] - m2;
+            v1 += d1 * d1;
+            v2 += d2 * d2;
+            cv += d1 * d2;
+        }
+        out = cv / (__builtin_sqrt(v1) * __builtin_sqrt(v2));
+    } else {
+        double Pi = 0.0, P0 = 0.0, Sy = 0.0;
+        const double* pp = a.partials + s * a.tiles_per_series * kPartStride;
+        for (int64_t k = 0; k < a.tiles_per_series; k++, pp += kPartStride) {
+            Pi += pp[i];
+            P0 += pp[0];
+            Sy += pp[64];
+        }
+        const double c0 = F[0];
+        double pre_s = 0.0, pre_q = 0.0, suf_s = 0.0, suf_q = 0.0;
+        for (int j = 0; j < i; j++) {
+            double y = F[j] - c0;
+            pre_s += y;
+            pre_q += y * y;
+            double z = F[T - 1 - j] - c0;
+            suf_s += z;
+            suf_q += z * z;
+        }
+        const double N = (double)(T - i);
+        const double sum1 = Sy - pre_s, sum2 = Sy - suf_s;
+        const double sq1 = P0 - pre_q, sq2 = P0 - suf_q;
+        const double v1 = sq1 - sum1 * sum1 / N;
+        const double v2 = sq2 - sum2 * sum2 / N;
+        const double cv = Pi - sum1 * sum2 / N;
+        out = cv / (__builtin_sqrt(v1) * __builtin_sqrt(v2));
+    }
+    a.acf[s * K + lane] = out;
+}
+
+}  // namespace
+
+hipError_t launch_tile(int method, int tw, const TileArgs& a, hipStream_t st) {
+    const int64_t ntiles = a.S * a.tiles_per_series;
+    if (ntiles <= 0) return hipSuccess;
+    if (ntiles > 0x7fffffffLL) return hipErrorInvalidValue;
+    dim3 grid((unsigned)ntiles), block(kThreads);
+    int nt = 0;
+    if (a.K > 0) nt = (a.K + 15) / 16 + 1;
+    if (tw == 512 && nt == 0) {
+        hipLaunchKernelGGL((tile_kernel<512, 0>), grid, block, 0, st, a, method);
+    } else if (tw == 4096) {
+        switch (nt) {
+        case 0: hipLaunchKernelGGL((tile_kernel<4096, 0>), grid, block, 0, st, a, method); break;
+        case 2: hipLaunchKernelGGL((tile_kernel<4096, 2>), grid, block, 0, st, a, method); break;
+        case 3: hipLaunchKernelGGL((tile_kernel<4096, 3>), grid, block, 0, st, a, method); break;
+        case 4: hipLaunchKernelGGL((tile_kernel<4096, 4>), grid, block, 0, st, a, method); break;
+        case 5: hipLaunchKernelGGL((tile_kernel<4096, 5>), grid, block, 0, st, a, method); break;
+        default: return hipErrorInvalidValue;
+        }
+    } else {
+        return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_acf_finalize(const FinalizeArgs& a, hipStream_t st) {
+    if (a.S <= 0 || a.K <= 0) return hipSuccess;
+    dim3 grid((unsigned)((a.S + 3) / 4)), block(256);
+    hipLaunchKernelGGL(acf_finalize_kernel, grid, block, 0, st, a);
+    return hipGetLastError();
+}
+
+}  // namespace sts

@@ -1,0 +1,99 @@
+"""Loader and ctypes bindings for libsts_hip.so (the C ABI in include/sts.h).
+
+This is the Python analogue of the JNI shim: plain pointers and
+sizes cross the boundary, no torch types.  There is deliberately NO fallback:
+if the HIP library is missing or no gfx950 device is visible, every operator
+raises -- the product path never computes on the CPU.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+PKG_ROOT = os.path.dirname(HERE)
+LIB_PATH = os.environ.get("STS_HIP_LIB", os.path.join(PKG_ROOT, "build", "libsts_hip.so"))
+
+_c_i64 = ctypes.c_int64
+_c_int = ctypes.c_int
+_c_vp = ctypes.c_void_p
+_c_dbl = ctypes.c_double
+
+# name -> (restype, argtypes); mirrors include/sts.h exactly (tests/test_abi.py checks
+# that every symbol declared there is exported and bound here).
+SIGNATURES = {
+    "sts_abi_version": (_c_int, []),
+    "sts_init": (_c_int, [_c_int]),
+    "sts_last_error": (ctypes.c_char_p, []),
+    "sts_fill_method_from_name": (_c_int, [ctypes.c_char_p]),
+    "sts_stream_synchronize": (_c_int, [_c_vp]),
+    "sts_profile_begin": (_c_int, []),
+    "sts_profile_end": (_c_int, [_c_vp, _c_vp]),
+    "sts_fill": (_c_int, [_c_vp, _c_vp, _c_i64, _c_i64, _c_i64, _c_i64, _c_int, _c_vp, _c_vp]),
+    "sts_diff_at_lag": (_c_int, [_c_vp, _c_vp, _c_i64, _c_i64, _c_i64, _c_i64, _c_int, _c_int, _c_vp]),
+    "sts_lag_matrix": (_c_int, [_c_vp, _c_vp, _c_i64, _c_i64, _c_i64, _c_int, _c_int, _c_vp]),
+    "sts_autocorr": (_c_int, [_c_vp, _c_i64, _c_i64, _c_i64, _c_int, _c_vp, _c_vp]),
+    "sts_ewma_add": (_c_int, [_c_vp, _c_vp, _c_i64, _c_i64, _c_i64, _c_i64, _c_vp, _c_vp]),
+    "sts_ewma_remove": (_c_int, [_c_vp, _c_vp, _c_i64, _c_i64, _c_i64, _c_i64, _c_vp, _c_vp]),
+    "sts_ar_fit": (_c_int, [_c_vp, _c_i64, _c_i64, _c_i64, _c_int, _c_int, _c_vp, _c_vp, _c_vp, _c_vp]),
+    "sts_ar_remove": (_c_int, [_c_vp, _c_vp, _c_i64, _c_i64, _c_i64, _c_i64, _c_vp, _c_vp, _c_int, _c_vp]),
+    "sts_ar_add": (_c_int, [_c_vp, _c_vp, _c_i64, _c_i64, _c_i64, _c_i64, _c_vp, _c_vp, _c_int, _c_vp]),
+    "sts_fill_autocorr": (_c_int, [_c_vp, _c_vp, _c_i64, _c_i64, _c_i64, _c_i64, _c_int, _c_int, _c_vp, _c_vp, _c_vp]),
+    "sts_fill_diff_ewma": (_c_int, [_c_vp, _c_vp, _c_i64, _c_i64, _c_i64, _c_i64, _c_int, _c_int, _c_vp, _c_vp, _c_vp]),
+    "sts_fill_lag_matrix": (_c_int, [_c_vp, _c_vp, _c_vp, _c_i64, _c_i64, _c_i64, _c_i64, _c_int, _c_int, _c_int,
+                                     _c_vp, _c_vp]),
+    "sts_ar_fit_remove": (_c_int, [_c_vp, _c_vp, _c_i64, _c_i64, _c_i64, _c_i64, _c_int, _c_int, _c_vp, _c_vp,
+                                   _c_vp, _c_vp]),
+    "sts_gen_panel": (_c_int, [_c_vp, _c_i64, _c_i64, _c_i64, _c_i64, ctypes.c_uint64, _c_dbl, _c_vp]),
+    "sts_gen_ar_panel": (_c_int, [_c_vp, _c_vp, _c_vp, _c_i64, _c_i64, _c_i64, _c_i64, ctypes.c_uint64, _c_int, _c_vp]),
+    "sts_fill_host": (_c_int, [_c_vp, _c_vp, _c_i64, _c_i64, _c_i64, _c_int, _c_vp]),
+    "sts_autocorr_host": (_c_int, [_c_vp, _c_i64, _c_i64, _c_i64, _c_int, _c_vp]),
+    "sts_diff_at_lag_host": (_c_int, [_c_vp, _c_vp, _c_i64, _c_i64, _c_i64, _c_int, _c_int]),
+    "sts_lag_matrix_host": (_c_int, [_c_vp, _c_vp, _c_i64, _c_i64, _c_i64, _c_int, _c_int]),
+    "sts_ewma_add_host": (_c_int, [_c_vp, _c_vp, _c_i64, _c_i64, _c_i64, _c_vp]),
+    "sts_ewma_remove_host": (_c_int, [_c_vp, _c_vp, _c_i64, _c_i64, _c_i64, _c_vp]),
+    "sts_ar_fit_host": (_c_int, [_c_vp, _c_i64, _c_i64, _c_i64, _c_int, _c_int, _c_vp, _c_vp, _c_vp]),
+    "sts_ar_remove_host": (_c_int, [_c_vp, _c_vp, _c_i64, _c_i64, _c_i64, _c_vp, _c_vp, _c_int]),
+    "sts_ar_add_host": (_c_int, [_c_vp, _c_vp, _c_i64, _c_i64, _c_i64, _c_vp, _c_vp, _c_int]),
+}
+
+_lib = None
+_lock = threading.Lock()
+_inited = set()
+
+
+class NativeLibraryError(RuntimeError):
+    """libsts_hip.so is missing or unusable: there is no CPU fallback."""
+
+
+def load_library(path: str = LIB_PATH):
+    """Load and bind libsts_hip.so (no device needed, used by the CPU ABI tests)."""
+    global _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(path):
+                raise NativeLibraryError(
+                    "libsts_hip.so not found at %s: build it with `python -c 'import __graft_entry__ as g; g.build()'`"
+                    " (there is no CPU fallback)" % path)
+            lib = ctypes.CDLL(path)
+            for name, (res, args) in SIGNATURES.items():
+                fn = getattr(lib, name)
+                fn.restype = res
+                fn.argtypes = args
+            _lib = lib
+    return _lib
+
+
+def lib():
+    return load_library()
+
+
+def ensure_device(device: int) -> None:
+    """sts_init(device) once per (thread, device): selects the HIP device and checks gfx950."""
+    key = (threading.get_ident(), device)
+    if key in _inited:
+        return
+    from .errors import raise_for_status
+    raise_for_status(lib().sts_init(device), "sts_init")
+    _inited.add(key)

@@ -1,0 +1,496 @@
+"""Parity of the HIP path (through the C ABI) with the CPU oracle.  Needs an MI355X.
+
+Tolerances (BASELINE.json north_star): index-driven work (lag, differencing,
+previous/next/nearest fill) and the recurrences restated in the reference's own
+order (linear fill, EWMA add/remove, AR add/remove) are BIT-EXACT; autocorrelation
+and AR coefficients within 1e-10 relative (RTOL below), NaN patterns identical.
+"""
+import zlib
+
+import numpy as np
+import pytest
+
+import oracle
+
+pytestmark = pytest.mark.gpu
+
+RTOL = 1e-10
+NaN = np.nan
+
+
+@pytest.fixture(scope="module")
+def torch():
+    import torch as _t
+    if not _t.cuda.is_available():
+        pytest.skip("no GPU")
+    from sparkts import _native
+    _native.ensure_device(0)
+    return _t
+
+
+def dev(torch, a):
+    return torch.as_tensor(np.ascontiguousarray(a, dtype=np.float64), device="cuda:0")
+
+
+def host(t):
+    return t.detach().cpu().numpy()
+
+
+def assert_bits(got, ref, what=""):
+    got = np.ascontiguousarray(got, dtype=np.float64)
+    ref = np.ascontiguousarray(ref, dtype=np.float64)
+    assert got.shape == ref.shape, (what, got.shape, ref.shape)
+    gb, rb = got.view(np.uint64), ref.view(np.uint64)
+    # all NaNs compare equal regardless of payload
+    same = (gb == rb) | (np.isnan(got) & np.isnan(ref))
+    if not same.all():
+        idx = np.argwhere(~same)[:5]
+        raise AssertionError("%s: %d mismatches, first %s got %s ref %s" % (
+            what, (~same).sum(), idx.tolist(), [got[tuple(i)] for i in idx], [ref[tuple(i)] for i in idx]))
+
+
+def assert_rel(got, ref, rtol=RTOL, what=""):
+    got = np.asarray(got)
+    ref = np.asarray(ref)
+    assert got.shape == ref.shape
+    assert np.array_equal(np.isnan(got), np.isnan(ref)), "%s: NaN pattern differs" % what
+    fin = ~np.isnan(ref)
+    if fin.any():
+        err = np.abs(got[fin] - ref[fin]) / np.maximum(np.abs(ref[fin]), 1e-300)
+        assert err.max() <= rtol, "%s: max rel err %g > %g" % (what, err.max(), rtol)
+
+
+def random_panel(rng, S, T, nan_p, runs=False):
+    x = 100.0 + rng.standard_normal((S, T)).cumsum(axis=1) * 0.1 + rng.random((S, T))
+    x[rng.random((S, T)) < nan_p] = NaN
+    if runs and T > 10:
+        for s in range(S):
+            a = rng.integers(0, T)
+            b = min(T, a + rng.integers(1, max(2, T // 3)))
+            x[s, a:b] = NaN
+    return x
+
+
+SHAPES = [(3, 1), (4, 2), (5, 3), (7, 5), (9, 63), (9, 64), (9, 65), (16, 390), (5, 511), (5, 512), (5, 513),
+          (11, 2520), (3, 4096), (3, 4097), (4, 4159), (4, 4161), (3, 9000), (2, 20000)]
+
+
+# ---------------- fills (a1-a5): bit-exact ----------------
+
+FILL_KATS = [  # T/FillSuite.scala:35-61
+    ("previous", [1.0, NaN, 3.0, NaN, 2.0], [1.0, 1.0, 3.0, 3.0, 2.0]),
+    ("next", [1.0, NaN, 3.0, NaN, 2.0], [1.0, 3.0, 3.0, 2.0, 2.0]),
+    ("linear", [1.0, NaN, 3.0, NaN, 2.0], [1.0, 2.0, 3.0, 2.5, 2.0]),
+    ("linear", [1.0, NaN, NaN, NaN, 5.0], [1.0, 2.0, 3.0, 4.0, 5.0]),
+    ("linear", [2.0, NaN, 1.0], [2.0, 1.5, 1.0]),
+    ("nearest", [1.0, NaN, 2.0], [1.0, 2.0, 2.0]),
+]
+
+
+@pytest.mark.parametrize("method,x,want", FILL_KATS)
+def test_fill_kats_device_and_host(torch, method, x, want):
+    from sparkts import UnivariateTimeSeries as uts
+    assert_bits(host(uts.fillts(dev(torch, x), method)), want, method)
+    assert_bits(uts.fillts(np.array(x), method), want, method + " host path")
+
+
+@pytest.mark.parametrize("method", ["linear", "previous", "next", "nearest"])
+@pytest.mark.parametrize("nan_p", [0.0, 0.05, 0.3, 0.9])
+def test_fill_panels(torch, method, nan_p):
+    from sparkts import UnivariateTimeSeries as uts
+    from sparkts import _native
+    rng = np.random.default_rng(zlib.crc32(("%s%g" % (method, nan_p)).encode()))
+    lib = _native.lib()
+    code = uts.fill_method_code(method)
+    for S, T in SHAPES:
+        x = random_panel(rng, S, T, nan_p, runs=True)
+        ref, err = oracle.panel_fill(x, method)
+        xd = dev(torch, x)
+        out = torch.empty_like(xd)
+        e = torch.zeros(S, dtype=torch.int32, device="cuda:0")
+        st = lib.sts_fill(xd.data_ptr(), out.data_ptr(), S, T, T, T, code, e.data_ptr(), None)
+        assert st == 0
+        torch.cuda.synchronize()
+        ge = host(e)
+        assert np.array_equal(ge != 0, err != 0), (method, S, T, ge, err)
+        ok = err == 0
+        assert_bits(host(out)[ok], ref[ok], "%s S=%d T=%d" % (method, S, T))
+
+
+@pytest.mark.parametrize("method", ["linear", "previous", "next", "nearest"])
+def test_fill_long_runs_and_edges(torch, method):
+    from sparkts import UnivariateTimeSeries as uts
+    T = 30000
+    rows = []
+    x = np.arange(T, dtype=np.float64) * 0.37 + 1.0
+    a = x.copy(); a[100:25000] = NaN; rows.append(a)          # run across many tiles (slow path both ways)
+    a = x.copy(); a[:9000] = NaN; rows.append(a)              # long leading run
+    a = x.copy(); a[-9000:] = NaN; rows.append(a)             # long trailing run
+    a = x.copy(); a[1:] = NaN; rows.append(a)                 # only x[0] valid (nearest throws)
+    a = x.copy(); a[4090:4200] = NaN; rows.append(a)          # run straddling a tile edge
+    a = x.copy(); a[::2] = NaN; rows.append(a)                # alternating
+    a = np.full(T, NaN); rows.append(a)                       # all NaN
+    a = x.copy(); a[4096 - 64 - 70:4096 + 200] = NaN; rows.append(a)  # run longer than the look-back halo
+    a = x.copy(); a[0] = NaN; a[8191:8192 + 130] = NaN; rows.append(a)
+    P = np.array(rows)
+    ref, err = oracle.panel_fill(P, method)
+    from sparkts import _native
+    lib = _native.lib()
+    xd = dev(torch, P)
+    out = torch.empty_like(xd)
+    e = torch.zeros(P.shape[0], dtype=torch.int32, device="cuda:0")
+    assert lib.sts_fill(xd.data_ptr(), out.data_ptr(), P.shape[0], T, T, T, uts.fill_method_code(method),
+                        e.data_ptr(), None) == 0
+    torch.cuda.synchronize()
+    assert np.array_equal(host(e) != 0, err != 0)
+    ok = err == 0
+    assert_bits(host(out)[ok], ref[ok], method)
+
+
+def test_fill_nearest_raises(torch):
+    from sparkts import UnivariateTimeSeries as uts
+    from sparkts.errors import IllegalArgumentException
+    with pytest.raises(IllegalArgumentException, match="Input is all NaNs!"):
+        uts.fillNearest(dev(torch, [5.0, NaN]))
+    with pytest.raises(IllegalArgumentException):
+        uts.fillNearest(np.array([[1.0, 2.0, 3.0], [NaN, NaN, NaN]]))
+
+
+def test_fill_unsupported(torch):
+    from sparkts import UnivariateTimeSeries as uts
+    from sparkts.errors import UnsupportedOperationException
+    with pytest.raises(UnsupportedOperationException):
+        uts.fillts(dev(torch, [1.0, NaN, 2.0]), "spline")
+    with pytest.raises(UnsupportedOperationException):
+        uts.fillts(dev(torch, [1.0, NaN, 2.0]), "cubic")
+
+
+def test_fill_padded_leading_dimension(torch):
+    from sparkts import _native
+    rng = np.random.default_rng(5)
+    S, T, ld = 6, 5000, 5003
+    x = random_panel(rng, S, T, 0.2)
+    buf = np.full((S, ld), 7.0); buf[:, :T] = x
+    ref, _ = oracle.panel_fill(x, "linear")
+    xd = dev(torch, buf)
+    out = torch.full((S, ld + 1), -1.0, dtype=torch.float64, device="cuda:0")
+    assert _native.lib().sts_fill(xd.data_ptr(), out.data_ptr(), S, T, ld, ld + 1, 0, None, None) == 0
+    o = host(out)
+    assert_bits(o[:, :T], ref)
+    assert (o[:, T:] == -1.0).all()
+
+
+# ---------------- autocorr (a8): 1e-10 relative ----------------
+
+@pytest.mark.parametrize("K", [1, 5, 16, 17, 20, 33, 48, 49, 60, 63])
+def test_autocorr_panels(torch, K):
+    from sparkts import UnivariateTimeSeries as uts
+    rng = np.random.default_rng(K)
+    for S, T in [(5, 1), (5, 2), (7, 40), (7, 121), (6, 130), (9, 390), (5, 2520), (3, 4096), (3, 4097), (2, 12345)]:
+        x = 50.0 + rng.standard_normal((S, T)).cumsum(axis=1) * 0.5 + rng.standard_normal((S, T))
+        got = host(uts.autocorr(dev(torch, x), K))
+        ref = np.array([oracle.autocorr(r, K) for r in x])
+        assert_rel(got, ref, what="K=%d T=%d" % (K, T))
+
+
+def test_autocorr_nan_and_constant(torch):
+    from sparkts import UnivariateTimeSeries as uts
+    K = 20
+    rows = [np.full(100, 5.0), np.r_[np.full(50, 1.0), np.full(50, 3.0)], np.arange(100.0)]
+    a = np.arange(100.0); a[40] = NaN; rows.append(a)
+    b = np.arange(30.0); b[15] = NaN; rows.append(b[:30])   # short series: NaN only in the middle
+    got = [host(uts.autocorr(dev(torch, r), K)) for r in rows]
+    ref = [oracle.autocorr(r, K) for r in rows]
+    for g, r in zip(got, ref):
+        assert_rel(g, r)
+
+
+def test_autocorr_reference_statistics(torch):
+    # T/UnivariateTimeSeriesSuite.scala:47-60 through the device path
+    from mt19937 import MersenneTwister
+    from sparkts import UnivariateTimeSeries as uts
+    rand = MersenneTwister(5)
+    iid = np.array([rand.next_double() * 5.0 for _ in range(10000)])
+    for r in host(uts.autocorr(dev(torch, iid), 3)):
+        assert abs(r) < 0.03
+    g = np.array([rand.next_gaussian() for _ in range(10000)])
+    ar = oracle.ar_add(g, 1.5, [0.2], inplace=True)
+    acf = host(uts.autocorr(dev(torch, ar), 3))
+    assert abs(0.2 - acf[0]) < 0.02 and 0.0 < acf[1] < 0.06 and 0.0 < acf[2] < 0.06
+
+
+@pytest.mark.parametrize("method", ["linear", "previous", "next", "nearest"])
+def test_fill_autocorr_fused(torch, method):
+    from sparkts import TimeSeriesRDD
+    for seed, (S, T, K) in enumerate([(50, 2520, 20), (6, 9000, 60), (3, 4096 * 3 + 17, 63)]):
+        x = oracle.gen_panel(seed + 3, S, T, 0.05)
+        if method == "nearest":
+            x[:, 1] = 100.0  # keep every series valid for nearest
+        rdd = TimeSeriesRDD(None, None, dev(torch, x))
+        filled, acf = rdd.fillAndAutocorr(method, K)
+        rf, racf, err = oracle.panel_fill_autocorr(x, method, K)
+        assert (err == 0).all()
+        assert_bits(host(filled.data), rf, method)
+        assert_rel(host(acf), racf, what=method)
+
+
+def test_fill_autocorr_c3_length(torch):
+    # C3 series length (982,800 minute bars), a few series: fused fill("linear") + ACF(60)
+    S, T, K = 3, 982_800, 60
+    x = oracle.gen_panel(3, S, T, 0.05)
+    from sparkts import TimeSeriesRDD
+    filled, acf = TimeSeriesRDD(None, None, dev(torch, x)).fillAndAutocorr("linear", K)
+    rf, racf, _ = oracle.panel_fill_autocorr(x, "linear", K, threads=3)
+    assert_bits(host(filled.data), rf)
+    assert_rel(host(acf), racf)
+
+
+# ---------------- differencing (a6), lag (a7): bit-exact ----------------
+
+@pytest.mark.parametrize("lag,start", [(1, 1), (5, 5), (3, 7), (40, 40), (0, 0), (0, 3)])
+def test_diff_at_lag(torch, lag, start):
+    from sparkts import UnivariateTimeSeries as uts
+    rng = np.random.default_rng(lag * 10 + start)
+    x = rng.standard_normal((13, 777))
+    got = host(uts.differencesAtLag(dev(torch, x), lag, startIndex=start))
+    ref = np.array([oracle.differences_at_lag(r, lag, start=start) for r in x])
+    assert_bits(got, ref)
+    # in place (dest eq ts): the reference's aliasing semantics
+    xd = dev(torch, x)
+    uts.differencesAtLag(xd, lag, destTs=xd, startIndex=start)
+    ref2 = np.array([oracle.differences_at_lag(r, lag, start=start, inplace=True) for r in x])
+    assert_bits(host(xd), ref2, "in place")
+
+
+def test_diff_requirement(torch):
+    from sparkts import UnivariateTimeSeries as uts
+    from sparkts.errors import IllegalArgumentException
+    with pytest.raises(IllegalArgumentException, match="starting index cannot be less than lag"):
+        uts.differencesAtLag(dev(torch, np.arange(10.0)), 3, startIndex=2)
+
+
+def test_diff_reference_kat(torch):
+    # T/UnivariateTimeSeriesSuite.scala:112-126
+    from mt19937 import MersenneTwister
+    from sparkts import UnivariateTimeSeries as uts
+    rand = MersenneTwister(10)
+    s = np.array([rand.next_gaussian() for _ in range(100)])
+    d = host(uts.differencesAtLag(dev(torch, s), 5))
+    assert d[10] == s[10] - s[5] and d[99] == s[99] - s[94]
+
+
+@pytest.mark.parametrize("p,inc", [(0, True), (1, False), (2, True), (2, False), (10, False), (10, True)])
+def test_lag_matrix(torch, p, inc):
+    from sparkts import UnivariateTimeSeries as uts
+    rng = np.random.default_rng(p)
+    x = rng.standard_normal((7, 300))
+    got = host(uts.lag(dev(torch, x), p, inc))
+    ref = np.array([oracle.lag(r, p, inc) for r in x])
+    assert_bits(got, ref)
+
+
+def test_lag_kat(torch):
+    from sparkts import UnivariateTimeSeries as uts
+    v = dev(torch, [1.0, 2.0, 3.0, 4.0, 5.0])
+    assert_bits(host(uts.lag(v, 2, True)), [[3.0, 2.0, 1.0], [4.0, 3.0, 2.0], [5.0, 4.0, 3.0]])
+    assert_bits(host(uts.lag(v, 2, False)), [[2.0, 1.0], [3.0, 2.0], [4.0, 3.0]])
+
+
+@pytest.mark.parametrize("method", ["nearest", "next"])
+def test_fill_lag_matrix_fused(torch, method):
+    from sparkts import _native
+    S, T, p = 5, 9000, 10
+    x = oracle.gen_panel(5, S, T, 0.3)
+    x[:, 1] = 1.0
+    xd = dev(torch, x)
+    filled = torch.empty_like(xd)
+    lm = torch.empty((S, p, T - p), dtype=torch.float64, device="cuda:0")
+    from sparkts import UnivariateTimeSeries as uts
+    assert _native.lib().sts_fill_lag_matrix(xd.data_ptr(), filled.data_ptr(), lm.data_ptr(), S, T, T, T,
+                                             uts.fill_method_code(method), p, 0, None, None) == 0
+    rf, _ = oracle.panel_fill(x, method)
+    assert_bits(host(filled), rf)
+    ref = np.array([oracle.lag(r, p, False) for r in rf])      # (S, rows, cols)
+    assert_bits(host(lm).transpose(0, 2, 1), ref)
+
+
+# ---------------- EWMA (a9, a10): bit-exact ----------------
+
+def test_ewma_kats(torch):
+    # T/models/EWMASuite.scala:22-51
+    from sparkts.models import EWMAModel
+    orig = dev(torch, np.arange(1, 11, dtype=np.float64))
+    for s, last in ((0.2, 6.54), (0.6, 9.33)):
+        out = torch.zeros_like(orig)
+        EWMAModel(s).addTimeDependentEffects(orig, out)
+        o = host(out)
+        assert o[0] == 1.0 and o[1] == s * 2.0 + (1 - s) * o[0]
+        assert round(o[-1] * 100) / 100 == last
+    sm = dev(torch, [1.0, 1.2, 1.56, 2.05, 2.64, 3.31, 4.05, 4.84, 5.67, 6.54])
+    o = torch.zeros_like(sm)
+    EWMAModel(0.2).removeTimeDependentEffects(sm, o)
+    assert int(host(o)[-1]) == 10
+
+
+def test_ewma_panels(torch):
+    from sparkts.models import EWMAModel
+    from sparkts.errors import NullPointerException
+    rng = np.random.default_rng(7)
+    for S, T in [(1, 1), (3, 31), (64, 33), (130, 390), (5, 4000)]:
+        x = rng.standard_normal((S, T)) + 10
+        s = rng.uniform(0.05, 0.95, S)
+        xd = dev(torch, x)
+        out = torch.empty_like(xd)
+        EWMAModel(dev(torch, s)).addTimeDependentEffects(xd, out)
+        assert_bits(host(out), np.array([oracle.ewma_add(r, v) for r, v in zip(x, s)]), "add")
+        EWMAModel(dev(torch, s)).removeTimeDependentEffects(xd, out)
+        assert_bits(host(out), np.array([oracle.ewma_remove(r, v) for r, v in zip(x, s)]), "remove")
+        # in place: add is safe; remove reads overwritten values (reference aliasing)
+        ip = dev(torch, x)
+        EWMAModel(dev(torch, s)).removeTimeDependentEffects(ip, ip)
+        ref = []
+        for r, v in zip(x, s):
+            rr = r.copy(); oracle.ewma_remove(rr, v, dest=rr); ref.append(rr)
+        assert_bits(host(ip), np.array(ref), "remove in place")
+    with pytest.raises(NullPointerException):
+        EWMAModel(0.2).removeTimeDependentEffects(dev(torch, [1.0, 2.0]))
+
+
+# ---------------- AR (a11-a13) ----------------
+
+def test_ar_fit_reference_suite(torch):
+    # T/models/AutoregressionSuite.scala:25-42, inputs from MersenneTwister(10)
+    from mt19937 import MersenneTwister
+    from sparkts.models import Autoregression
+    for coefs, tol_c in (([0.2], 0.07), ([0.2, 0.3], 0.15)):
+        rand = MersenneTwister(10)
+        ts = oracle.ar_add(np.array([rand.next_gaussian() for _ in range(5000)]), 1.5, coefs, inplace=True)
+        m = Autoregression.fitModel(dev(torch, ts), len(coefs))
+        rc, rcoef = oracle.ar_fit(ts, len(coefs))
+        assert abs(m.c - 1.5) < tol_c
+        got = host(m.coefficients)
+        for g, want in zip(got, coefs):
+            assert abs(g - want) < 0.03
+        assert_rel([m.c, *got], [rc, *rcoef])
+
+
+@pytest.mark.parametrize("p", [1, 2, 5, 8, 16, 17, 31])
+@pytest.mark.parametrize("no_intercept", [False, True])
+def test_ar_fit_panels(torch, p, no_intercept):
+    from sparkts.models import Autoregression
+    S, T = 24, 2520
+    x = oracle.gen_ar_panel(4, S, T, min(p, 5))
+    if p > 5:
+        x = x + 0.01 * np.sin(np.arange(T))[None, :]
+    m = Autoregression.fitModel(dev(torch, x), p, no_intercept)
+    rc = np.empty(S); rcoef = np.empty((S, p))
+    for s in range(S):
+        rc[s], rcoef[s] = oracle.ar_fit(x[s], p, no_intercept)
+    assert_rel(host(m.coefficients), rcoef, what="coef")
+    if not no_intercept:
+        assert_rel(host(m.c), rc, what="c")
+
+
+def test_ar_fit_long_series_unstaged(torch):
+    from sparkts.models import Autoregression
+    x = oracle.gen_ar_panel(9, 4, 10000, 5)
+    m = Autoregression.fitModel(dev(torch, x), 5)
+    for s in range(4):
+        rc, rcoef = oracle.ar_fit(x[s], 5)
+        assert_rel(host(m.coefficients)[s], rcoef)
+        assert_rel(host(m.c)[s], rc)
+
+
+def test_ar_not_enough_data(torch):
+    from sparkts.models import Autoregression
+    from sparkts.errors import MathIllegalArgumentException
+    with pytest.raises(MathIllegalArgumentException):
+        Autoregression.fitModel(dev(torch, [1.0, 2.0, 3.0, 4.0]), 2)
+
+
+def test_ar_remove_add_bit_exact(torch):
+    from sparkts.models import ARModel
+    rng = np.random.default_rng(11)
+    for p in (1, 2, 5, 16, 33):
+        S, T = 9, 1000
+        x = rng.standard_normal((S, T))
+        c = rng.standard_normal(S)
+        coef = rng.uniform(-0.3, 0.3, (S, p))
+        m = ARModel(dev(torch, c), dev(torch, coef))
+        xd = dev(torch, x)
+        rem = host(m.removeTimeDependentEffects(xd))
+        add = host(m.addTimeDependentEffects(xd))
+        assert_bits(rem, np.array([oracle.ar_remove(x[s], c[s], coef[s]) for s in range(S)]), "remove p=%d" % p)
+        assert_bits(add, np.array([oracle.ar_add(x[s], c[s], coef[s]) for s in range(S)]), "add p=%d" % p)
+        # in-place remove reads overwritten values; in-place add equals out-of-place
+        ip = dev(torch, x)
+        m.removeTimeDependentEffects(ip, ip)
+        ref = []
+        for s in range(S):
+            r = x[s].copy()
+            for i in range(T):
+                v = r[i] - c[s]
+                for j in range(min(p, i)):
+                    v -= r[i - j - 1] * coef[s, j]
+                r[i] = v
+            ref.append(r)
+        assert_bits(host(ip), np.array(ref), "remove in place p=%d" % p)
+
+
+def test_ar_add_remove_round_trip(torch):
+    # T/models/AutoregressionSuite.scala:44-51
+    from sparkts.models import ARModel
+    ts = np.random.default_rng(0).random(1000)
+    m = ARModel(1.5, [0.2, 0.3])
+    added = m.addTimeDependentEffects(dev(torch, ts))
+    removed = host(m.removeTimeDependentEffects(added))
+    assert np.all(np.abs(ts - removed) < 1e-3)
+
+
+def test_ar_fit_remove_fused(torch):
+    from sparkts.models import Autoregression
+    S, T, p = 40, 2520, 5
+    x = oracle.gen_ar_panel(4, S, T, p)
+    m, resid = Autoregression.fitModelAndRemove(dev(torch, x), p)
+    c, coef = host(m.c), host(m.coefficients)
+    ref_resid = np.array([oracle.ar_remove(x[s], c[s], coef[s]) for s in range(S)])
+    assert_bits(host(resid), ref_resid)   # bit-exact given the fitted model
+    _, rc, rcoef = oracle.panel_ar_fit_remove(x, p)
+    assert_rel(coef, rcoef)
+    assert_rel(c, rc)
+
+
+# ---------------- C2 fused pipeline: bit-exact ----------------
+
+@pytest.mark.parametrize("lag", [1, 3])
+def test_fill_diff_ewma(torch, lag):
+    from sparkts import _native
+    S, T = 300, 390
+    x = oracle.gen_panel(2, S, T, 0.05)
+    x[3, :40] = NaN
+    s = np.full(S, 0.2)
+    xd = dev(torch, x)
+    out = torch.empty_like(xd)
+    assert _native.lib().sts_fill_diff_ewma(xd.data_ptr(), out.data_ptr(), S, T, T, T, 3, lag,
+                                            dev(torch, s).data_ptr(), None, None) == 0
+    ref = []
+    for r in x:
+        f = oracle.fill_previous(r)
+        d = oracle.differences_at_lag(f, lag)
+        ref.append(oracle.ewma_add(d, 0.2))
+    assert_bits(host(out), np.array(ref))
+
+
+# ---------------- generator ----------------
+
+def test_generator_matches_cpu(torch):
+    from sparkts import _native
+    lib = _native.lib()
+    S, T = 37, 1001
+    out = torch.empty((S, T), dtype=torch.float64, device="cuda:0")
+    assert lib.sts_gen_panel(out.data_ptr(), 5, S, T, T, 123, 0.3, None) == 0
+    assert_bits(host(out), oracle.gen_panel(123, S, T, 0.3, s0=5))
+    c = torch.empty(S, dtype=torch.float64, device="cuda:0")
+    phi = torch.empty((S, 5), dtype=torch.float64, device="cuda:0")
+    assert lib.sts_gen_ar_panel(out.data_ptr(), c.data_ptr(), phi.data_ptr(), 5, S, T, T, 77, 5, None) == 0
+    assert_bits(host(out), oracle.gen_ar_panel(77, S, T, 5, s0=5))
