@@ -133,6 +133,7 @@ int method_ok(int method, bool allow_none, const char* name) {
 }
 
 int tile_width(int64_t T) { return T <= 512 ? 512 : 4096; }
+constexpr int64_t kTilesPerChunk = 16;  // tiles per workgroup (prefetch pipeline depth 1)
 
 // Measurement hook (bench.py): HIP events recorded on the launch stream around every
 // tile-kernel launch of this thread while profiling is on.
@@ -168,13 +169,15 @@ int run_tile(const double* in, double* out, double* lagmat, int64_t S, int64_t T
     a.ld_in = ld_in;
     a.ld_out = ld_out;
     a.tiles_per_series = (T + tw - 1) / tw;
+    a.tiles_per_chunk = a.tiles_per_series < kTilesPerChunk ? a.tiles_per_series : kTilesPerChunk;
+    a.chunks_per_series = (a.tiles_per_series + a.tiles_per_chunk - 1) / a.tiles_per_chunk;
     a.K = K;
     a.max_lag = max_lag;
     a.include_original = inc;
-    if (S * a.tiles_per_series > 0x7fffffffLL) return fail(STS_ERR_BAD_ARG, "%s: panel too large for one launch", name);
+    if (S * a.chunks_per_series > 0x7fffffffLL) return fail(STS_ERR_BAD_ARG, "%s: panel too large for one launch", name);
     Scratch part(st);
     if (K > 0) {
-        hipError_t e = part.alloc((size_t)(S * a.tiles_per_series) * sts::kPartStride * sizeof(double));
+        hipError_t e = part.alloc((size_t)(S * a.chunks_per_series) * sts::kPartStride * sizeof(double));
         if (e != hipSuccess) return hip_fail(e, "hipMallocAsync(partials)");
         a.partials = static_cast<double*>(part.p);
     }
@@ -190,7 +193,7 @@ int run_tile(const double* in, double* out, double* lagmat, int64_t S, int64_t T
         f.S = S;
         f.T = T;
         f.ldF = out ? ld_out : ld_in;
-        f.tiles_per_series = a.tiles_per_series;
+        f.parts_per_series = a.chunks_per_series;
         f.K = K;
         e = sts::launch_acf_finalize(f, st);
         if (e != hipSuccess) return hip_fail(e, "acf finalize");

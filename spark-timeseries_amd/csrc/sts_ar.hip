@@ -11,8 +11,9 @@
 // the series ends.  P_0..P_p come from v_mfma_f64_16x16x4_f64 rank-4 updates exactly as
 // in the autocorrelation tile kernel (rows of 16 steps, U_t = sum_a A_a^T A_{a+t}).
 // The data are centred first (y = x - mean, exact algebra for the intercept model), the
-// intercept is eliminated (centred normal equations) and the p x p system is solved by
-// Cholesky in fp64; agreement with the Householder solution is ~cond(C) * 1e-16.
+// intercept is eliminated (centred normal equations), the p x p system is solved by
+// Cholesky in fp64 and one step of iterative refinement against an exact residual pass
+// (corrected semi-normal equations) brings the error back to Householder-QR level.
 #include "sts_internal.hpp"
 
 #include <hip/hip_runtime.h>
@@ -24,15 +25,16 @@ typedef double d4 __attribute__((ext_vector_type(4)));
 constexpr int kPMax = 31;
 constexpr int kLd = kPMax + 2;   // row stride of the (p+1) x (p+1) Gram in LDS
 
-template <bool STAGED>
+template <bool STAGED, int PB>
 __global__ __launch_bounds__(64) void ar_fit_kernel(ArArgs a, int NT) {
     extern __shared__ __attribute__((aligned(16))) double lds[];
     double* scr = lds;                       // 256: one U_t tile
     double* lagp = scr + 256;                // 64: P_d
     double* G = lagp + 64;                   // (p+1) x kLd
     double* cs = G + (kPMax + 1) * kLd;      // p+1 column sums (+1 pad)
-    double* sol = cs + kPMax + 2;            // c, coef[p] (+pad)
-    double* sx = sol + kPMax + 3;            // staged series (T doubles), 16-B aligned offset
+    double* sol = cs + kPMax + 2;            // c, coef[p], status
+    double* zz = sol + kPMax + 4;            // refinement: gradient (kPMax + 2) | solve (kPMax + 2)
+    double* sx = zz + 2 * (kPMax + 2);       // staged series (T doubles)
     const int lane = threadIdx.x;
     const int64_t s = blockIdx.x;
     const int64_t T = a.T;
@@ -107,67 +109,111 @@ __global__ __launch_bounds__(64) void ar_fit_kernel(ArArgs a, int NT) {
     }
     __syncthreads();
 
-    // ---- centred normal equations + Cholesky (lane 0) ----
-    if (lane == 0) {
+    // ---- centred normal equations + Cholesky (lane 0), then one step of iterative
+    //      refinement with an exact residual pass (corrected semi-normal equations:
+    //      recovers the Householder-QR accuracy the normal equations lose to cond^2) ----
+    const bool intercept = !a.no_intercept;
+    const double fm = (double)m;
+    const bool bad = __builtin_isnan(sy) || __builtin_isnan(part);
+    if (lane == 0 && !bad) {
         int status = STS_OK;
-        double coef[kPMax];
-        double cst = 0.0;
-        if (__builtin_isnan(sy) || __builtin_isnan(part)) {
-            for (int j = 0; j < p; j++) coef[j] = __builtin_nan("");
-            cst = __builtin_nan("");
-        } else {
-            const double fm = (double)m;
-            // A = C (p x p) in G[1..p][1..p], rhs in G[0][1..p]
-            if (!a.no_intercept) {
-                for (int j = 1; j <= p; j++) {
-                    for (int k = 1; k <= p; k++) G[j * kLd + k] -= cs[j] * cs[k] / fm;
-                    G[0 * kLd + j] -= cs[0] * cs[j] / fm;
-                }
-            }
-            // Cholesky in place on the lower triangle of A (1-based block)
-            for (int j = 1; j <= p && status == STS_OK; j++) {
-                double d = G[j * kLd + j];
-                for (int k = 1; k < j; k++) d -= G[j * kLd + k] * G[j * kLd + k];
-                if (!(d > 0.0)) { status = STS_ERR_SINGULAR; break; }
-                const double l = __builtin_sqrt(d);
-                G[j * kLd + j] = l;
-                for (int i = j + 1; i <= p; i++) {
-                    double v = G[i * kLd + j];
-                    for (int k = 1; k < j; k++) v -= G[i * kLd + k] * G[j * kLd + k];
-                    G[i * kLd + j] = v / l;
-                }
-            }
-            if (status == STS_OK) {
-                double z[kPMax];
-                for (int i = 1; i <= p; i++) {
-                    double v = G[0 * kLd + i];
-                    for (int k = 1; k < i; k++) v -= G[i * kLd + k] * z[k - 1];
-                    z[i - 1] = v / G[i * kLd + i];
-                }
-                for (int i = p; i >= 1; i--) {
-                    double v = z[i - 1];
-                    for (int k = i + 1; k <= p; k++) v -= G[k * kLd + i] * coef[k - 1];
-                    coef[i - 1] = v / G[i * kLd + i];
-                }
-                if (a.no_intercept) {
-                    cst = 0.0;
-                } else {
-                    double sphi = 0.0, sc = cs[0];
-                    for (int k = 1; k <= p; k++) {
-                        sphi += coef[k - 1];
-                        sc -= coef[k - 1] * cs[k];
-                    }
-                    cst = sc / fm + mu * (1.0 - sphi);
-                }
-            } else {
-                for (int j = 0; j < p; j++) coef[j] = __builtin_nan("");
-                cst = __builtin_nan("");
+        if (intercept) {
+            for (int j = 1; j <= p; j++) {
+                for (int k = 1; k <= p; k++) G[j * kLd + k] -= cs[j] * cs[k] / fm;
+                G[0 * kLd + j] -= cs[0] * cs[j] / fm;
             }
         }
-        a.c[s] = cst;
-        for (int j = 0; j < p; j++) a.coef[s * p + j] = coef[j];
-        sol[0] = cst;
-        for (int j = 0; j < p; j++) sol[1 + j] = coef[j];
+        // Cholesky in place on the lower triangle of the 1-based p x p block
+        for (int j = 1; j <= p && status == STS_OK; j++) {
+            double d = G[j * kLd + j];
+            for (int k = 1; k < j; k++) d -= G[j * kLd + k] * G[j * kLd + k];
+            if (!(d > 0.0)) { status = STS_ERR_SINGULAR; break; }
+            const double l = __builtin_sqrt(d);
+            G[j * kLd + j] = l;
+            for (int i = j + 1; i <= p; i++) {
+                double v = G[i * kLd + j];
+                for (int k = 1; k < j; k++) v -= G[i * kLd + k] * G[j * kLd + k];
+                G[i * kLd + j] = v / l;
+            }
+        }
+        sol[kPMax + 2] = (double)status;
+        if (status == STS_OK) {
+            // rhs in row 0; solution phi -> sol[1..p], centred intercept -> sol[0]
+            for (int i = 1; i <= p; i++) {
+                double v = G[0 * kLd + i];
+                for (int k = 1; k < i; k++) v -= G[i * kLd + k] * sol[k];
+                sol[i] = v / G[i * kLd + i];
+            }
+            for (int i = p; i >= 1; i--) {
+                double v = sol[i];
+                for (int k = i + 1; k <= p; k++) v -= G[k * kLd + i] * sol[k];
+                sol[i] = v / G[i * kLd + i];
+            }
+            double sc = cs[0];
+            for (int k = 1; k <= p; k++) sc -= sol[k] * cs[k];
+            sol[0] = intercept ? sc / fm : 0.0;
+        }
+    }
+    __syncthreads();
+    const int status = bad ? STS_OK : (int)sol[kPMax + 2];
+    if (!bad && status == STS_OK) {
+        // residual pass: e_r = Y_r - c' - sum_k phi_k X_k(r); g = [sum e, sum e X_k]
+        double g[PB + 1];
+#pragma unroll
+        for (int k = 0; k <= PB; k++) g[k] = 0.0;
+        const double cpr = sol[0];
+        for (int64_t r = lane; r < m; r += 64) {
+            double e = Y(r + p) - cpr;
+#pragma unroll
+            for (int k = 1; k <= PB; k++)
+                if (k <= p) e -= sol[k] * Y(r + p - k);
+            g[0] += e;
+#pragma unroll
+            for (int k = 1; k <= PB; k++)
+                if (k <= p) g[k] += e * Y(r + p - k);
+        }
+#pragma unroll
+        for (int k = 0; k <= PB; k++) {
+            if (k <= p) {
+#pragma unroll
+                for (int d = 32; d >= 1; d >>= 1) g[k] += __shfl_xor(g[k], d);
+            }
+        }
+#pragma unroll
+        for (int k = 0; k <= PB; k++)
+            if (lane == 0 && k <= p) zz[k] = g[k];
+        if (lane == 0) {
+            double* gg = zz;                 // gradient g[0..p]
+            double* z = zz + (kPMax + 2);    // correction z[1..p]
+            const double g0 = gg[0];
+            for (int i = 1; i <= p; i++) {
+                double v = gg[i] - (intercept ? cs[i] * g0 / fm : 0.0);
+                for (int k = 1; k < i; k++) v -= G[i * kLd + k] * z[k];
+                z[i] = v / G[i * kLd + i];
+            }
+            for (int i = p; i >= 1; i--) {
+                double v = z[i];
+                for (int k = i + 1; k <= p; k++) v -= G[k * kLd + i] * z[k];
+                z[i] = v / G[i * kLd + i];
+            }
+            double dc = g0;
+            for (int k = 1; k <= p; k++) dc -= z[k] * cs[k];
+            double sphi = 0.0;
+            for (int k = 1; k <= p; k++) {
+                sol[k] += z[k];
+                sphi += sol[k];
+            }
+            // un-shift: y = x - mu  =>  c = c' + mu * (1 - sum phi)
+            sol[0] = intercept ? (sol[0] + dc / fm) + mu * (1.0 - sphi) : 0.0;
+        }
+    }
+    if (lane == 0) {
+        if (bad || status != STS_OK) {
+            sol[0] = __builtin_nan("");
+            for (int j = 1; j <= p; j++) sol[j] = __builtin_nan("");
+        }
+        a.c[s] = sol[0];
+        for (int j = 0; j < p; j++) a.coef[s * p + j] = sol[1 + j];
         if (a.err) a.err[s] = status;
     }
     if (!a.out) return;
@@ -189,14 +235,14 @@ hipError_t launch_ar_fit(const ArArgs& a, hipStream_t st) {
     if (a.S <= 0) return hipSuccess;
     if (a.p < 1 || a.p > kPMax) return hipErrorInvalidValue;
     const int NT = (a.p + 15) / 16 + 1;
-    const size_t fixed = (256 + 64 + (kPMax + 1) * kLd + (kPMax + 2) + (kPMax + 3)) * sizeof(double);
+    const size_t fixed = (256 + 64 + (kPMax + 1) * kLd + (kPMax + 2) + (kPMax + 4) + 2 * (kPMax + 2)) * sizeof(double);
     dim3 grid((unsigned)a.S), block(64);
-    if (a.T <= 6144) {
-        const size_t bytes = fixed + (size_t)a.T * sizeof(double);
-        hipLaunchKernelGGL((ar_fit_kernel<true>), grid, block, bytes, st, a, NT);
-    } else {
-        hipLaunchKernelGGL((ar_fit_kernel<false>), grid, block, fixed, st, a, NT);
-    }
+    const bool staged = a.T <= 6144;
+    const size_t bytes = fixed + (staged ? (size_t)a.T * sizeof(double) : 0);
+    if (staged && a.p <= 8) hipLaunchKernelGGL((ar_fit_kernel<true, 8>), grid, block, bytes, st, a, NT);
+    else if (staged) hipLaunchKernelGGL((ar_fit_kernel<true, kPMax>), grid, block, bytes, st, a, NT);
+    else if (a.p <= 8) hipLaunchKernelGGL((ar_fit_kernel<false, 8>), grid, block, bytes, st, a, NT);
+    else hipLaunchKernelGGL((ar_fit_kernel<false, kPMax>), grid, block, bytes, st, a, NT);
     return hipGetLastError();
 }
 

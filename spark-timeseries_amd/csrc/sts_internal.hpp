@@ -24,6 +24,8 @@ struct TileArgs {
     int32_t* err;         // per-series error flags (may be null)
     int64_t S, T, ld_in, ld_out;
     int64_t tiles_per_series;
+    int64_t tiles_per_chunk;    // tiles one workgroup walks (register-prefetched pipeline)
+    int64_t chunks_per_series;  // = ceil(tiles_per_series / tiles_per_chunk)
     int K;                // ACF lags (0 = no ACF)
     int max_lag;          // lag matrix p
     int include_original; // lag matrix inc
@@ -33,7 +35,7 @@ struct FinalizeArgs {
     const double* F;      // filled series (or raw input when no fill), ld = ldF
     const double* partials;
     double* acf;          // S x K
-    int64_t S, T, ldF, tiles_per_series;
+    int64_t S, T, ldF, parts_per_series;   // ACF partials per series (one per chunk)
     int K;
 };
 

@@ -73,248 +73,342 @@ __device__ int64_t scan_fwd(const double* src, int64_t from, int64_t T, int lane
 }
 
 template <int TW, int NT>
-__global__ __launch_bounds__(kThreads) void tile_kernel(TileArgs a, int method) {
+__global__ __launch_bounds__(kThreads, 3) void tile_kernel(TileArgs a, int method) {
     constexpr int EW = kHB + TW + kHA;
     constexpr int NW = EW / 64;
+    constexpr int NP2 = EW / 2;                              // double2 per extended tile
+    constexpr int RPT = (NP2 + kThreads - 1) / kThreads;     // prefetch registers per thread
     static_assert(EW % 64 == 0, "extended tile must be whole words");
     static_assert(NW <= 128, "word scan handles at most 128 words");
     __shared__ __attribute__((aligned(16))) double vals[EW];
     __shared__ unsigned long long mask[NW];
-    __shared__ int lastUpTo[NW];
-    __shared__ int firstFrom[NW];
-    __shared__ int64_t sh_i[2];
-    __shared__ double sh_d[3];
+    __shared__ int lastUpTo[NW];     // last valid E-position in words <= w (-1: none)
+    __shared__ int firstFrom[NW];    // first valid E-position in words >= w (kBig: none)
+    __shared__ unsigned short nanpos[EW];   // compacted NaN positions of the tile
+    __shared__ int sh_i[3];          // lext, next (series positions), NaN count
+    __shared__ double sh_d[3];       // c0, value at lext, value at next
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = tid >> 6;
-    const int64_t ntiles = a.S * a.tiles_per_series;
-    const int64_t tile = xcd_remap(blockIdx.x, ntiles);
-    const int64_t s = tile / a.tiles_per_series;
-    const int64_t k = tile - s * a.tiles_per_series;
+    // one workgroup = one CHUNK of tiles_per_chunk consecutive tiles of one series
+    const int64_t nchunk = a.S * a.chunks_per_series;
+    const int64_t ch = xcd_remap(blockIdx.x, nchunk);
+    const int64_t s = ch / a.chunks_per_series;
+    const int64_t cidx = ch - s * a.chunks_per_series;
+    const int64_t k_begin = cidx * a.tiles_per_chunk;
+    const int64_t k_end = (k_begin + a.tiles_per_chunk < a.tiles_per_series) ? k_begin + a.tiles_per_chunk
+                                                                              : a.tiles_per_series;
     const int64_t T = a.T;
-    const int64_t t0 = k * TW;
-    const int64_t t1 = (t0 + TW < T) ? t0 + TW : T;
-    const int64_t e0 = t0 - kHB;
     const double* src = a.in + s * a.ld_in;
-
-    // ---- 1. stage E = [e0, e0 + EW) in LDS (NaN outside the series) ----
-    {
-        const bool interior = (e0 >= 0) && (e0 + EW <= T) && ((reinterpret_cast<uintptr_t>(src) & 15) == 0);
-        if (interior) {
-            const double2* s2 = reinterpret_cast<const double2*>(src + e0);
-            double2* v2 = reinterpret_cast<double2*>(vals);
-            constexpr int kFull = (EW / 2) / kThreads;      // whole rounds
-#pragma unroll
-            for (int j = 0; j < kFull; j++) v2[tid + j * kThreads] = s2[tid + j * kThreads];
-            if (kFull * kThreads + tid < EW / 2) v2[kFull * kThreads + tid] = s2[kFull * kThreads + tid];
-        } else {
-            for (int q = tid; q < EW; q += kThreads) {
-                int64_t t = e0 + q;
-                vals[q] = (t >= 0 && t < T) ? src[t] : __builtin_nan("");
-            }
-        }
-    }
-    __syncthreads();
-
-    // ---- 2. validity ballots, one 64-bit word per 64 steps ----
-    for (int w = wave; w < NW; w += kWaves) {
-        unsigned long long m = __ballot(!isnan_d(vals[w * 64 + lane]));
-        if (lane == 0) mask[w] = m;
-    }
-    __syncthreads();
-
-    // positions to produce: [qA, qB) (E-relative); ACF needs 16*NT steps past the tile
-    const int qA = kHB;
-    const int qW = kHB + (int)(t1 - t0);                       // end of the written range
-    int qB = qW + (NT > 0 ? 16 * NT : 0);
-    if (e0 + qB > T) qB = (int)(T - e0);
+    const bool src_al = (reinterpret_cast<uintptr_t>(src) & 15) == 0;
     const bool needL = (method == STS_FILL_LINEAR || method == STS_FILL_PREVIOUS || method == STS_FILL_NEAREST);
     const bool needN = (method == STS_FILL_LINEAR || method == STS_FILL_NEXT || method == STS_FILL_NEAREST);
-
-    // ---- 3. word-level scans (wave 0) + slow paths + ACF shift ----
-    if (wave == 0) {
-        const int w0 = 2 * lane, w1 = 2 * lane + 1;
-        unsigned long long m0 = (w0 < NW) ? mask[w0] : 0ull;
-        unsigned long long m1 = (w1 < NW) ? mask[w1] : 0ull;
-        int l0 = m0 ? w0 * 64 + 63 - __clzll(m0) : -1;
-        int l1 = m1 ? w1 * 64 + 63 - __clzll(m1) : -1;
-        int f0 = m0 ? w0 * 64 + __ffsll(m0) - 1 : kBig;
-        int f1 = m1 ? w1 * 64 + __ffsll(m1) - 1 : kBig;
-        int incl = l1 > l0 ? l1 : l0;         // max over my two words
-        int fmin = f0 < f1 ? f0 : f1;         // min over my two words
-        // inclusive prefix max over lanes
-        int pm = incl;
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            int o = __shfl_up(pm, d);
-            if (lane >= d) pm = o > pm ? o : pm;
-        }
-        int ex = __shfl_up(pm, 1);
-        if (lane == 0) ex = -1;
-        // inclusive suffix min over lanes
-        int sm = fmin;
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            int o = __shfl_down(sm, d);
-            if (lane + d < 64) sm = o < sm ? o : sm;
-        }
-        int exs = __shfl_down(sm, 1);
-        if (lane == 63) exs = kBig;
-        if (w0 < NW) {
-            lastUpTo[w0] = ex > l0 ? ex : l0;
-            int a0 = f1 < exs ? f1 : exs;
-            firstFrom[w0] = f0 < a0 ? f0 : a0;
-        }
-        if (w1 < NW) {
-            int a1 = ex > l0 ? ex : l0;
-            lastUpTo[w1] = a1 > l1 ? a1 : l1;
-            firstFrom[w1] = f1 < exs ? f1 : exs;
-        }
-        const int firstValidE = __shfl(sm, 0);     // min over all words
-        const int lastValidE = __shfl(pm, 63);     // max over all words
-        int64_t lext = -1, next = T;
-        if (needL && e0 > 0 && firstValidE > qA) lext = scan_back(src, e0, lane);
-        if (needN && e0 + EW < T && qB > qA && lastValidE < qB - 1) next = scan_fwd(src, e0 + EW, T, lane);
-        double c0 = 0.0;
-        if (NT > 0) {
-            double x0 = src[0];
-            if (method == STS_FILL_NEXT && isnan_d(x0)) {
-                int64_t f = scan_fwd(src, 0, T, lane);
-                x0 = (f < T) ? src[f] : __builtin_nan("");
-            }
-            c0 = x0;
-        }
-        if (lane == 0) {
-            sh_i[0] = lext;
-            sh_i[1] = next;
-            sh_d[0] = (lext >= 0) ? src[lext] : 0.0;
-            sh_d[1] = (next < T) ? src[next] : 0.0;
-            sh_d[2] = c0;
-        }
-    }
-    __syncthreads();
-
-    const int64_t lext = sh_i[0], next = sh_i[1];
-    const double lextv = sh_d[0], nextv = sh_d[1], c0 = sh_d[2];
-    bool series_err = false;
-
-    // value of the filled series at E-position q (t = e0 + q < T)
-    auto fill_at = [&](int q) -> double {
-        double v = vals[q];
-        if (method == STS_FILL_NONE || !isnan_d(v)) return v;
-        const int64_t t = e0 + q;
-        const int w = q >> 6, b = q & 63;
-        int64_t Lt = -1, Nt = T;
-        double Lv = 0.0, Nv = 0.0;
-        if (needL) {
-            unsigned long long m = mask[w] & (((2ull << b)) - 1ull);
-            int Lq = m ? w * 64 + 63 - __clzll(m) : (w > 0 ? lastUpTo[w - 1] : -1);
-            if (Lq >= 0) { Lt = e0 + Lq; Lv = vals[Lq]; }
-            else { Lt = lext; Lv = lextv; }
-        }
-        if (needN) {
-            unsigned long long m = mask[w] & (~0ull << b);
-            int Nq = m ? w * 64 + __ffsll(m) - 1 : (w + 1 < NW ? firstFrom[w + 1] : kBig);
-            if (Nq < kBig) { Nt = e0 + Nq; Nv = vals[Nq]; }
-            else { Nt = next; Nv = nextv; }
-        }
-        switch (method) {
-        case STS_FILL_PREVIOUS:
-            return Lt >= 0 ? Lv : __builtin_nan("");
-        case STS_FILL_NEXT:
-            return Nt < T ? Nv : __builtin_nan("");
-        case STS_FILL_NEAREST: {
-            if (t == 0) return v;                     // index 0 is never modified
-            const int64_t P = (Lt >= 1) ? Lt : -1;    // index 0 is never a previous source
-            if (P < 0 && Nt >= T) { series_err = true; return v; }
-            if (Nt >= T || (P >= 0 && t - P < Nt - t)) return Lv;   // ties go to next
-            return Nv;
-        }
-        case STS_FILL_LINEAR: {
-            if (Lt < 0 || Nt >= T) return v;          // runs touching index 0 or n-1 stay NaN
-            const double inc = (Nv - Lv) / (double)(int)(Nt - Lt);
-            double r = Lv;
-            for (int64_t j = Lt + 1; j <= t; j++) r = r + inc;   // sequential, as :259-261
-            return r;
-        }
-        default:
-            return v;
-        }
-    };
-
-    // ---- 4. produce F on [qA, qB): write filled output / lag matrix ----
-    // F is written back into vals IN PLACE at NaN positions only: every (L, N) source
-    // read by another thread is a valid position, whose value never changes.
     double* dst = a.out ? a.out + s * a.ld_out : nullptr;
-    const bool dst_al = dst && ((reinterpret_cast<uintptr_t>(dst) & 15) == 0);
     const int64_t lrows = T - a.max_lag;
     const int ncols = a.max_lag + (a.include_original ? 1 : 0);
     const int init = a.include_original ? 0 : 1;
-    for (int q = qA + 2 * tid; q < qB; q += 2 * kThreads) {
-        const double v0 = vals[q];
-        const double v1 = (q + 1 < qB) ? vals[q + 1] : 0.0;
-        const double f0 = isnan_d(v0) ? fill_at(q) : v0;
-        const double f1 = (q + 1 < qB && isnan_d(v1)) ? fill_at(q + 1) : v1;
-        const int64_t t = e0 + q;
-        if (dst && q < qW) {
-            if (dst_al && q + 1 < qW) {
-                *reinterpret_cast<double2*>(dst + t) = make_double2(f0, f1);
-            } else {
-                dst[t] = f0;
-                if (q + 1 < qW) dst[t + 1] = f1;
+
+    // ACF shift c0 = F(0), once per workgroup (before any prefetch is in flight)
+    double c0 = 0.0;
+    if (NT > 0) {
+        if (wave == 0) {
+            double x0 = src[0];
+            if (method == STS_FILL_NEXT && isnan_d(x0)) {
+                const int64_t f = scan_fwd(src, 0, T, lane);
+                x0 = (f < T) ? src[f] : __builtin_nan("");
             }
+            if (lane == 0) sh_d[0] = x0;
         }
-        if (a.lagmat && q < qW) {
-            double* lm = a.lagmat + s * lrows * ncols;
-            for (int c = init; c <= a.max_lag; c++) {
-                double* col = lm + (int64_t)(c - init) * lrows;
-                const int64_t r0 = t - a.max_lag + c;
-                if (r0 >= 0 && r0 < lrows) col[r0] = f0;
-                if (q + 1 < qW && r0 + 1 >= 0 && r0 + 1 < lrows) col[r0 + 1] = f1;
-            }
-        }
-        if (NT > 0) {
-            if (isnan_d(v0)) vals[q] = f0;
-            if (q + 1 < qB && isnan_d(v1)) vals[q + 1] = f1;
-        }
+        __syncthreads();
+        c0 = sh_d[0];
+        __syncthreads();
     }
+
+    // register prefetch of one INTERIOR extended tile [e0, e0 + EW); the first and last tile
+    // of a series (which touch its ends) are loaded synchronously with bounds checks
+    static_assert(RPT <= 9, "prefetch registers are spelled out for RPT <= 9");
+    double2 R0, R1, R2, R3, R4, R5, R6, R7, R8;   // named: an array here ends up in scratch
+    auto interior = [&](int64_t kk) {
+        const int64_t e0 = kk * TW - kHB;
+        return e0 >= 0 && e0 + EW <= T && src_al;
+    };
+    // (a macro, not a lambda: a captured register array would be forced to scratch)
+#define STS_LD1(j)                                                                          \
+    if constexpr (j < RPT) {                                                                \
+        const int q2_ = tid + j * kThreads;                                                 \
+        R##j = s2_[q2_ < NP2 ? q2_ : NP2 - 1];                                              \
+    }
+#define STS_ISSUE(kk)                                                                       \
+    do {                                                                                    \
+        const double2* s2_ = reinterpret_cast<const double2*>(src + ((kk) * TW - kHB));     \
+        STS_LD1(0) STS_LD1(1) STS_LD1(2) STS_LD1(3) STS_LD1(4)                              \
+        STS_LD1(5) STS_LD1(6) STS_LD1(7) STS_LD1(8)                                         \
+    } while (0)
+// define R on the no-prefetch path too, so the registers are dead between their store to
+// LDS and the next issue (otherwise the loop-carried values stay live across the body)
+#define STS_CLEAR()                                                                         \
+    do {                                                                                    \
+        R0 = R1 = R2 = R3 = R4 = R5 = R6 = R7 = R8 = make_double2(0.0, 0.0);                \
+    } while (0)
+#define STS_ST1(j)                                                                          \
+    if constexpr (j < RPT) {                                                                \
+        const int q2_ = tid + j * kThreads;                                                 \
+        if (q2_ < NP2) v2_[q2_] = R##j;                                                     \
+    }
+
+    d4 U[NT > 0 ? NT : 1];
+#pragma unroll
+    for (int t = 0; t < (NT > 0 ? NT : 1); t++) U[t] = d4{0.0, 0.0, 0.0, 0.0};
+    double sy = 0.0;
+    bool series_err = false;
+
+    bool have = interior(k_begin);
+    if (have) STS_ISSUE(k_begin);
+    else STS_CLEAR();
+    for (int64_t k = k_begin; k < k_end; k++) {
+        const int t0 = (int)(k * TW);
+        const int t1 = (t0 + TW < T) ? t0 + TW : (int)T;
+        const int e0 = t0 - kHB;
+
+        // ---- 1. prefetched registers (or a bounds-checked edge load) -> LDS ----
+        if (have) {
+            double2* v2_ = reinterpret_cast<double2*>(vals);
+            STS_ST1(0) STS_ST1(1) STS_ST1(2) STS_ST1(3) STS_ST1(4) STS_ST1(5) STS_ST1(6) STS_ST1(7) STS_ST1(8)
+        } else {
+            for (int q = tid; q < EW; q += kThreads) {
+                const int t = e0 + q;
+                vals[q] = (t >= 0 && t < T) ? src[t] : __builtin_nan("");
+            }
+        }
+        const bool have_next = (k + 1 < k_end) && interior(k + 1);
+        __syncthreads();
+
+        // positions to produce: [qA, qB) (E-relative); the ACF needs 16*NT steps past the tile
+        const int qA = kHB;
+        const int qW = kHB + (t1 - t0);                  // end of the written range
+        int qB = qW + (NT > 0 ? 16 * NT : 0);
+        if (e0 + qB > T) qB = (int)T - e0;
+
+        // ---- 2. validity ballots (wave v owns words v, v+4, ...) ----
+#pragma unroll 2
+        for (int i = 0; i < (NW + kWaves - 1) / kWaves; i++) {
+            const int w = wave + i * kWaves;
+            if (w < NW) {
+                const unsigned long long m = __ballot(!isnan_d(vals[w * 64 + lane]));
+                if (lane == 0) mask[w] = m;
+            }
+        }
+        __syncthreads();
+
+        // ---- 3. word scans in every wave (lane l: words 2l, 2l+1): last/first valid
+        //      position around each word and the NaN-list base of each word; each wave then
+        //      writes the scan results and the compacted NaN positions of its own words ----
+        {
+            const int w0 = 2 * lane, w1 = 2 * lane + 1;
+            const unsigned long long m0 = (w0 < NW) ? mask[w0] : ~0ull;
+            const unsigned long long m1 = (w1 < NW) ? mask[w1] : ~0ull;
+            const int l0 = (w0 < NW && m0) ? w0 * 64 + 63 - __clzll(m0) : -1;
+            const int l1 = (w1 < NW && m1) ? w1 * 64 + 63 - __clzll(m1) : -1;
+            const int f0 = (w0 < NW && m0) ? w0 * 64 + __ffsll(m0) - 1 : kBig;
+            const int f1 = (w1 < NW && m1) ? w1 * 64 + __ffsll(m1) - 1 : kBig;
+            // NaN positions to impute: invalid AND inside [qA, qB)
+            auto need = [&](int w, unsigned long long m) -> unsigned long long {
+                const int lo = qA - w * 64, hi = qB - w * 64;      // bit range [lo, hi)
+                if (method == STS_FILL_NONE || hi <= 0 || lo >= 64) return 0ull;
+                unsigned long long r = ~m;
+                if (lo > 0) r &= ~0ull << lo;
+                if (hi < 64) r &= (1ull << hi) - 1ull;
+                return r;
+            };
+            const unsigned long long n0 = (w0 < NW) ? need(w0, m0) : 0ull;
+            const unsigned long long n1 = (w1 < NW) ? need(w1, m1) : 0ull;
+            int pm = l1 > l0 ? l1 : l0;                           // inclusive prefix max
+            int sm = f0 < f1 ? f0 : f1;                           // inclusive suffix min
+            int pc = __popcll(n0) + __popcll(n1);                 // inclusive prefix count
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) {
+                const int o = __shfl_up(pm, d);
+                const int c = __shfl_up(pc, d);
+                const int u = __shfl_down(sm, d);
+                if (lane >= d) { pm = o > pm ? o : pm; pc += c; }
+                if (lane + d < 64) sm = u < sm ? u : sm;
+            }
+            int ex = __shfl_up(pm, 1);
+            int exc = __shfl_up(pc, 1);
+            int exs = __shfl_down(sm, 1);
+            if (lane == 0) { ex = -1; exc = 0; }
+            if (lane == 63) exs = kBig;
+            const int nnan = __shfl(pc, 63);
+            const int firstValidE = __shfl(sm, 0);
+            const int lastValidE = __shfl(pm, 63);
+            if (wave == 0) {
+                if (w0 < NW) {
+                    lastUpTo[w0] = ex > l0 ? ex : l0;
+                    const int a0 = f1 < exs ? f1 : exs;
+                    firstFrom[w0] = f0 < a0 ? f0 : a0;
+                }
+                if (w1 < NW) {
+                    const int a1 = ex > l0 ? ex : l0;
+                    lastUpTo[w1] = a1 > l1 ? a1 : l1;
+                    firstFrom[w1] = f1 < exs ? f1 : exs;
+                }
+                // slow paths: a NaN run longer than the halos (rare)
+                int lext = -1, next = (int)T;
+                if (needL && e0 > 0 && firstValidE > qA && nnan > 0) lext = (int)scan_back(src, e0, lane);
+                if (needN && e0 + EW < T && qB > qA && lastValidE < qB - 1 && nnan > 0)
+                    next = (int)scan_fwd(src, e0 + EW, T, lane);
+                if (lane == 0) {
+                    sh_i[0] = lext;
+                    sh_i[1] = next;
+                    sh_i[2] = nnan;
+                    sh_d[1] = (lext >= 0) ? src[lext] : 0.0;
+                    sh_d[2] = (next < T) ? src[next] : 0.0;
+                }
+            }
+            // compacted NaN list: this wave's words
+#pragma unroll 1
+            for (int i = 0; i < (NW + kWaves - 1) / kWaves; i++) {
+                const int w = wave + i * kWaves;
+                if (w < NW) {
+                    const int base = (w & 1) ? __shfl(exc, w >> 1) + __popcll(__shfl(n0, w >> 1))
+                                             : __shfl(exc, w >> 1);
+                    const unsigned long long nm = (w & 1) ? __shfl(n1, w >> 1) : __shfl(n0, w >> 1);
+                    if ((nm >> lane) & 1ull) {
+                        const unsigned long long below = nm & ((1ull << lane) - 1ull);
+                        nanpos[base + __popcll(below)] = (unsigned short)(w * 64 + lane);
+                    }
+                }
+            }
+        }
+        __syncthreads();
+
+        // ---- 4. impute the compacted NaN positions, all lanes busy; F goes back into
+        //      vals IN PLACE (every (L, N) source is a valid position, never rewritten) ----
+        {
+            const int nnan = sh_i[2];
+            const int lext = sh_i[0], next = sh_i[1];
+            const double lextv = sh_d[1], nextv = sh_d[2];
+            for (int idx = tid; idx < nnan; idx += kThreads) {
+                const int q = nanpos[idx];
+                const int t = e0 + q;
+                const int w = q >> 6, b = q & 63;
+                const unsigned long long m = mask[w];
+                int Lt = -1, Nt = (int)T;
+                double Lv = 0.0, Nv = 0.0;
+                if (needL) {
+                    const unsigned long long lo = m & ((1ull << b) - 1ull);
+                    const int Lq = lo ? w * 64 + 63 - __clzll(lo) : (w > 0 ? lastUpTo[w - 1] : -1);
+                    if (Lq >= 0) { Lt = e0 + Lq; Lv = vals[Lq]; }
+                    else { Lt = lext; Lv = lextv; }
+                }
+                if (needN) {
+                    const unsigned long long hi = (b == 63) ? 0ull : (m & (~0ull << (b + 1)));
+                    const int Nq = hi ? w * 64 + __ffsll(hi) - 1 : (w + 1 < NW ? firstFrom[w + 1] : kBig);
+                    if (Nq < kBig) { Nt = e0 + Nq; Nv = vals[Nq]; }
+                    else { Nt = next; Nv = nextv; }
+                }
+                double f = __builtin_nan("");
+                switch (method) {
+                case STS_FILL_PREVIOUS:
+                    if (Lt >= 0) f = Lv;
+                    break;
+                case STS_FILL_NEXT:
+                    if (Nt < T) f = Nv;
+                    break;
+                case STS_FILL_NEAREST: {
+                    if (t == 0) break;                        // index 0 is never modified
+                    const int P = (Lt >= 1) ? Lt : -1;        // index 0 is never a previous source
+                    if (P < 0 && Nt >= T) { series_err = true; break; }
+                    f = (Nt >= T || (P >= 0 && t - P < Nt - t)) ? Lv : Nv;   // ties go to next
+                    break;
+                }
+                case STS_FILL_LINEAR: {
+                    if (Lt < 0 || Nt >= T) break;             // runs touching index 0 or n-1 stay NaN
+                    const double inc = (Nv - Lv) / (double)(Nt - Lt);
+                    double r = Lv;
+                    for (int j = t - Lt; j > 0; j--) r = r + inc;   // sequential, as :259-261
+                    f = r;
+                    break;
+                }
+                default:
+                    break;
+                }
+                vals[q] = f;
+            }
+        }
+        __syncthreads();
+
+        // ---- 5. filled output + lag matrix (16-B stores), then y = F - F(0) in place
+        //      (0 past the series end) for the MFMA phase; start the next tile's loads ----
+        {
+            const bool al = dst && ((reinterpret_cast<uintptr_t>(dst) & 15) == 0);
+            double2* v2 = reinterpret_cast<double2*>(vals);
+            const int qBfull = (NT > 0) ? ((qW + 64 + 16 * NT < EW) ? qW + 64 + 16 * NT : EW) : 0;
+            for (int q2 = (qA >> 1) + tid; 2 * q2 < qW || 2 * q2 < qBfull; q2 += kThreads) {
+                const int q = 2 * q2;
+                double2 f = v2[q2];
+                if (q < qW) {
+                    const int t = e0 + q;
+                    if (dst) {
+                        if (al && q + 1 < qW) {
+                            *reinterpret_cast<double2*>(dst + t) = f;
+                        } else {
+                            dst[t] = f.x;
+                            if (q + 1 < qW) dst[t + 1] = f.y;
+                        }
+                    }
+                    if (a.lagmat) {
+                        double* lm = a.lagmat + s * lrows * ncols;
+                        for (int c = init; c <= a.max_lag; c++) {
+                            double* col = lm + (int64_t)(c - init) * lrows;
+                            const int64_t r0 = (int64_t)t - a.max_lag + c;
+                            if (r0 >= 0 && r0 < lrows) col[r0] = f.x;
+                            if (q + 1 < qW && r0 + 1 >= 0 && r0 + 1 < lrows) col[r0 + 1] = f.y;
+                        }
+                    }
+                }
+                if (NT > 0 && q < qBfull) {
+                    f.x = (q < qB) ? f.x - c0 : 0.0;
+                    f.y = (q + 1 < qB) ? f.y - c0 : 0.0;
+                    v2[q2] = f;
+                }
+            }
+        }
+        if (have_next) STS_ISSUE(k + 1);   // in flight during the MFMA phase of tile k
+        else STS_CLEAR();
+
+        if constexpr (NT > 0) {
+            __syncthreads();
+            // ---- 6. lag products on MFMA: U_t += y(j0 + l) x y(j0 + 16t + l) ----
+            constexpr int CPW = TW / 64 / kWaves;   // 64-step chunks per wave
+            const int tlen = t1 - t0;
+            const int nch = (tlen + 63) / 64;
+            int c = wave * CPW;
+            int cend = c + CPW;
+            if (cend > nch) cend = nch;
+            for (; c < cend; c++) {
+                const int jrel = 64 * c + lane;
+                const double* yb = vals + qA + jrel;
+                double bv[NT];
+#pragma unroll
+                for (int t = 0; t < NT; t++) bv[t] = yb[16 * t];
+                const double av = (jrel < tlen) ? bv[0] : 0.0;   // A only inside the tile
+#pragma unroll
+                for (int t = 0; t < NT; t++) U[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv[t], U[t], 0, 0, 0);
+                sy += av;
+            }
+        }
+        have = have_next;
+        __syncthreads();   // vals / mask / lists are reused by the next tile
+    }
+#undef STS_ISSUE
+#undef STS_LD1
+#undef STS_ST1
+#undef STS_CLEAR
     if (series_err && a.err) a.err[s] = STS_ERR_ALL_NAN;
 
     if constexpr (NT > 0) {
-        // ---- 5. y = F - F(0) in place (0 past the series end) ----
-        __syncthreads();
-        // every index the MFMA loop can touch must hold y (0 past the data): the last
-        // chunk may read 63 + 16*(NT-1) steps past qW
-        const int qBfull = (qW + 64 + 16 * NT < EW) ? qW + 64 + 16 * NT : EW;
-        for (int q = qA + tid; q < qBfull; q += kThreads) vals[q] = (q < qB) ? vals[q] - c0 : 0.0;
-        __syncthreads();
-
-        // ---- 6. lag products on MFMA: U_t += A(j0 + l) x B(j0 + 16t + l) ----
-        constexpr int CPW = TW / 64 / kWaves;   // 64-step chunks per wave
-        const int nchunks = (int)((t1 - t0 + 63) / 64);
-        int c = wave * CPW;
-        int cend = c + CPW;
-        if (cend > nchunks) cend = nchunks;
-        d4 U[NT];
-#pragma unroll
-        for (int t = 0; t < NT; t++) U[t] = d4{0.0, 0.0, 0.0, 0.0};
-        double sy = 0.0;
-        const int tlen = (int)(t1 - t0);
-        for (; c < cend; c++) {
-            const int jrel = 64 * c + lane;
-            const double* yb = vals + qA + jrel;
-            const double av = (jrel < tlen) ? yb[0] : 0.0;
-            double bv[NT];
-            bv[0] = av;
-#pragma unroll
-            for (int t = 1; t < NT; t++) bv[t] = yb[16 * t];
-#pragma unroll
-            for (int t = 0; t < NT; t++) U[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv[t], U[t], 0, 0, 0);
-            sy += av;
-        }
-        __syncthreads();   // every wave is done reading y
-
         // ---- 7. diagonal extraction: lane i accumulates lag i in a fixed order ----
         double* scr = vals + wave * 256;
         double lagacc = 0.0;
@@ -335,7 +429,7 @@ __global__ __launch_bounds__(kThreads) void tile_kernel(TileArgs a, int method) 
         if (lane == 0) wsum[wave * kPartStride + 64] = sy;
         __syncthreads();
         if (wave == 0) {
-            double* part = a.partials + tile * kPartStride;
+            double* part = a.partials + ch * kPartStride;
             double tot = 0.0;
 #pragma unroll
             for (int w = 0; w < kWaves; w++) tot += wsum[w * kPartStride + lane];
@@ -384,8 +478,8 @@ __global__ __launch_bounds__(256) void acf_finalize_kernel(FinalizeArgs a) {
         out = cv / (__builtin_sqrt(v1) * __builtin_sqrt(v2));
     } else {
         double Pi = 0.0, P0 = 0.0, Sy = 0.0;
-        const double* pp = a.partials + s * a.tiles_per_series * kPartStride;
-        for (int64_t k = 0; k < a.tiles_per_series; k++, pp += kPartStride) {
+        const double* pp = a.partials + s * a.parts_per_series * kPartStride;
+        for (int64_t k = 0; k < a.parts_per_series; k++, pp += kPartStride) {
             Pi += pp[i];
             P0 += pp[0];
             Sy += pp[64];
@@ -414,10 +508,10 @@ __global__ __launch_bounds__(256) void acf_finalize_kernel(FinalizeArgs a) {
 }  // namespace
 
 hipError_t launch_tile(int method, int tw, const TileArgs& a, hipStream_t st) {
-    const int64_t ntiles = a.S * a.tiles_per_series;
-    if (ntiles <= 0) return hipSuccess;
-    if (ntiles > 0x7fffffffLL) return hipErrorInvalidValue;
-    dim3 grid((unsigned)ntiles), block(kThreads);
+    const int64_t nchunk = a.S * a.chunks_per_series;
+    if (nchunk <= 0) return hipSuccess;
+    if (nchunk > 0x7fffffffLL) return hipErrorInvalidValue;
+    dim3 grid((unsigned)nchunk), block(kThreads);
     int nt = 0;
     if (a.K > 0) nt = (a.K + 15) / 16 + 1;
     if (tw == 512 && nt == 0) {

@@ -1,0 +1,155 @@
+// sts_jni.cpp -- JNI shim: com.cloudera.sparkts.StsNative -> libsts_hip.so (include/sts.h).
+//
+// Built only where a JDK is present (`make -C spark-timeseries_amd jni JAVA_HOME=...`); this
+// image has no JDK, so the shim is compiled and exercised on a JVM host.
+// The Scala side gathers a Spark partition's records into ONE
+// series-contiguous double[] panel (S x T) and makes one call per partition.
+//
+// Each native method pins the Java arrays (GetPrimitiveArrayCritical: no copy on HotSpot),
+// calls the `_host` C entry point (which stages through HBM on the calling executor
+// thread's own HIP stream) and maps the status to the SAME exception class and message the
+// reference throws.  Critical sections contain no JNI calls.
+#include <jni.h>
+
+#include "sts.h"
+
+namespace {
+
+struct Pinned {
+    JNIEnv* env;
+    jarray arr;
+    void* p;
+    Pinned(JNIEnv* e, jarray a) : env(e), arr(a), p(a ? e->GetPrimitiveArrayCritical(a, nullptr) : nullptr) {}
+    ~Pinned() {
+        if (p) env->ReleasePrimitiveArrayCritical(arr, p, 0);
+    }
+    double* d() { return static_cast<double*>(p); }
+    int32_t* i() { return static_cast<int32_t*>(p); }
+};
+
+void throw_for(JNIEnv* env, int status) {
+    const char* cls = "java/lang/RuntimeException";
+    const char* msg = sts_last_error();
+    switch (status) {
+    case STS_OK: return;
+    case STS_ERR_ALL_NAN: cls = "java/lang/IllegalArgumentException"; msg = "Input is all NaNs!"; break;
+    case STS_ERR_REQUIREMENT:
+    case STS_ERR_BAD_ARG: cls = "java/lang/IllegalArgumentException"; break;
+    case STS_ERR_UNSUPPORTED_METHOD: cls = "java/lang/UnsupportedOperationException"; break;
+    case STS_ERR_NULL_DEST: cls = "java/lang/NullPointerException"; break;
+    case STS_ERR_NOT_ENOUGH_DATA: cls = "org/apache/commons/math3/exception/MathIllegalArgumentException"; break;
+    case STS_ERR_SINGULAR: cls = "org/apache/commons/math3/linear/SingularMatrixException"; break;
+    default: break;
+    }
+    jclass c = env->FindClass(cls);
+    if (!c) c = env->FindClass("java/lang/RuntimeException");
+    env->ThrowNew(c, msg);
+}
+
+}  // namespace
+
+extern "C" {
+
+// UnivariateTimeSeries.fillts over a partition panel (S/UnivariateTimeSeries.scala:141-150)
+JNIEXPORT void JNICALL Java_com_cloudera_sparkts_StsNative_fill(JNIEnv* env, jclass, jdoubleArray in,
+                                                                 jdoubleArray out, jlong S, jlong T,
+                                                                 jstring method) {
+    const char* m = env->GetStringUTFChars(method, nullptr);
+    int code = sts_fill_method_from_name(m);
+    env->ReleaseStringUTFChars(method, m);
+    if (code < 0) return throw_for(env, STS_ERR_UNSUPPORTED_METHOD);
+    int st;
+    {
+        Pinned pi(env, in), po(env, out);
+        st = sts_fill_host(pi.d(), po.d(), S, T, T, code, nullptr);
+    }
+    throw_for(env, st);
+}
+
+// UnivariateTimeSeries.autocorr (S/UnivariateTimeSeries.scala:68-93); acf is S x numLags
+JNIEXPORT void JNICALL Java_com_cloudera_sparkts_StsNative_autocorr(JNIEnv* env, jclass, jdoubleArray in,
+                                                                     jlong S, jlong T, jint numLags,
+                                                                     jdoubleArray acf) {
+    int st;
+    {
+        Pinned pi(env, in), pa(env, acf);
+        st = sts_autocorr_host(pi.d(), S, T, T, numLags, pa.d());
+    }
+    throw_for(env, st);
+}
+
+// UnivariateTimeSeries.differencesAtLag(ts, dest, lag, startIndex); dest may be ts (in place)
+JNIEXPORT void JNICALL Java_com_cloudera_sparkts_StsNative_differencesAtLag(JNIEnv* env, jclass, jdoubleArray in,
+                                                                             jdoubleArray dest, jlong S, jlong T,
+                                                                             jint lag, jint start) {
+    int st;
+    if (env->IsSameObject(in, dest)) {
+        Pinned p(env, in);
+        st = sts_diff_at_lag_host(p.d(), p.d(), S, T, T, lag, start);
+    } else {
+        Pinned pi(env, in), po(env, dest);
+        st = sts_diff_at_lag_host(pi.d(), po.d(), S, T, T, lag, start);
+    }
+    throw_for(env, st);
+}
+
+// UnivariateTimeSeries.lag / Lag.lagMatTrimBoth (S/Lag.scala:62-77): out is S blocks of
+// (T - maxLag) x (maxLag + inc) column-major (Breeze DenseMatrix data)
+JNIEXPORT void JNICALL Java_com_cloudera_sparkts_StsNative_lag(JNIEnv* env, jclass, jdoubleArray in,
+                                                                jdoubleArray out, jlong S, jlong T, jint maxLag,
+                                                                jboolean includeOriginal) {
+    int st;
+    {
+        Pinned pi(env, in), po(env, out);
+        st = sts_lag_matrix_host(pi.d(), po.d(), S, T, T, maxLag, includeOriginal ? 1 : 0);
+    }
+    throw_for(env, st);
+}
+
+// EWMAModel.add/removeTimeDependentEffects (S/models/EWMA.scala:125-142); dest may be ts
+JNIEXPORT void JNICALL Java_com_cloudera_sparkts_StsNative_ewma(JNIEnv* env, jclass, jboolean add,
+                                                                 jdoubleArray in, jdoubleArray dest, jlong S,
+                                                                 jlong T, jdoubleArray smoothing) {
+    if (!dest) return throw_for(env, STS_ERR_NULL_DEST);
+    int st;
+    if (env->IsSameObject(in, dest)) {
+        Pinned p(env, in), ps(env, smoothing);
+        st = add ? sts_ewma_add_host(p.d(), p.d(), S, T, T, ps.d()) : sts_ewma_remove_host(p.d(), p.d(), S, T, T, ps.d());
+    } else {
+        Pinned pi(env, in), po(env, dest), ps(env, smoothing);
+        st = add ? sts_ewma_add_host(pi.d(), po.d(), S, T, T, ps.d())
+                 : sts_ewma_remove_host(pi.d(), po.d(), S, T, T, ps.d());
+    }
+    throw_for(env, st);
+}
+
+// Autoregression.fitModel(ts, maxLag, noIntercept) (S/models/Autoregression.scala:38-53)
+JNIEXPORT void JNICALL Java_com_cloudera_sparkts_StsNative_arFit(JNIEnv* env, jclass, jdoubleArray in, jlong S,
+                                                                  jlong T, jint p, jboolean noIntercept,
+                                                                  jdoubleArray c, jdoubleArray coef) {
+    int st;
+    {
+        Pinned pi(env, in), pc(env, c), pk(env, coef);
+        st = sts_ar_fit_host(pi.d(), S, T, T, p, noIntercept ? 1 : 0, pc.d(), pk.d(), nullptr);
+    }
+    throw_for(env, st);
+}
+
+// ARModel.add/removeTimeDependentEffects (S/models/Autoregression.scala:60-88); dest may be ts
+JNIEXPORT void JNICALL Java_com_cloudera_sparkts_StsNative_ar(JNIEnv* env, jclass, jboolean add, jdoubleArray in,
+                                                               jdoubleArray dest, jlong S, jlong T, jdoubleArray c,
+                                                               jdoubleArray coef, jint p) {
+    int st;
+    if (env->IsSameObject(in, dest)) {
+        Pinned pi(env, in), pc(env, c), pk(env, coef);
+        st = add ? sts_ar_add_host(pi.d(), pi.d(), S, T, T, pc.d(), pk.d(), p)
+                 : sts_ar_remove_host(pi.d(), pi.d(), S, T, T, pc.d(), pk.d(), p);
+    } else {
+        Pinned pi(env, in), po(env, dest), pc(env, c), pk(env, coef);
+        st = add ? sts_ar_add_host(pi.d(), po.d(), S, T, T, pc.d(), pk.d(), p)
+                 : sts_ar_remove_host(pi.d(), po.d(), S, T, T, pc.d(), pk.d(), p);
+    }
+    throw_for(env, st);
+}
+
+}  // extern "C"

@@ -20,5 +20,9 @@ for s in $STEPS; do
     bench) run bench_small 400 python -u bench.py --series ${BENCH_SERIES:-1000} --steps 3 --warmup 1 --cpu-seconds 3 ;;
     benchfull) run bench_full 600 python -u bench.py ;;
     smoke) run smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()" ;;
+    prof) export TMPDIR=/tmp; run rocprof_stats 600 rocprofv3 --kernel-trace --stats -T -d gpurun_out/prof -o bench --output-format csv -- python -u bench.py --series ${PROF_SERIES:-2000} --steps 5 --warmup 1 --no-cpu-baseline ;;
+    pmcfetch) export TMPDIR=/tmp; run pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE -T -d gpurun_out/pmc_fetch -o bench --output-format csv -- python -u bench.py --series ${PROF_SERIES:-2000} --steps 2 --warmup 0 --no-cpu-baseline ;;
+    pmcwrite) export TMPDIR=/tmp; run pmc_write 300 rocprofv3 --pmc WRITE_SIZE -T -d gpurun_out/pmc_write -o bench --output-format csv -- python -u bench.py --series ${PROF_SERIES:-2000} --steps 2 --warmup 0 --no-cpu-baseline ;;
+    custom) run custom ${CUSTOM_SECS:-300} bash -c "$CUSTOM_CMD" ;;
   esac
 done
