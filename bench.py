@@ -35,6 +35,9 @@ WORKLOADS = {
     "c2": (1_000_000, 390, 0.05, 2,
            "C2: fillPrevious -> differencesAtLag(1) -> EWMA(0.2).add, 1,000,000 series x 390 steps"),
     "c4": (500_000, 2_520, 0.0, 4, "C4: AR(5) fit + removeTimeDependentEffects, 500,000 series x 2,520 steps"),
+    "c5": (1_250, 10_000_000, 0.30, 5,
+           "C5 shard: fill('nearest') + lag(10, false), 1,250 series x 10,000,000 steps per GPU (N=8 -> C5's "
+           "10k x 10M); lag matrices written into a reused scratch slab, 10 series per call"),
 }
 
 
@@ -94,6 +97,10 @@ def main():
     else:
         raise_for_status(lib.sts_gen_panel(x.data_ptr(), s0, S, T, T, seed, nan_p, sp), "gen")
     smooth = torch.full((S,), 0.2, dtype=torch.float64, device=dev)
+    if args.workload == "c5":
+        P, LB = 10, 10            # lag(10, includeOriginal = false); series per call
+        lagbuf = torch.empty((LB, P, T - P), dtype=torch.float64, device=dev)
+        x[:, 1] = 1.0 + x[:, 1].nan_to_num(0.0)   # keep x[1] valid: fillNearest throws on an all-NaN tail
 
     def step():
         if args.workload in ("c3", "c1"):
@@ -104,6 +111,12 @@ def main():
         elif args.workload == "c2":
             raise_for_status(lib.sts_fill_diff_ewma(x.data_ptr(), out.data_ptr(), S, T, T, T, 3, 1, smooth.data_ptr(),
                                                     err.data_ptr(), sp), "fill_diff_ewma")
+        elif args.workload == "c5":
+            for b0 in range(0, S, LB):
+                nb = min(LB, S - b0)
+                raise_for_status(lib.sts_fill_lag_matrix(x[b0].data_ptr(), out[b0].data_ptr(), lagbuf.data_ptr(), nb,
+                                                         T, T, T, 1, P, 0, err[b0:].data_ptr(), sp),
+                                 "fill_lag_matrix")
         elif args.workload == "c4":
             raise_for_status(lib.sts_ar_fit_remove(x.data_ptr(), out.data_ptr(), S, T, T, T, p_ar, 0,
                                                    c_fit.data_ptr(), coef_fit.data_ptr(), err.data_ptr(), sp),
@@ -143,14 +156,19 @@ def main():
     value = elems / elapsed
     ms_per_step = elapsed / args.steps * 1e3
     # dominant kernel: the fused series-tile kernel (fill + ACF partials / fill only)
-    bytes_per_launch = 16.0 * S * T      # 8 B read + 8 B filled write per element
+    bytes_per_step = 16.0 * S * T        # 8 B read + 8 B filled write per element
+    if args.workload == "c5":            # + the lag matrix: 8 * P bytes per row, (T - P) rows per series
+        bytes_per_step += 8.0 * P * (T - P) * S
+    bytes_per_launch = bytes_per_step * args.steps / max(1, launches[0])
     roofline = None
-    if args.workload in ("c3", "c1") and launches[0] > 0:
+    if args.workload in ("c3", "c1", "c5") and launches[0] > 0:
         avg_ms = kern_ms[0] / launches[0]
-        achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9
+        achieved = bytes_per_step * args.steps / (kern_ms[0] * 1e-3) / 1e9
         roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                     "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": None,
-                    "kernel": "sts::tile_kernel<4096,5> (fill linear + ACF partials, FP64 MFMA)",
+                    "kernel": {"c3": "sts::tile_kernel<4096,5> (fill linear + ACF partials, FP64 MFMA)",
+                               "c1": "sts::tile_kernel<4096,3> (fill linear + ACF partials, FP64 MFMA)",
+                               "c5": "sts::tile_kernel<4096,0> (fill nearest + lag-matrix columns)"}[args.workload],
                     "avg_kernel_ms": round(avg_ms, 4), "bytes_per_launch": bytes_per_launch}
     elif launches[0] == 0:
         step_bytes = 16.0 * S * T
@@ -172,7 +190,7 @@ def main():
             "data": "synthetic: Philox4x32-10 counter-based panel generated in HBM (SURVEY.md 8(d)), %g NaN" % nan_p,
             "config": {"workload": desc, "series_per_gpu": S, "steps_per_series": T,
                        "numLags": K if args.workload in ("c3", "c1") else None,
-                       "fill": {"c3": "linear", "c1": "linear", "c2": "previous", "c4": None}[args.workload],
+                       "fill": {"c3": "linear", "c1": "linear", "c2": "previous", "c4": None, "c5": "nearest"}[args.workload],
                        "parallelism": "dp%d (series sharded by key, one process per GPU)" % world},
             "roofline": roofline,
             "cpu_baseline": cpu,
@@ -204,6 +222,11 @@ def cpu_baseline(args, S, T, K, seed, nan_p, out, acf, p_ar):
             rf, racf, _ = oracle.panel_fill_autocorr(xs, "linear", K, threads=threads)
         elif args.workload == "c2":
             rf = oracle.panel_fill_diff_ewma(xs, 0.2, threads=threads)
+        elif args.workload == "c5":
+            xs[:, 1] = 1.0 + np.nan_to_num(xs[:, 1])
+            rf, _ = oracle.panel_fill(xs, "nearest", threads=threads)
+            for r in rf:
+                oracle.lag(r, 10, False)
         else:
             rf, _, _ = oracle.panel_ar_fit_remove(xs, p_ar, threads=threads)
         elapsed += time.perf_counter() - t0

@@ -43,10 +43,19 @@ __global__ __launch_bounds__(64) void ar_fit_kernel(ArArgs a, int NT) {
 
     // ---- pass 1: stage + mean ----
     double part = 0.0;
-    for (int64_t t = lane; t < T; t += 64) {
-        double v = xg[t];
-        if (STAGED) sx[t] = v;
-        part += v;
+    for (int64_t t0 = 0; t0 < T; t0 += 512) {     // 8 independent loads in flight per lane
+        double v[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            const int64_t t = t0 + u * 64 + lane;
+            v[u] = (t < T) ? xg[t] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            const int64_t t = t0 + u * 64 + lane;
+            if (STAGED && t < T) sx[t] = v[u];
+            part += v[u];
+        }
     }
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) part += __shfl_xor(part, d);

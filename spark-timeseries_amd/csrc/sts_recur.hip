@@ -56,14 +56,24 @@ __global__ __launch_bounds__(64) void recur_kernel(RecurArgs a) {
     double e = 0.0;                                // EWMA state
     double carry = __builtin_nan("");              // fillPrevious carry
 
+    // blocks move through LDS: all 32 row segments of a block are loaded before any is
+    // stored (lanes 0-31 take row 2i, lanes 32-63 row 2i+1: whole 256-B row segments)
+    const int col = lane & 31;
     for (int64_t tc = 0; tc < T; tc += kCH) {
         const int len = (T - tc < kCH) ? (int)(T - tc) : kCH;
-        // load block: lanes 0-31 row r, lanes 32-63 row r+1
-        {
-            const int col = lane & 31;
-            for (int r = 0; r < ns; r += 2) {
-                const int row = r + (lane >> 5);
-                if (row < ns && col < len) tile[row * kRow + col] = a.in[(s0 + row) * a.ld_in + tc + col];
+        const double* base = a.in + (s0 + (lane >> 5)) * a.ld_in + tc + col;
+#pragma unroll
+        for (int h = 0; h < 2; h++) {      // two batches of 16 loads in flight
+            double pre[16];
+#pragma unroll
+            for (int i = 0; i < 16; i++) {
+                const int row = 2 * (16 * h + i) + (lane >> 5);
+                pre[i] = (row < ns && col < len) ? base[(int64_t)(2 * (16 * h + i)) * a.ld_in] : 0.0;
+            }
+#pragma unroll
+            for (int i = 0; i < 16; i++) {
+                const int row = 2 * (16 * h + i) + (lane >> 5);
+                if (row < ns && col < len) tile[row * kRow + col] = pre[i];
             }
         }
         __syncthreads();
@@ -121,10 +131,11 @@ __global__ __launch_bounds__(64) void recur_kernel(RecurArgs a) {
         }
         __syncthreads();
         {
-            const int col = lane & 31;
-            for (int r = 0; r < ns; r += 2) {
-                const int row = r + (lane >> 5);
-                if (row < ns && col < len) a.out[(s0 + row) * a.ld_out + tc + col] = tile[row * kRow + col];
+            double* obase = a.out + (s0 + (lane >> 5)) * a.ld_out + tc + col;
+#pragma unroll 8
+            for (int i = 0; i < 32; i++) {
+                const int row = 2 * i + (lane >> 5);
+                if (row < ns && col < len) obase[(int64_t)(2 * i) * a.ld_out] = tile[row * kRow + col];
             }
         }
         __syncthreads();

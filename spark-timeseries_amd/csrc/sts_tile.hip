@@ -42,12 +42,40 @@ constexpr int kBig = 1 << 30;
 
 __device__ __forceinline__ bool isnan_d(double v) { return __builtin_isnan(v); }
 
+// Diagnostic build only (-DSTS_STAMPS, `make stamps`): per-phase s_memtime accumulation,
+// summed over waves into a device array read back by sts_debug_stamps().  The shipped
+// library has no stamps.
+#ifdef STS_STAMPS
+__device__ unsigned long long g_stamps[16];
+#define STAMP(i)                                                                            \
+    do {                                                                                    \
+        const unsigned long long now_ = __builtin_amdgcn_s_memtime();                      \
+        st_acc[i] += now_ - st_prev;                                                        \
+        st_prev = now_;                                                                     \
+    } while (0)
+#else
+#define STAMP(i) \
+    do {         \
+    } while (0)
+#endif
+
 // Bijective XCD-aware remap (cdna_hip_programming.md §5 "XCD swizzle must be
 // bijective"): consecutive tile ids -> one XCD, so neighbour tiles of one series
 // share the L2 that holds their overlapping halos.
 __device__ __forceinline__ int64_t xcd_remap(int64_t b, int64_t n) {
     int64_t q = n / 8, r = n % 8, x = b % 8;
     return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
+}
+
+// bit i of x -> bit 2i (Morton spread of a 32-bit value), scalar ops
+__device__ __forceinline__ unsigned long long spread2(unsigned long long x) {
+    x &= 0xFFFFFFFFull;
+    x = (x | (x << 16)) & 0x0000FFFF0000FFFFull;
+    x = (x | (x << 8)) & 0x00FF00FF00FF00FFull;
+    x = (x | (x << 4)) & 0x0F0F0F0F0F0F0F0Full;
+    x = (x | (x << 2)) & 0x3333333333333333ull;
+    x = (x | (x << 1)) & 0x5555555555555555ull;
+    return x;
 }
 
 // Wave-wide search of global memory for the last valid index < from (stop at 0).
@@ -84,7 +112,8 @@ __global__ __launch_bounds__(kThreads, 3) void tile_kernel(TileArgs a, int metho
     __shared__ unsigned long long mask[NW];
     __shared__ int lastUpTo[NW];     // last valid E-position in words <= w (-1: none)
     __shared__ int firstFrom[NW];    // first valid E-position in words >= w (kBig: none)
-    __shared__ unsigned short nanpos[EW];   // compacted NaN positions of the tile
+    __shared__ int wbase[NW + 1];    // NaN-list offset of each word (exclusive prefix count)
+    __shared__ unsigned long long wneed[NW];   // NaN positions to impute, per word
     __shared__ int sh_i[3];          // lext, next (series positions), NaN count
     __shared__ double sh_d[3];       // c0, value at lext, value at next
 
@@ -163,6 +192,10 @@ __global__ __launch_bounds__(kThreads, 3) void tile_kernel(TileArgs a, int metho
     double sy = 0.0;
     bool series_err = false;
 
+#ifdef STS_STAMPS
+    unsigned long long st_acc[12] = {0};
+    unsigned long long st_prev = __builtin_amdgcn_s_memtime();
+#endif
     bool have = interior(k_begin);
     if (have) STS_ISSUE(k_begin);
     else STS_CLEAR();
@@ -171,10 +204,26 @@ __global__ __launch_bounds__(kThreads, 3) void tile_kernel(TileArgs a, int metho
         const int t1 = (t0 + TW < T) ? t0 + TW : (int)T;
         const int e0 = t0 - kHB;
 
-        // ---- 1. prefetched registers (or a bounds-checked edge load) -> LDS ----
+        // ---- 1. prefetched registers (or a bounds-checked edge load) -> LDS; for prefetched
+        //      tiles the validity ballots come straight from the registers: register j of
+        //      wave v holds steps 128v + 512j + 2*lane (+1), i.e. words 2v + 8j and 2v + 8j + 1
+        //      as an even/odd bit interleave ----
         if (have) {
             double2* v2_ = reinterpret_cast<double2*>(vals);
             STS_ST1(0) STS_ST1(1) STS_ST1(2) STS_ST1(3) STS_ST1(4) STS_ST1(5) STS_ST1(6) STS_ST1(7) STS_ST1(8)
+#define STS_BAL1(j)                                                                         \
+    if constexpr (j < RPT) {                                                                \
+        const unsigned long long bx_ = __ballot(!isnan_d(R##j.x));                          \
+        const unsigned long long by_ = __ballot(!isnan_d(R##j.y));                          \
+        const int w_ = 2 * wave + 8 * j;                                                    \
+        if (lane == 0) {                                                                    \
+            if (w_ < NW) mask[w_] = spread2(bx_) | (spread2(by_) << 1);                     \
+            if (w_ + 1 < NW) mask[w_ + 1] = spread2(bx_ >> 32) | (spread2(by_ >> 32) << 1); \
+        }                                                                                   \
+    }
+            STS_BAL1(0) STS_BAL1(1) STS_BAL1(2) STS_BAL1(3) STS_BAL1(4) STS_BAL1(5) STS_BAL1(6) STS_BAL1(7)
+            STS_BAL1(8)
+#undef STS_BAL1
         } else {
             for (int q = tid; q < EW; q += kThreads) {
                 const int t = e0 + q;
@@ -182,7 +231,9 @@ __global__ __launch_bounds__(kThreads, 3) void tile_kernel(TileArgs a, int metho
             }
         }
         const bool have_next = (k + 1 < k_end) && interior(k + 1);
+        STAMP(0);
         __syncthreads();
+        STAMP(1);
 
         // positions to produce: [qA, qB) (E-relative); the ACF needs 16*NT steps past the tile
         const int qA = kHB;
@@ -190,21 +241,24 @@ __global__ __launch_bounds__(kThreads, 3) void tile_kernel(TileArgs a, int metho
         int qB = qW + (NT > 0 ? 16 * NT : 0);
         if (e0 + qB > T) qB = (int)T - e0;
 
-        // ---- 2. validity ballots (wave v owns words v, v+4, ...) ----
+        // ---- 2. validity ballots from LDS for the edge tiles (wave v owns words v, v+4, ...) ----
+        if (!have) {
 #pragma unroll 2
-        for (int i = 0; i < (NW + kWaves - 1) / kWaves; i++) {
-            const int w = wave + i * kWaves;
-            if (w < NW) {
-                const unsigned long long m = __ballot(!isnan_d(vals[w * 64 + lane]));
-                if (lane == 0) mask[w] = m;
+            for (int i = 0; i < (NW + kWaves - 1) / kWaves; i++) {
+                const int w = wave + i * kWaves;
+                if (w < NW) {
+                    const unsigned long long m = __ballot(!isnan_d(vals[w * 64 + lane]));
+                    if (lane == 0) mask[w] = m;
+                }
             }
+            STAMP(2);
+            __syncthreads();
         }
-        __syncthreads();
+        STAMP(3);
 
-        // ---- 3. word scans in every wave (lane l: words 2l, 2l+1): last/first valid
-        //      position around each word and the NaN-list base of each word; each wave then
-        //      writes the scan results and the compacted NaN positions of its own words ----
-        {
+        // ---- 3. word scans (wave 0; lane l: words 2l, 2l+1): last valid position up to
+        //      each word, first valid from each word, and the NaN-list offset of each word ----
+        if (wave == 0) {
             const int w0 = 2 * lane, w1 = 2 * lane + 1;
             const unsigned long long m0 = (w0 < NW) ? mask[w0] : ~0ull;
             const unsigned long long m1 = (w1 < NW) ? mask[w1] : ~0ull;
@@ -242,46 +296,37 @@ __global__ __launch_bounds__(kThreads, 3) void tile_kernel(TileArgs a, int metho
             const int nnan = __shfl(pc, 63);
             const int firstValidE = __shfl(sm, 0);
             const int lastValidE = __shfl(pm, 63);
-            if (wave == 0) {
-                if (w0 < NW) {
-                    lastUpTo[w0] = ex > l0 ? ex : l0;
-                    const int a0 = f1 < exs ? f1 : exs;
-                    firstFrom[w0] = f0 < a0 ? f0 : a0;
-                }
-                if (w1 < NW) {
-                    const int a1 = ex > l0 ? ex : l0;
-                    lastUpTo[w1] = a1 > l1 ? a1 : l1;
-                    firstFrom[w1] = f1 < exs ? f1 : exs;
-                }
-                // slow paths: a NaN run longer than the halos (rare)
-                int lext = -1, next = (int)T;
-                if (needL && e0 > 0 && firstValidE > qA && nnan > 0) lext = (int)scan_back(src, e0, lane);
-                if (needN && e0 + EW < T && qB > qA && lastValidE < qB - 1 && nnan > 0)
-                    next = (int)scan_fwd(src, e0 + EW, T, lane);
-                if (lane == 0) {
-                    sh_i[0] = lext;
-                    sh_i[1] = next;
-                    sh_i[2] = nnan;
-                    sh_d[1] = (lext >= 0) ? src[lext] : 0.0;
-                    sh_d[2] = (next < T) ? src[next] : 0.0;
-                }
+            if (w0 < NW) {
+                lastUpTo[w0] = ex > l0 ? ex : l0;
+                const int a0 = f1 < exs ? f1 : exs;
+                firstFrom[w0] = f0 < a0 ? f0 : a0;
+                wbase[w0] = exc;
+                wneed[w0] = n0;
             }
-            // compacted NaN list: this wave's words
-#pragma unroll 1
-            for (int i = 0; i < (NW + kWaves - 1) / kWaves; i++) {
-                const int w = wave + i * kWaves;
-                if (w < NW) {
-                    const int base = (w & 1) ? __shfl(exc, w >> 1) + __popcll(__shfl(n0, w >> 1))
-                                             : __shfl(exc, w >> 1);
-                    const unsigned long long nm = (w & 1) ? __shfl(n1, w >> 1) : __shfl(n0, w >> 1);
-                    if ((nm >> lane) & 1ull) {
-                        const unsigned long long below = nm & ((1ull << lane) - 1ull);
-                        nanpos[base + __popcll(below)] = (unsigned short)(w * 64 + lane);
-                    }
-                }
+            if (w1 < NW) {
+                const int a1 = ex > l0 ? ex : l0;
+                lastUpTo[w1] = a1 > l1 ? a1 : l1;
+                firstFrom[w1] = f1 < exs ? f1 : exs;
+                wbase[w1] = exc + __popcll(n0);
+                wneed[w1] = n1;
+            }
+            // slow paths: a NaN run longer than the halos (rare)
+            int lext = -1, next = (int)T;
+            if (needL && e0 > 0 && firstValidE > qA && nnan > 0) lext = (int)scan_back(src, e0, lane);
+            if (needN && e0 + EW < T && qB > qA && lastValidE < qB - 1 && nnan > 0)
+                next = (int)scan_fwd(src, e0 + EW, T, lane);
+            if (lane == 0) {
+                wbase[NW] = nnan;
+                sh_i[0] = lext;
+                sh_i[1] = next;
+                sh_i[2] = nnan;
+                sh_d[1] = (lext >= 0) ? src[lext] : 0.0;
+                sh_d[2] = (next < T) ? src[next] : 0.0;
             }
         }
+        STAMP(4);
         __syncthreads();
+        STAMP(5);
 
         // ---- 4. impute the compacted NaN positions, all lanes busy; F goes back into
         //      vals IN PLACE (every (L, N) source is a valid position, never rewritten) ----
@@ -290,7 +335,22 @@ __global__ __launch_bounds__(kThreads, 3) void tile_kernel(TileArgs a, int metho
             const int lext = sh_i[0], next = sh_i[1];
             const double lextv = sh_d[1], nextv = sh_d[2];
             for (int idx = tid; idx < nnan; idx += kThreads) {
-                const int q = nanpos[idx];
+                // the word holding NaN #idx: last w with wbase[w] <= idx (binary search) ...
+                int lo = 0, hi = NW;
+                while (hi - lo > 1) {
+                    const int mid = (lo + hi) >> 1;
+                    if (wbase[mid] <= idx) lo = mid;
+                    else hi = mid;
+                }
+                // ... and the position of its (idx - wbase[w])-th set need-bit (popcount bisection)
+                unsigned long long nm = wneed[lo];
+                int kk = idx - wbase[lo], bit = 0;
+#pragma unroll
+                for (int width = 32; width >= 1; width >>= 1) {
+                    const int c = __popcll(nm & ((1ull << width) - 1ull));
+                    if (kk >= c) { kk -= c; nm >>= width; bit += width; }
+                }
+                const int q = lo * 64 + bit;
                 const int t = e0 + q;
                 const int w = q >> 6, b = q & 63;
                 const unsigned long long m = mask[w];
@@ -337,7 +397,9 @@ __global__ __launch_bounds__(kThreads, 3) void tile_kernel(TileArgs a, int metho
                 vals[q] = f;
             }
         }
+        STAMP(6);
         __syncthreads();
+        STAMP(7);
 
         // ---- 5. filled output + lag matrix (16-B stores), then y = F - F(0) in place
         //      (0 past the series end) for the MFMA phase; start the next tile's loads ----
@@ -345,6 +407,35 @@ __global__ __launch_bounds__(kThreads, 3) void tile_kernel(TileArgs a, int metho
             const bool al = dst && ((reinterpret_cast<uintptr_t>(dst) & 15) == 0);
             double2* v2 = reinterpret_cast<double2*>(vals);
             const int qBfull = (NT > 0) ? ((qW + 64 + 16 * NT < EW) ? qW + 64 + 16 * NT : EW) : 0;
+            const bool fast = al && !a.lagmat && (t1 - t0 == TW) && (NT == 0 || qBfull == EW);
+            if (fast) {
+                // full interior tile: every LDS read first, then 16-B stores and the y rewrite
+                constexpr int FJ = (NP2 - kHB / 2 + kThreads - 1) / kThreads;
+                constexpr int FH = (FJ + 1) / 2;     // two halves: fewer live registers
+#pragma unroll
+                for (int h = 0; h < 2; h++) {
+                    double2 fv[FH];
+#pragma unroll
+                    for (int j = 0; j < FH; j++) {
+                        const int q2 = (qA >> 1) + tid + (h * FH + j) * kThreads;
+                        fv[j] = v2[q2 < NP2 ? q2 : NP2 - 1];
+                    }
+#pragma unroll
+                    for (int j = 0; j < FH; j++) {
+                        const int q2 = (qA >> 1) + tid + (h * FH + j) * kThreads;
+                        const int q = 2 * q2;
+                        if (h * FH + j < FJ && q2 < NP2) {
+                            if (q < qW) *reinterpret_cast<double2*>(dst + (e0 + q)) = fv[j];
+                            if (NT > 0) {
+                                double2 y;
+                                y.x = (q < qB) ? fv[j].x - c0 : 0.0;
+                                y.y = (q + 1 < qB) ? fv[j].y - c0 : 0.0;
+                                v2[q2] = y;
+                            }
+                        }
+                    }
+                }
+            } else
             for (int q2 = (qA >> 1) + tid; 2 * q2 < qW || 2 * q2 < qBfull; q2 += kThreads) {
                 const int q = 2 * q2;
                 double2 f = v2[q2];
@@ -377,9 +468,11 @@ __global__ __launch_bounds__(kThreads, 3) void tile_kernel(TileArgs a, int metho
         }
         if (have_next) STS_ISSUE(k + 1);   // in flight during the MFMA phase of tile k
         else STS_CLEAR();
+        STAMP(8);
 
         if constexpr (NT > 0) {
             __syncthreads();
+            STAMP(9);
             // ---- 6. lag products on MFMA: U_t += y(j0 + l) x y(j0 + 16t + l) ----
             constexpr int CPW = TW / 64 / kWaves;   // 64-step chunks per wave
             const int tlen = t1 - t0;
@@ -400,13 +493,22 @@ __global__ __launch_bounds__(kThreads, 3) void tile_kernel(TileArgs a, int metho
             }
         }
         have = have_next;
+        STAMP(10);
         __syncthreads();   // vals / mask / lists are reused by the next tile
+        STAMP(11);
     }
 #undef STS_ISSUE
 #undef STS_LD1
 #undef STS_ST1
 #undef STS_CLEAR
     if (series_err && a.err) a.err[s] = STS_ERR_ALL_NAN;
+#ifdef STS_STAMPS
+    if (lane == 0) {
+#pragma unroll
+        for (int i = 0; i < 12; i++) atomicAdd(&g_stamps[i], st_acc[i]);
+        atomicAdd(&g_stamps[12], 1ull);
+    }
+#endif
 
     if constexpr (NT > 0) {
         // ---- 7. diagonal extraction: lane i accumulates lag i in a fixed order ----
@@ -530,6 +632,14 @@ hipError_t launch_tile(int method, int tw, const TileArgs& a, hipStream_t st) {
     }
     return hipGetLastError();
 }
+
+#ifdef STS_STAMPS
+extern "C" int sts_debug_stamps(unsigned long long* out16) {
+    if (hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * 16) != hipSuccess) return 4;
+    unsigned long long z[16] = {0};
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), z, sizeof(z)) == hipSuccess ? 0 : 4;
+}
+#endif
 
 hipError_t launch_acf_finalize(const FinalizeArgs& a, hipStream_t st) {
     if (a.S <= 0 || a.K <= 0) return hipSuccess;
