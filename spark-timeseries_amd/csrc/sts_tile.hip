@@ -67,15 +67,16 @@ __device__ __forceinline__ int64_t xcd_remap(int64_t b, int64_t n) {
     return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
 }
 
-// bit i of x -> bit 2i (Morton spread of a 32-bit value), scalar ops
-__device__ __forceinline__ unsigned long long spread2(unsigned long long x) {
-    x &= 0xFFFFFFFFull;
-    x = (x | (x << 16)) & 0x0000FFFF0000FFFFull;
-    x = (x | (x << 8)) & 0x00FF00FF00FF00FFull;
-    x = (x | (x << 4)) & 0x0F0F0F0F0F0F0F0Full;
-    x = (x | (x << 2)) & 0x3333333333333333ull;
-    x = (x | (x << 1)) & 0x5555555555555555ull;
-    return x;
+// Interleave two 32-step validity ballots into one 64-step word: bit i of ev -> bit 2i,
+// bit i of od -> bit 2i + 1.  s_bitreplicate_b64_b32 doubles every bit (i -> 2i, 2i + 1)
+// in one scalar op; the masks keep the even / odd copy.
+__device__ __forceinline__ unsigned long long bitrep(unsigned x) {
+    unsigned long long r;
+    asm("s_bitreplicate_b64_b32 %0, %1" : "=s"(r) : "s"(x));
+    return r;
+}
+__device__ __forceinline__ unsigned long long interleave2(unsigned ev, unsigned od) {
+    return (bitrep(ev) & 0x5555555555555555ull) | (bitrep(od) & 0xAAAAAAAAAAAAAAAAull);
 }
 
 // Wave-wide search of global memory for the last valid index < from (stop at 0).
@@ -217,8 +218,8 @@ __global__ __launch_bounds__(kThreads, 3) void tile_kernel(TileArgs a, int metho
         const unsigned long long by_ = __ballot(!isnan_d(R##j.y));                          \
         const int w_ = 2 * wave + 8 * j;                                                    \
         if (lane == 0) {                                                                    \
-            if (w_ < NW) mask[w_] = spread2(bx_) | (spread2(by_) << 1);                     \
-            if (w_ + 1 < NW) mask[w_ + 1] = spread2(bx_ >> 32) | (spread2(by_ >> 32) << 1); \
+            if (w_ < NW) mask[w_] = interleave2((unsigned)bx_, (unsigned)by_);              \
+            if (w_ + 1 < NW) mask[w_ + 1] = interleave2((unsigned)(bx_ >> 32), (unsigned)(by_ >> 32)); \
         }                                                                                   \
     }
             STS_BAL1(0) STS_BAL1(1) STS_BAL1(2) STS_BAL1(3) STS_BAL1(4) STS_BAL1(5) STS_BAL1(6) STS_BAL1(7)
@@ -407,31 +408,40 @@ __global__ __launch_bounds__(kThreads, 3) void tile_kernel(TileArgs a, int metho
             const bool al = dst && ((reinterpret_cast<uintptr_t>(dst) & 15) == 0);
             double2* v2 = reinterpret_cast<double2*>(vals);
             const int qBfull = (NT > 0) ? ((qW + 64 + 16 * NT < EW) ? qW + 64 + 16 * NT : EW) : 0;
-            const bool fast = al && !a.lagmat && (t1 - t0 == TW) && (NT == 0 || qBfull == EW);
+            // fast path: a full tile not at the series end -- the written range is exactly
+            // [kHB, kHB + TW) and every y the MFMA phase reads is F - c0 (no zero tail), so
+            // every index and guard below is a compile-time constant
+            const bool fast = (dst == nullptr || al) && !a.lagmat && (t1 - t0 == TW) &&
+                              (NT == 0 || e0 + qW + 16 * NT <= T);
             if (fast) {
-                // full interior tile: every LDS read first, then 16-B stores and the y rewrite
-                constexpr int FJ = (NP2 - kHB / 2 + kThreads - 1) / kThreads;
-                constexpr int FH = (FJ + 1) / 2;     // two halves: fewer live registers
+                constexpr int FS = TW / 2 / kThreads;                          // stored double2
+                constexpr int FY = NT > 0 ? (NP2 - kHB / 2 + kThreads - 1) / kThreads : FS;
+                constexpr int FH = (FY + 1) / 2;     // two halves: fewer live registers
+                double2* vp = v2 + (kHB >> 1) + tid;
+                const bool wr = dst != nullptr;   // wave-uniform (a null test of dp is per lane)
+                double2* dp = reinterpret_cast<double2*>(dst + t0) + tid;
 #pragma unroll
                 for (int h = 0; h < 2; h++) {
                     double2 fv[FH];
 #pragma unroll
                     for (int j = 0; j < FH; j++) {
-                        const int q2 = (qA >> 1) + tid + (h * FH + j) * kThreads;
-                        fv[j] = v2[q2 < NP2 ? q2 : NP2 - 1];
+                        const int jj = h * FH + j;
+                        if (jj < FY && (jj * kThreads + kThreads <= NP2 - kHB / 2 ||
+                                        tid + jj * kThreads < NP2 - kHB / 2))
+                            fv[j] = vp[jj * kThreads];
                     }
 #pragma unroll
                     for (int j = 0; j < FH; j++) {
-                        const int q2 = (qA >> 1) + tid + (h * FH + j) * kThreads;
-                        const int q = 2 * q2;
-                        if (h * FH + j < FJ && q2 < NP2) {
-                            if (q < qW) *reinterpret_cast<double2*>(dst + (e0 + q)) = fv[j];
-                            if (NT > 0) {
-                                double2 y;
-                                y.x = (q < qB) ? fv[j].x - c0 : 0.0;
-                                y.y = (q + 1 < qB) ? fv[j].y - c0 : 0.0;
-                                v2[q2] = y;
-                            }
+                        const int jj = h * FH + j;
+                        if (jj >= FY) continue;
+                        const bool in = jj * kThreads + kThreads <= NP2 - kHB / 2 ||
+                                        tid + jj * kThreads < NP2 - kHB / 2;
+                        if (jj < FS && wr) dp[jj * kThreads] = fv[j];
+                        if (NT > 0 && in) {
+                            double2 y;
+                            y.x = fv[j].x - c0;
+                            y.y = fv[j].y - c0;
+                            vp[jj * kThreads] = y;
                         }
                     }
                 }
