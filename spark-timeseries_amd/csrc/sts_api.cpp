@@ -9,8 +9,10 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <cstdint>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -158,7 +160,13 @@ void prof_mark(hipStream_t st) {
 int run_tile(const double* in, double* out, double* lagmat, int64_t S, int64_t T, int64_t ld_in, int64_t ld_out,
              int method, int K, double* acf, int max_lag, int inc, int32_t* err, hipStream_t st, const char* name) {
     if (S == 0 || T == 0) return STS_OK;
-    const int tw = (K > 0) ? 4096 : tile_width(T);
+    // the workgroup tile kernel serves every call; the wave-private segment kernel is an
+    // opt-in alternative (STS_TILE_KERNEL=seg: aligned panels, no lag matrix, K <= 60)
+    const char* force = std::getenv("STS_TILE_KERNEL");
+    const bool seg = force && !std::strcmp(force, "seg") && !lagmat && sts::seg_nt(K) >= 0 &&
+                     (reinterpret_cast<uintptr_t>(in) & 15) == 0 && (ld_in % 2) == 0 &&
+                     (!out || ((reinterpret_cast<uintptr_t>(out) & 15) == 0 && ld_out % 2 == 0)) && T < 0x7fff0000LL;
+    const int tw = seg ? sts::kSegW : (K > 0) ? 4096 : tile_width(T);
     sts::TileArgs a{};
     a.in = in;
     a.out = out;
@@ -169,7 +177,8 @@ int run_tile(const double* in, double* out, double* lagmat, int64_t S, int64_t T
     a.ld_in = ld_in;
     a.ld_out = ld_out;
     a.tiles_per_series = (T + tw - 1) / tw;
-    a.tiles_per_chunk = a.tiles_per_series < kTilesPerChunk ? a.tiles_per_series : kTilesPerChunk;
+    const int64_t per_chunk = seg ? sts::kSegTiles : kTilesPerChunk;
+    a.tiles_per_chunk = a.tiles_per_series < per_chunk ? a.tiles_per_series : per_chunk;
     a.chunks_per_series = (a.tiles_per_series + a.tiles_per_chunk - 1) / a.tiles_per_chunk;
     a.K = K;
     a.max_lag = max_lag;
@@ -182,7 +191,7 @@ int run_tile(const double* in, double* out, double* lagmat, int64_t S, int64_t T
         a.partials = static_cast<double*>(part.p);
     }
     prof_mark(st);
-    hipError_t e = sts::launch_tile(method, tw, a, st);
+    hipError_t e = seg ? sts::launch_segment(method, a, st) : sts::launch_tile(method, tw, a, st);
     prof_mark(st);
     if (e != hipSuccess) return hip_fail(e, name);
     if (K > 0) {

@@ -43,6 +43,14 @@ struct FinalizeArgs {
 hipError_t launch_tile(int method, int tw, const TileArgs& a, hipStream_t st);
 hipError_t launch_acf_finalize(const FinalizeArgs& a, hipStream_t st);
 
+// Wave-private segment kernel (sts_seg.hip): tiles of kSegW steps, kSegTiles tiles per
+// wave.  TileArgs.tiles_per_series = ceil(T / kSegW), tiles_per_chunk = tiles per
+// segment, chunks_per_series = segments per series.  seg_nt(K) < 0: K not supported.
+constexpr int kSegW = 512;
+constexpr int kSegTiles = 128;
+int seg_nt(int K);
+hipError_t launch_segment(int method, const TileArgs& a, hipStream_t st);
+
 hipError_t launch_diff(const double* in, double* out, int64_t S, int64_t T, int64_t ld_in,
                        int64_t ld_out, int lag, int start, hipStream_t st);
 hipError_t launch_diff_inplace(double* x, int64_t S, int64_t T, int64_t ld, int lag, int start,

@@ -31,6 +31,10 @@
 
 #include <hip/hip_runtime.h>
 
+#ifndef STS_MFMA_PIPE
+#define STS_MFMA_PIPE 0   // experiment knob: software-pipelined MFMA operand loads
+#endif
+
 namespace sts {
 namespace {
 
@@ -101,15 +105,37 @@ __device__ int64_t scan_fwd(const double* src, int64_t from, int64_t T, int lane
     }
 }
 
-template <int TW, int NT>
+// Padded LDS index of extended-tile position q: 4 doubles of padding per 32.  Keeps the
+// lag-product B-operand gathers (16-step-spaced groups, see below) conflict-free across the
+// 64 LDS banks; 16-B pairs (even q) never straddle a pad.
+template <bool PAD>
+__device__ __forceinline__ int px_(int q) { return PAD ? q + ((q >> 5) << 2) : q; }
+template <bool PAD>
+__device__ __forceinline__ int px2_(int q2) { return PAD ? q2 + ((q2 >> 4) << 1) : q2; }   // double2 index
+
+// Lag-product decompositions (see the header): SHIFTED (K <= 60) uses NT = 2 or 4 MFMAs
+// per 64 steps with window shifts q*t (q = 16 / NT) and B columns h(j) = 16(j/q) + 16 - q
+// + j%q -- every lag 0 .. 16 NT - q exactly once per step, and the same lag map h(j) - i in
+// every accumulator; TOEPLITZ (K = 61..63) uses NT = floor((K + 15) / 16) + 1 MFMAs with
+// U_t holding lag 16t + j - i.
+template <int TW, int NT, bool SHIFTED>
 __global__ __launch_bounds__(kThreads, 3) void tile_kernel(TileArgs a, int method) {
     constexpr int EW = kHB + TW + kHA;
+    constexpr int NA = SHIFTED ? 2 : (NT > 0 ? NT : 1);      // MFMA accumulators
+    constexpr int QS = (SHIFTED && NT > 0) ? 16 / NT : 16;   // window shift step (shifted scheme)
+    // y is needed this far past the written range (A windows reach 4t <= 12 past the
+    // tile, and the used lags <= 60 past that; the Toeplitz scheme reaches 16 NT)
+    constexpr int REACH = (NT == 0) ? 0 : (SHIFTED ? 80 : 16 * NT);
+    constexpr bool PAD = SHIFTED && NT > 0;                  // padded LDS layout (B gathers)
+    constexpr int EWP = PAD ? EW + EW / 8 : EW;
+    auto px = [](int q) { return px_<PAD>(q); };
+    auto px2 = [](int q2) { return px2_<PAD>(q2); };
     constexpr int NW = EW / 64;
     constexpr int NP2 = EW / 2;                              // double2 per extended tile
     constexpr int RPT = (NP2 + kThreads - 1) / kThreads;     // prefetch registers per thread
     static_assert(EW % 64 == 0, "extended tile must be whole words");
     static_assert(NW <= 128, "word scan handles at most 128 words");
-    __shared__ __attribute__((aligned(16))) double vals[EW];
+    __shared__ __attribute__((aligned(16))) double vals[EWP];   // padded (px) for the shifted scheme
     __shared__ unsigned long long mask[NW];
     __shared__ int lastUpTo[NW];     // last valid E-position in words <= w (-1: none)
     __shared__ int firstFrom[NW];    // first valid E-position in words >= w (kBig: none)
@@ -120,7 +146,7 @@ __global__ __launch_bounds__(kThreads, 3) void tile_kernel(TileArgs a, int metho
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
-    const int wave = tid >> 6;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform: scalar loop control
     // one workgroup = one CHUNK of tiles_per_chunk consecutive tiles of one series
     const int64_t nchunk = a.S * a.chunks_per_series;
     const int64_t ch = xcd_remap(blockIdx.x, nchunk);
@@ -184,12 +210,12 @@ __global__ __launch_bounds__(kThreads, 3) void tile_kernel(TileArgs a, int metho
 #define STS_ST1(j)                                                                          \
     if constexpr (j < RPT) {                                                                \
         const int q2_ = tid + j * kThreads;                                                 \
-        if (q2_ < NP2) v2_[q2_] = R##j;                                                     \
+        if (q2_ < NP2) v2_[px2(q2_)] = R##j;                                                \
     }
 
-    d4 U[NT > 0 ? NT : 1];
+    d4 U[NA];
 #pragma unroll
-    for (int t = 0; t < (NT > 0 ? NT : 1); t++) U[t] = d4{0.0, 0.0, 0.0, 0.0};
+    for (int t = 0; t < NA; t++) U[t] = d4{0.0, 0.0, 0.0, 0.0};
     double sy = 0.0;
     bool series_err = false;
 
@@ -228,7 +254,7 @@ __global__ __launch_bounds__(kThreads, 3) void tile_kernel(TileArgs a, int metho
         } else {
             for (int q = tid; q < EW; q += kThreads) {
                 const int t = e0 + q;
-                vals[q] = (t >= 0 && t < T) ? src[t] : __builtin_nan("");
+                vals[px(q)] = (t >= 0 && t < T) ? src[t] : __builtin_nan("");
             }
         }
         const bool have_next = (k + 1 < k_end) && interior(k + 1);
@@ -236,10 +262,10 @@ __global__ __launch_bounds__(kThreads, 3) void tile_kernel(TileArgs a, int metho
         __syncthreads();
         STAMP(1);
 
-        // positions to produce: [qA, qB) (E-relative); the ACF needs 16*NT steps past the tile
+        // positions to produce: [qA, qB) (E-relative); the ACF needs REACH steps past the tile
         const int qA = kHB;
         const int qW = kHB + (t1 - t0);                  // end of the written range
-        int qB = qW + (NT > 0 ? 16 * NT : 0);
+        int qB = qW + REACH;
         if (e0 + qB > T) qB = (int)T - e0;
 
         // ---- 2. validity ballots from LDS for the edge tiles (wave v owns words v, v+4, ...) ----
@@ -248,7 +274,7 @@ __global__ __launch_bounds__(kThreads, 3) void tile_kernel(TileArgs a, int metho
             for (int i = 0; i < (NW + kWaves - 1) / kWaves; i++) {
                 const int w = wave + i * kWaves;
                 if (w < NW) {
-                    const unsigned long long m = __ballot(!isnan_d(vals[w * 64 + lane]));
+                    const unsigned long long m = __ballot(!isnan_d(vals[px(w * 64 + lane)]));
                     if (lane == 0) mask[w] = m;
                 }
             }
@@ -360,13 +386,13 @@ __global__ __launch_bounds__(kThreads, 3) void tile_kernel(TileArgs a, int metho
                 if (needL) {
                     const unsigned long long lo = m & ((1ull << b) - 1ull);
                     const int Lq = lo ? w * 64 + 63 - __clzll(lo) : (w > 0 ? lastUpTo[w - 1] : -1);
-                    if (Lq >= 0) { Lt = e0 + Lq; Lv = vals[Lq]; }
+                    if (Lq >= 0) { Lt = e0 + Lq; Lv = vals[px(Lq)]; }
                     else { Lt = lext; Lv = lextv; }
                 }
                 if (needN) {
                     const unsigned long long hi = (b == 63) ? 0ull : (m & (~0ull << (b + 1)));
                     const int Nq = hi ? w * 64 + __ffsll(hi) - 1 : (w + 1 < NW ? firstFrom[w + 1] : kBig);
-                    if (Nq < kBig) { Nt = e0 + Nq; Nv = vals[Nq]; }
+                    if (Nq < kBig) { Nt = e0 + Nq; Nv = vals[px(Nq)]; }
                     else { Nt = next; Nv = nextv; }
                 }
                 double f = __builtin_nan("");
@@ -395,7 +421,7 @@ __global__ __launch_bounds__(kThreads, 3) void tile_kernel(TileArgs a, int metho
                 default:
                     break;
                 }
-                vals[q] = f;
+                vals[px(q)] = f;
             }
         }
         STAMP(6);
@@ -407,17 +433,17 @@ __global__ __launch_bounds__(kThreads, 3) void tile_kernel(TileArgs a, int metho
         {
             const bool al = dst && ((reinterpret_cast<uintptr_t>(dst) & 15) == 0);
             double2* v2 = reinterpret_cast<double2*>(vals);
-            const int qBfull = (NT > 0) ? ((qW + 64 + 16 * NT < EW) ? qW + 64 + 16 * NT : EW) : 0;
+            const int qBfull = (NT > 0) ? ((SHIFTED || qW + 64 + 16 * NT >= EW) ? EW : qW + 64 + 16 * NT) : 0;
             // fast path: a full tile not at the series end -- the written range is exactly
             // [kHB, kHB + TW) and every y the MFMA phase reads is F - c0 (no zero tail), so
             // every index and guard below is a compile-time constant
             const bool fast = (dst == nullptr || al) && !a.lagmat && (t1 - t0 == TW) &&
-                              (NT == 0 || e0 + qW + 16 * NT <= T);
+                              (NT == 0 || e0 + qW + REACH <= T);
             if (fast) {
                 constexpr int FS = TW / 2 / kThreads;                          // stored double2
                 constexpr int FY = NT > 0 ? (NP2 - kHB / 2 + kThreads - 1) / kThreads : FS;
                 constexpr int FH = (FY + 1) / 2;     // two halves: fewer live registers
-                double2* vp = v2 + (kHB >> 1) + tid;
+                const int vq = (kHB >> 1) + tid;
                 const bool wr = dst != nullptr;   // wave-uniform (a null test of dp is per lane)
                 double2* dp = reinterpret_cast<double2*>(dst + t0) + tid;
 #pragma unroll
@@ -428,7 +454,7 @@ __global__ __launch_bounds__(kThreads, 3) void tile_kernel(TileArgs a, int metho
                         const int jj = h * FH + j;
                         if (jj < FY && (jj * kThreads + kThreads <= NP2 - kHB / 2 ||
                                         tid + jj * kThreads < NP2 - kHB / 2))
-                            fv[j] = vp[jj * kThreads];
+                            fv[j] = v2[px2(vq + jj * kThreads)];
                     }
 #pragma unroll
                     for (int j = 0; j < FH; j++) {
@@ -441,14 +467,14 @@ __global__ __launch_bounds__(kThreads, 3) void tile_kernel(TileArgs a, int metho
                             double2 y;
                             y.x = fv[j].x - c0;
                             y.y = fv[j].y - c0;
-                            vp[jj * kThreads] = y;
+                            v2[px2(vq + jj * kThreads)] = y;
                         }
                     }
                 }
             } else
             for (int q2 = (qA >> 1) + tid; 2 * q2 < qW || 2 * q2 < qBfull; q2 += kThreads) {
                 const int q = 2 * q2;
-                double2 f = v2[q2];
+                double2 f = v2[px2(q2)];
                 if (q < qW) {
                     const int t = e0 + q;
                     if (dst) {
@@ -472,9 +498,12 @@ __global__ __launch_bounds__(kThreads, 3) void tile_kernel(TileArgs a, int metho
                 if (NT > 0 && q < qBfull) {
                     f.x = (q < qB) ? f.x - c0 : 0.0;
                     f.y = (q + 1 < qB) ? f.y - c0 : 0.0;
-                    v2[q2] = f;
+                    v2[px2(q2)] = f;
                 }
             }
+            // shifted scheme, first tile: the pre-chunk (positions [0, 4t) of the series) reads
+            // the look-back range as y = 0
+            if (SHIFTED && NT > 0 && e0 < 0 && tid < kHB / 2) v2[px2(tid)] = make_double2(0.0, 0.0);
         }
         if (have_next) STS_ISSUE(k + 1);   // in flight during the MFMA phase of tile k
         else STS_CLEAR();
@@ -483,23 +512,86 @@ __global__ __launch_bounds__(kThreads, 3) void tile_kernel(TileArgs a, int metho
         if constexpr (NT > 0) {
             __syncthreads();
             STAMP(9);
-            // ---- 6. lag products on MFMA: U_t += y(j0 + l) x y(j0 + 16t + l) ----
+            // ---- 6. lag products on MFMA ----
             constexpr int CPW = TW / 64 / kWaves;   // 64-step chunks per wave
             const int tlen = t1 - t0;
             const int nch = (tlen + 63) / 64;
             int c = wave * CPW;
             int cend = c + CPW;
             if (cend > nch) cend = nch;
-            for (; c < cend; c++) {
-                const int jrel = 64 * c + lane;
-                const double* yb = vals + qA + jrel;
-                double bv[NT];
+            if constexpr (SHIFTED) {
+                // A = y(chunk + QS t + lane), B = y(chunk + QS t + 16 (lane >> 4) + h(lane & 15));
+                // wave 0 of the first tile also runs chunk -1 (the look-back, y = 0), whose
+                // shifted windows hold the series' first QS t steps
+                // per-lane operand offsets (padded) relative to a chunk start
+                int oa[NT], ob[NT];
 #pragma unroll
-                for (int t = 0; t < NT; t++) bv[t] = yb[16 * t];
-                const double av = (jrel < tlen) ? bv[0] : 0.0;   // A only inside the tile
+                for (int t = 0; t < NT; t++) {
+                    const int j = lane & 15;
+                    const int ra = QS * t + lane;
+                    const int rb = QS * t + 16 * (lane >> 4) + 16 * (j / QS) + (16 - QS) + (j % QS);
+                    oa[t] = px(ra);
+                    ob[t] = px(rb);
+                }
+                auto chunk_mfma = [&](const double* yb) {
+                    double av[NT], bv[NT];
 #pragma unroll
-                for (int t = 0; t < NT; t++) U[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv[t], U[t], 0, 0, 0);
-                sy += av;
+                    for (int t = 0; t < NT; t++) {
+                        av[t] = yb[oa[t]];
+                        bv[t] = yb[ob[t]];
+                    }
+#pragma unroll
+                    for (int t = 0; t < NT; t++)
+                        U[t % NA] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[t], bv[t], U[t % NA], 0, 0, 0);
+                    sy += av[0];
+                };
+                // wave 0 of the first tile also runs chunk -1 (the look-back, y = 0), whose
+                // shifted windows hold the series' first QS t steps
+                if (k == 0 && wave == 0) chunk_mfma(vals);
+#if STS_MFMA_PIPE
+                // software pipeline: chunk c + 1's operands load while chunk c's MFMAs run
+                if (c < cend) {
+                    double av[NT], bv[NT];
+                    const double* yb = vals + px(qA + 64 * c);
+#pragma unroll
+                    for (int t = 0; t < NT; t++) {
+                        av[t] = yb[oa[t]];
+                        bv[t] = yb[ob[t]];
+                    }
+                    for (; c < cend; c++) {
+                        double an[NT], bn[NT];
+                        const double* yn = vals + px(qA + 64 * (c + 1 < cend ? c + 1 : c));
+#pragma unroll
+                        for (int t = 0; t < NT; t++) {
+                            an[t] = yn[oa[t]];
+                            bn[t] = yn[ob[t]];
+                        }
+#pragma unroll
+                        for (int t = 0; t < NT; t++)
+                            U[t % NA] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[t], bv[t], U[t % NA], 0, 0, 0);
+                        sy += av[0];
+#pragma unroll
+                        for (int t = 0; t < NT; t++) {
+                            av[t] = an[t];
+                            bv[t] = bn[t];
+                        }
+                    }
+                }
+#else
+                for (; c < cend; c++) chunk_mfma(vals + px(qA + 64 * c));   // chunk start: a multiple of 32
+#endif
+            } else {
+                // U_t += y(j0 + l) x y(j0 + 16t + l)
+                for (; c < cend; c++) {
+                    const int jrel = 64 * c + lane;
+                    double bv[NT];
+#pragma unroll
+                    for (int t = 0; t < NT; t++) bv[t] = vals[px(qA + jrel + 16 * t)];
+                    const double av = (jrel < tlen) ? bv[0] : 0.0;   // A only inside the tile
+#pragma unroll
+                    for (int t = 0; t < NT; t++) U[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv[t], U[t], 0, 0, 0);
+                    sy += av;
+                }
             }
         }
         have = have_next;
@@ -521,18 +613,33 @@ __global__ __launch_bounds__(kThreads, 3) void tile_kernel(TileArgs a, int metho
 #endif
 
     if constexpr (NT > 0) {
-        // ---- 7. diagonal extraction: lane i accumulates lag i in a fixed order ----
+        // ---- 7. diagonal extraction: lane d accumulates lag d in a fixed order ----
         double* scr = vals + wave * 256;
         double lagacc = 0.0;
+        if constexpr (SHIFTED) {
+            d4 D = U[0];
 #pragma unroll
-        for (int t = 0; t < NT; t++) {
+            for (int t = 1; t < NA; t++) D += U[t];
 #pragma unroll
-            for (int r = 0; r < 4; r++) scr[((lane >> 4) + 4 * r) * 16 + (lane & 15)] = U[t][r];
+            for (int r = 0; r < 4; r++) scr[((lane >> 4) + 4 * r) * 16 + (lane & 15)] = D[r];
             __syncthreads();
 #pragma unroll
-            for (int b = 0; b < 16; b++)
-                if (((b + lane) >> 4) == t) lagacc += scr[b * 16 + ((b + lane) & 15)];
+            for (int j = 0; j < 16; j++) {
+                const int i = 16 * (j / QS) + (16 - QS) + (j % QS) - lane;   // entry (i, j) holds lag h(j) - i
+                if (i >= 0 && i < 16) lagacc += scr[i * 16 + j];
+            }
             __syncthreads();
+        } else {
+#pragma unroll
+            for (int t = 0; t < NT; t++) {
+#pragma unroll
+                for (int r = 0; r < 4; r++) scr[((lane >> 4) + 4 * r) * 16 + (lane & 15)] = U[t][r];
+                __syncthreads();
+#pragma unroll
+                for (int b = 0; b < 16; b++)
+                    if (((b + lane) >> 4) == t) lagacc += scr[b * 16 + ((b + lane) & 15)];
+                __syncthreads();
+            }
         }
 #pragma unroll
         for (int d = 32; d >= 1; d >>= 1) sy += __shfl_xor(sy, d);
@@ -624,19 +731,14 @@ hipError_t launch_tile(int method, int tw, const TileArgs& a, hipStream_t st) {
     if (nchunk <= 0) return hipSuccess;
     if (nchunk > 0x7fffffffLL) return hipErrorInvalidValue;
     dim3 grid((unsigned)nchunk), block(kThreads);
-    int nt = 0;
-    if (a.K > 0) nt = (a.K + 15) / 16 + 1;
-    if (tw == 512 && nt == 0) {
-        hipLaunchKernelGGL((tile_kernel<512, 0>), grid, block, 0, st, a, method);
+    if (tw == 512 && a.K == 0) {
+        hipLaunchKernelGGL((tile_kernel<512, 0, false>), grid, block, 0, st, a, method);
     } else if (tw == 4096) {
-        switch (nt) {
-        case 0: hipLaunchKernelGGL((tile_kernel<4096, 0>), grid, block, 0, st, a, method); break;
-        case 2: hipLaunchKernelGGL((tile_kernel<4096, 2>), grid, block, 0, st, a, method); break;
-        case 3: hipLaunchKernelGGL((tile_kernel<4096, 3>), grid, block, 0, st, a, method); break;
-        case 4: hipLaunchKernelGGL((tile_kernel<4096, 4>), grid, block, 0, st, a, method); break;
-        case 5: hipLaunchKernelGGL((tile_kernel<4096, 5>), grid, block, 0, st, a, method); break;
-        default: return hipErrorInvalidValue;
-        }
+        if (a.K == 0) hipLaunchKernelGGL((tile_kernel<4096, 0, false>), grid, block, 0, st, a, method);
+        else if (a.K <= 24) hipLaunchKernelGGL((tile_kernel<4096, 2, true>), grid, block, 0, st, a, method);
+        else if (a.K <= 60) hipLaunchKernelGGL((tile_kernel<4096, 4, true>), grid, block, 0, st, a, method);
+        else if (a.K <= 63) hipLaunchKernelGGL((tile_kernel<4096, 5, false>), grid, block, 0, st, a, method);
+        else return hipErrorInvalidValue;
     } else {
         return hipErrorInvalidValue;
     }

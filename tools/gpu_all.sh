@@ -1,0 +1,26 @@
+#!/bin/bash
+# One GPU session: every workload's bench line, the rocprof stats of the default bench
+# command, and FETCH_SIZE / WRITE_SIZE passes.  Every GPU step has its own time limit; a
+# step that dies by signal/timeout (rc >= 124) or fails ends the session.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+step() {  # step <name> <seconds> <cmd...>
+  local name=$1 secs=$2; shift 2
+  echo "=== $name $(date +%T)" >&2
+  timeout -k 10 "$secs" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc" >&2
+  tail -3 "gpurun_out/$name.log" >&2
+  if [ $rc -ne 0 ]; then echo "stopping: $name rc=$rc" >&2; exit $rc; fi
+}
+for s in ${STEPS:-c1 c2 c4 c5 prof fetch write}; do
+  case $s in
+    c1|c2|c3|c4|c5) step bench_$s 300 python -u bench.py --workload $s ;;
+    prof) step prof_c3 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_c3 -o bench --output-format csv -- python -u bench.py ;;
+    fetch) step pmc_fetch_c3 300 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch_c3 -o bench --output-format csv -- python -u bench.py --steps 2 --warmup 0 --no-cpu-baseline ;;
+    write) step pmc_write_c3 300 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write_c3 -o bench --output-format csv -- python -u bench.py --steps 2 --warmup 0 --no-cpu-baseline ;;
+    tests) step pytest_gpu 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider ;;
+    custom) step custom ${CUSTOM_SECS:-300} bash -c "$CUSTOM_CMD" ;;
+  esac
+done
