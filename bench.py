@@ -155,27 +155,26 @@ def main():
     elems = float(S) * T * world * args.steps
     value = elems / elapsed
     ms_per_step = elapsed / args.steps * 1e3
-    # dominant kernel: the fused series-tile kernel (fill + ACF partials / fill only)
-    bytes_per_step = 16.0 * S * T        # 8 B read + 8 B filled write per element
+    # dominant kernel (one launch per step, or one per lag-matrix batch for c5), timed with
+    # HIP events the library records on the launch stream (sts_profile_begin/end)
+    bytes_per_step = 16.0 * S * T        # 8 B read + 8 B written per element
     if args.workload == "c5":            # + the lag matrix: 8 * P bytes per row, (T - P) rows per series
         bytes_per_step += 8.0 * P * (T - P) * S
-    bytes_per_launch = bytes_per_step * args.steps / max(1, launches[0])
+    kernel = {"c3": "sts::tile_kernel<4096,4,shifted> (fill linear + ACF partials, FP64 MFMA)",
+              "c1": "sts::tile_kernel<4096,2,shifted> (fill linear + ACF partials, FP64 MFMA)",
+              "c5": "sts::tile_kernel<4096,0> (fill nearest + lag-matrix columns)",
+              "c2": "sts::recur_kernel<kFillDiffEwma> (fillPrevious -> differencesAtLag(1) -> EWMA add, lane per series)",
+              "c4": "sts::ar_fit_kernel (AR(5) Gram on FP64 MFMA + solve + fused remove)"}[args.workload]
     roofline = None
-    if args.workload in ("c3", "c1", "c5") and launches[0] > 0:
+    if launches[0] > 0:
         avg_ms = kern_ms[0] / launches[0]
-        achieved = bytes_per_step * args.steps / (kern_ms[0] * 1e-3) / 1e9
+        bytes_per_launch = bytes_per_step * args.steps / launches[0]
+        achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9
         roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                    "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": None,
-                    "kernel": {"c3": "sts::tile_kernel<4096,5> (fill linear + ACF partials, FP64 MFMA)",
-                               "c1": "sts::tile_kernel<4096,3> (fill linear + ACF partials, FP64 MFMA)",
-                               "c5": "sts::tile_kernel<4096,0> (fill nearest + lag-matrix columns)"}[args.workload],
-                    "avg_kernel_ms": round(avg_ms, 4), "bytes_per_launch": bytes_per_launch}
-    elif launches[0] == 0:
-        step_bytes = 16.0 * S * T
-        achieved = step_bytes / (ms_per_step * 1e-3) / 1e9 / 1.0
-        roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                    "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": None,
-                    "note": "whole-step time (single kernel per step)"}
+                    "frac": round(achieved / HBM_PEAK_GBPS, 4),
+                    "traffic": measured_traffic(args.workload, S, T), "kernel": kernel,
+                    "avg_kernel_ms": round(avg_ms, 4), "bytes_per_launch": bytes_per_launch,
+                    "kernel_launches_timed": int(launches[0])}
 
     cpu = None
     if rank == 0 and not args.no_cpu_baseline:
@@ -198,6 +197,21 @@ def main():
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def measured_traffic(workload, S, T):
+    """HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC passes
+    (profiles/<round>_c3_traffic.json, written by tools/collect.py from separate FETCH_SIZE
+    / WRITE_SIZE passes over this same default workload); None when no pass covers it."""
+    import glob
+    if workload != "c3" or (S, T) != WORKLOADS["c3"][:2]:
+        return None
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_c3_traffic.json")))
+    if not files:
+        return None
+    with open(files[-1]) as f:
+        rec = json.load(f)
+    return rec.get("traffic_bytes_per_launch")
 
 
 def cpu_baseline(args, S, T, K, seed, nan_p, out, acf, p_ar):

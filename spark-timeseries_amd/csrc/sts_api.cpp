@@ -156,6 +156,15 @@ void prof_mark(hipStream_t st) {
     (void)hipEventRecord(g_prof.pool[g_prof.used++], st);
 }
 
+// a kernel launch bracketed by profiling events (bench.py's per-kernel timing)
+template <typename F>
+hipError_t timed(hipStream_t st, F&& launch) {
+    prof_mark(st);
+    const hipError_t e = launch();
+    prof_mark(st);
+    return e;
+}
+
 // fill (+ optional ACF partials / lag matrix) through the tile kernel
 int run_tile(const double* in, double* out, double* lagmat, int64_t S, int64_t T, int64_t ld_in, int64_t ld_out,
              int method, int K, double* acf, int max_lag, int inc, int32_t* err, hipStream_t st, const char* name) {
@@ -463,7 +472,7 @@ static int ar_fit_common(const double* in, double* out, int64_t S, int64_t T, in
     sts::ArArgs a{};
     a.in = in; a.out = out; a.c = c; a.coef = coef; a.err = es.dev;
     a.S = S; a.T = T; a.ld_in = ld_in; a.ld_out = ld_out; a.p = p; a.no_intercept = no_intercept ? 1 : 0;
-    HIP_TRY(sts::launch_ar_fit(a, st), name);
+    HIP_TRY(timed(st, [&] { return sts::launch_ar_fit(a, st); }), name);
     return es.finish(name);
 }
 
@@ -497,7 +506,7 @@ int sts_fill_diff_ewma(const double* in, double* out, int64_t S, int64_t T, int6
         sts::RecurArgs a{};
         a.in = in; a.out = out; a.S = S; a.T = T; a.ld_in = ld_in; a.ld_out = ld_out; a.sm = smoothing;
         a.lag = lag; a.start = lag; a.method = method;
-        HIP_TRY(sts::launch_recur(sts::kFillDiffEwma, a, st), "fill_diff_ewma");
+        HIP_TRY(timed(st, [&] { return sts::launch_recur(sts::kFillDiffEwma, a, st); }), "fill_diff_ewma");
         return es.finish("fill_diff_ewma");
     }
     // general composition: fill -> (in place) differences -> (in place) EWMA add, all on `out`
