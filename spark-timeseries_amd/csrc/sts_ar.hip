@@ -18,6 +18,8 @@
 
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 namespace sts {
 namespace {
 
@@ -238,11 +240,356 @@ __global__ __launch_bounds__(64) void ar_fit_kernel(ArArgs a, int NT) {
     }
 }
 
+
+// ---------------------------------------------------------------------------------------
+// Register-resident variant for short series and small p (C4: T = 2,520, p = 5): one WAVE
+// per series, four independent waves per workgroup.  Lane l owns the contiguous block of
+// B steps [lB, lB + B) in registers, so every lagged operand of the three passes (lag
+// products, refinement residuals, the fused remove) is a static register index; only the
+// first p steps of a block need the previous lane's last p values (one wave shuffle per
+// pass).  No LDS beyond the head/tail terms; the block loads/stores are 16 B per lane.
+// The lag products P_0..P_p are lane-local FP64 FMAs: for p <= 8 the 16 x 16 MFMA tile
+// would compute >= 24 lags to use p + 1 of them, and on MI355X the FP64 VALU and FP64
+// MFMA peaks are equal (profiles/r01_ubench_fp64.jsonl).  The (p+1) x (p+1) Gram and the
+// Cholesky are lane-parallel (lane j owns row j).  Same algebra as ar_fit_kernel: centred
+// data, Gram from lag products minus head/tail terms, Cholesky + one step of refinement
+// against an exact residual pass (corrected semi-normal equations: Householder-QR accuracy).
+constexpr int kRegPB = 8;             // p <= kRegPB
+constexpr int kRegWaves = 4;
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d);
+    return v;
+}
+
+#ifdef STS_STAMPS
+__device__ unsigned long long g_ar_stamps[16];
+#define AR_STAMP(i)                                                                          \
+    do {                                                                                     \
+        const unsigned long long now_ = __builtin_amdgcn_s_memtime();                       \
+        st_acc[i] += now_ - st_prev;                                                         \
+        st_prev = now_;                                                                      \
+    } while (0)
+#else
+#define AR_STAMP(i) \
+    do {            \
+    } while (0)
+#endif
+
+struct ArWaveLds {
+    double L[(kRegPB + 1) * (kRegPB + 1)];   // Cholesky factor rows (1-based block)
+    double cs[kRegPB + 1];                   // column sums of the design
+    double head[kRegPB];                     // Y(0 .. p-1)
+    double tail[kRegPB];                     // Y(T-p .. T-1)
+};
+
+#ifndef STS_AR_WAVES_PER_EU
+#define STS_AR_WAVES_PER_EU 2   // 256 VGPRs: the block (2B), windows and Gram rows stay spill-free
+#endif
+template <int P, int B>
+__global__ __launch_bounds__(64 * kRegWaves, STS_AR_WAVES_PER_EU) void ar_fit_blk_kernel(ArArgs a) {
+    __shared__ ArWaveLds lds[kRegWaves];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int64_t s = (int64_t)blockIdx.x * kRegWaves + wave;
+    if (s >= a.S) return;
+    ArWaveLds& w = lds[wave];
+    const int T = (int)a.T;
+    const int t0 = lane * B;                  // this lane's block [t0, t0 + B)
+    const double* xg = a.in + s * a.ld_in;
+    const bool intercept = !a.no_intercept;
+#ifdef STS_STAMPS
+    unsigned long long st_acc[8] = {0};
+    unsigned long long st_prev = __builtin_amdgcn_s_memtime();
+#endif
+
+    // ---- the block into registers (16 B per lane per load when aligned); mean ----
+    double x[B];
+    const bool full = (t0 + B <= T);
+    const bool al = ((reinterpret_cast<uintptr_t>(xg) & 15) == 0) && (B % 2 == 0);
+    if (full && al) {
+        const double2* s2 = reinterpret_cast<const double2*>(xg + t0);
+#pragma unroll
+        for (int j = 0; j < B / 2; j++) {
+            const double2 v = s2[j];
+            x[2 * j] = v.x;
+            x[2 * j + 1] = v.y;
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < B; j++) {
+            const int t = t0 + j;
+            const double v = xg[t < T ? t : T - 1];
+            x[j] = (t < T) ? v : 0.0;
+        }
+    }
+    double part = 0.0;
+#pragma unroll
+    for (int j = 0; j < B; j++) part += x[j];
+    part = wave_sum(part);
+    const double mu = intercept ? part / (double)T : 0.0;
+    AR_STAMP(0);
+    // the previous lane's last P raw values (0 before the series)
+    double xp[P + 1];
+#pragma unroll
+    for (int k = 1; k <= P; k++) {
+        const double v = __shfl_up(x[B - k], 1);
+        xp[k] = (lane > 0) ? v : 0.0;
+    }
+    // y at block offset j - k (k >= 1 may reach into the previous lane's block)
+    auto Y = [&](int j) -> double { return (t0 + j < T) ? x[j] - mu : 0.0; };
+    auto Yprev = [&](int k) -> double { return (lane > 0) ? xp[k] - mu : 0.0; };
+
+    // ---- lag products P_d = sum_t y_t y_{t-d}; head / tail of the series to LDS ----
+    double Pd[P + 1];
+#pragma unroll
+    for (int d = 0; d <= P; d++) Pd[d] = 0.0;
+    double sy = 0.0;
+    {
+        double win[P + 1];                    // win[k] = y_{t-k}: a rolling window, no arrays of B
+#pragma unroll
+        for (int k = 1; k <= P; k++) win[k] = Yprev(k);
+#pragma unroll
+        for (int j = 0; j < B; j++) {
+            const double yj = Y(j);
+            sy += yj;
+            Pd[0] += yj * yj;
+#pragma unroll
+            for (int d = 1; d <= P; d++) Pd[d] += yj * win[d];
+#pragma unroll
+            for (int k = P; k >= 2; k--) win[k] = win[k - 1];
+            win[1] = yj;
+            if (j < P && lane == 0) w.head[j] = yj;
+            const int t = t0 + j;
+            if (t >= T - P && t < T) w.tail[t - (T - P)] = yj;
+        }
+    }
+    AR_STAMP(1);
+    sy = wave_sum(sy);
+#pragma unroll
+    for (int d = 0; d <= P; d++) Pd[d] = wave_sum(Pd[d]);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+    AR_STAMP(2);
+    // Y(u) for u in the head [0, P) or the tail [T - P, T) (T >= 2P + 1: disjoint)
+    auto Yh = [&](int u) -> double { return (u < P) ? w.head[u] : w.tail[u - (T - P)]; };
+
+    // ---- Gram of [Y | X_1..X_p], lane-parallel: lane j < P + 1 holds row j ----
+    const int m = T - P;
+    const double fm = (double)m;
+    const int jr = (lane <= P) ? lane : P;
+    double row[P + 1];
+#pragma unroll
+    for (int k = 0; k <= P; k++) {
+        const int lo = jr < k ? jr : k, hi = jr < k ? k : jr, d = hi - lo;
+        double g = 0.0;
+#pragma unroll
+        for (int dd = 0; dd <= P; dd++)
+            if (dd == d) g = Pd[dd];
+        for (int u = 0; u < P - hi; u++) g -= Yh(u) * Yh(u + d);           // head rows
+        for (int u = T - hi; u <= T - 1 - d; u++) g -= Yh(u) * Yh(u + d);  // tail rows
+        row[k] = g;
+    }
+    double csj = sy;                                                        // column sums
+    for (int u = 0; u < P - jr; u++) csj -= Yh(u);
+    for (int u = T - jr; u < T; u++) csj -= Yh(u);
+    const bool bad = __builtin_isnan(sy) || __builtin_isnan(part);
+
+    // ---- centred normal equations (intercept eliminated); rhs_j = row[0] ----
+    if (intercept) {
+#pragma unroll
+        for (int k = 0; k <= P; k++) row[k] -= csj * __shfl(csj, k) / fm;
+    }
+    // ---- Cholesky of the 1..P block, lane-parallel (lane i owns row i of L) ----
+    bool ok = true;
+#pragma unroll
+    for (int j = 1; j <= P; j++) {
+        const double djj = __shfl(row[j], j);
+        ok = ok && (djj > 0.0);
+        const double l = __builtin_sqrt(djj);
+        if (lane == j) row[j] = l;
+        else if (lane > j) row[j] = row[j] / l;
+#pragma unroll
+        for (int k = j + 1; k <= P; k++) {
+            const double lkj = __shfl(row[j], k);
+            if (lane >= k) row[k] -= row[j] * lkj;
+        }
+    }
+    if (lane <= P) {
+#pragma unroll
+        for (int k = 0; k <= P; k++) w.L[lane * (kRegPB + 1) + k] = row[k];
+        w.cs[lane] = csj;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+    auto Lu = [&](int i, int k) -> double { return w.L[i * (kRegPB + 1) + k]; };
+    auto solve = [&](double (&z)[P + 1]) {
+#pragma unroll
+        for (int i = 1; i <= P; i++) {
+            double v = z[i];
+#pragma unroll
+            for (int k = 1; k < i; k++) v -= Lu(i, k) * z[k];
+            z[i] = v / Lu(i, i);
+        }
+#pragma unroll
+        for (int i = P; i >= 1; i--) {
+            double v = z[i];
+#pragma unroll
+            for (int k = i + 1; k <= P; k++) v -= Lu(k, i) * z[k];
+            z[i] = v / Lu(i, i);
+        }
+    };
+    double phi[P + 1];
+    phi[0] = 0.0;
+#pragma unroll
+    for (int i = 1; i <= P; i++) phi[i] = __shfl(row[0], i);
+    const int status = (!bad && !ok) ? STS_ERR_SINGULAR : STS_OK;
+    double cpr = 0.0;
+    if (!bad && ok) {
+        solve(phi);
+        double sc = w.cs[0];
+#pragma unroll
+        for (int k = 1; k <= P; k++) sc -= phi[k] * w.cs[k];
+        cpr = intercept ? sc / fm : 0.0;
+        AR_STAMP(3);
+
+        // ---- refinement: exact residual pass e_t = Y_t - c' - sum_k phi_k Y_{t-k},
+        //      rows t = P .. T-1 of the lag design ----
+        double g[P + 1];
+#pragma unroll
+        for (int k = 0; k <= P; k++) g[k] = 0.0;
+        {
+            // x "changes" here: y_t = x_t - mu is recomputed instead of being kept live
+            // from the lag-product pass (2B more VGPRs)
+#pragma unroll
+            for (int j = 0; j < B; j++) asm volatile("" : "+v"(x[j]));
+            double win[P + 1];
+#pragma unroll
+            for (int k = 1; k <= P; k++) win[k] = Yprev(k);
+#pragma unroll
+            for (int j = 0; j < B; j++) {
+                const double yj = Y(j);
+                double e = yj - cpr;
+#pragma unroll
+                for (int k = 1; k <= P; k++) e -= phi[k] * win[k];
+                const int t = t0 + j;
+                e = (t >= P && t < T) ? e : 0.0;
+                g[0] += e;
+#pragma unroll
+                for (int k = 1; k <= P; k++) g[k] += e * win[k];
+#pragma unroll
+                for (int k = P; k >= 2; k--) win[k] = win[k - 1];
+                win[1] = yj;
+            }
+        }
+        AR_STAMP(4);
+#pragma unroll
+        for (int k = 0; k <= P; k++) g[k] = wave_sum(g[k]);
+        double z[P + 1];
+        const double g0 = g[0];
+#pragma unroll
+        for (int i = 1; i <= P; i++) z[i] = g[i] - (intercept ? w.cs[i] * g0 / fm : 0.0);
+        z[0] = 0.0;
+        solve(z);
+        double dc = g0;
+#pragma unroll
+        for (int k = 1; k <= P; k++) dc -= z[k] * w.cs[k];
+        double sphi = 0.0;
+#pragma unroll
+        for (int k = 1; k <= P; k++) {
+            phi[k] += z[k];
+            sphi += phi[k];
+        }
+        // un-shift: y = x - mu  =>  c = c' + mu * (1 - sum phi)
+        cpr = intercept ? (cpr + dc / fm) + mu * (1.0 - sphi) : 0.0;
+        AR_STAMP(5);
+    } else {
+        cpr = __builtin_nan("");
+#pragma unroll
+        for (int k = 1; k <= P; k++) phi[k] = __builtin_nan("");
+    }
+    if (lane == 0) {
+        a.c[s] = cpr;
+#pragma unroll
+        for (int j = 0; j < P; j++) a.coef[s * P + j] = phi[1 + j];
+        if (a.err) a.err[s] = status;
+    }
+    if (!a.out) return;
+
+    // ---- fused removeTimeDependentEffects with the fitted model, in the reference's order
+    //      (S/models/Autoregression.scala:60-73): d = x_t - c; d -= x_{t-j-1} * coef_j ----
+    double* dst = a.out + s * a.ld_out;
+    const bool st16 = full && al && ((reinterpret_cast<uintptr_t>(dst) & 15) == 0);
+    double xw[P + 1];                          // xw[k] = x_{t-k}
+#pragma unroll
+    for (int k = 1; k <= P; k++) xw[k] = xp[k];
+    double rprev = 0.0;
+#pragma unroll
+    for (int j = 0; j < B; j++) {
+        const int t = t0 + j;
+        double d = x[j] - cpr;
+#pragma unroll
+        for (int k = 1; k <= P; k++)
+            if (t - k >= 0) d -= xw[k] * phi[k];
+#pragma unroll
+        for (int k = P; k >= 2; k--) xw[k] = xw[k - 1];
+        xw[1] = x[j];
+        if (st16) {
+            if (j & 1) *reinterpret_cast<double2*>(dst + t - 1) = make_double2(rprev, d);
+            rprev = d;
+        } else if (t < T) {
+            dst[t] = d;
+        }
+    }
+#ifdef STS_STAMPS
+    AR_STAMP(6);
+    if (lane == 0) {
+#pragma unroll
+        for (int i = 0; i < 7; i++) atomicAdd(&g_ar_stamps[i], st_acc[i]);
+        atomicAdd(&g_ar_stamps[15], 1ull);
+    }
+#endif
+}
+
 }  // namespace
+
+#ifdef STS_STAMPS
+extern "C" int sts_debug_ar_stamps(unsigned long long* out16) {
+    if (hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_ar_stamps), sizeof(unsigned long long) * 16) != hipSuccess) return 4;
+    unsigned long long z[16] = {0};
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_ar_stamps), z, sizeof(z)) == hipSuccess ? 0 : 4;
+}
+#endif
 
 hipError_t launch_ar_fit(const ArArgs& a, hipStream_t st) {
     if (a.S <= 0) return hipSuccess;
     if (a.p < 1 || a.p > kPMax) return hipErrorInvalidValue;
+    // register path: p <= 8, T <= 64 * 40 (lane blocks of B steps, B in {8, 16, 24, 32, 40})
+    if (a.p <= kRegPB && a.T <= 64 * 40 && !std::getenv("STS_AR_STAGED")) {
+        dim3 g((unsigned)((a.S + kRegWaves - 1) / kRegWaves)), b(64 * kRegWaves);
+        const int64_t need = (a.T + 63) / 64;
+        const int B = need <= 8 ? 8 : need <= 16 ? 16 : need <= 24 ? 24 : need <= 32 ? 32 : 40;
+#define STS_AR_BLK(PP)                                                                          \
+        case PP:                                                                                \
+            switch (B) {                                                                        \
+            case 8: hipLaunchKernelGGL((ar_fit_blk_kernel<PP, 8>), g, b, 0, st, a); break;      \
+            case 16: hipLaunchKernelGGL((ar_fit_blk_kernel<PP, 16>), g, b, 0, st, a); break;    \
+            case 24: hipLaunchKernelGGL((ar_fit_blk_kernel<PP, 24>), g, b, 0, st, a); break;    \
+            case 32: hipLaunchKernelGGL((ar_fit_blk_kernel<PP, 32>), g, b, 0, st, a); break;    \
+            default: hipLaunchKernelGGL((ar_fit_blk_kernel<PP, 40>), g, b, 0, st, a); break;    \
+            }                                                                                   \
+            break;
+        switch (a.p) {
+            STS_AR_BLK(1) STS_AR_BLK(2) STS_AR_BLK(3) STS_AR_BLK(4)
+            STS_AR_BLK(5) STS_AR_BLK(6) STS_AR_BLK(7) STS_AR_BLK(8)
+        default: return hipErrorInvalidValue;
+        }
+#undef STS_AR_BLK
+        return hipGetLastError();
+    }
     const int NT = (a.p + 15) / 16 + 1;
     const size_t fixed = (256 + 64 + (kPMax + 1) * kLd + (kPMax + 2) + (kPMax + 4) + 2 * (kPMax + 2)) * sizeof(double);
     dim3 grid((unsigned)a.S), block(64);

@@ -66,10 +66,12 @@ __device__ __forceinline__ bool isnan_d(double v) { return __builtin_isnan(v); }
 
 // Order LDS traffic between lanes of ONE wave: LDS instructions of a wave execute in
 // order, so only the compiler has to be kept from reordering across the hand-off.
+// (LDS-only fences: a fence on all address spaces would also emit s_waitcnt vmcnt(0) and
+// drain the register prefetch and the stores at every hand-off.)
 __device__ __forceinline__ void wave_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
     __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
 }
 
 __device__ __forceinline__ unsigned long long bitrep(unsigned x) {

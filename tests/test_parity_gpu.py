@@ -391,6 +391,41 @@ def test_ar_fit_panels(torch, p, no_intercept):
         assert_rel(host(m.c), rc, what="c")
 
 
+@pytest.mark.parametrize("p", [1, 3, 8])
+def test_ar_fit_register_path_shapes(torch, p):
+    # the register-resident kernel (p <= 8, T <= 2560): ragged last chunk, T at the chunk
+    # edges, both intercept modes, fused remove bit-exact given the fitted model
+    from sparkts.models import Autoregression
+    for T in (2 * p + 1, 64, 65, 127, 1000, 2559, 2560):
+        x = oracle.gen_ar_panel(7, 6, T, min(p, 5)) + 0.01 * np.sin(np.arange(T))[None, :]
+        for no_int in (False, True):
+            m = Autoregression.fitModel(dev(torch, x), p, no_int)
+            rc = np.empty(6); rcoef = np.empty((6, p))
+            for s in range(6):
+                rc[s], rcoef[s] = oracle.ar_fit(x[s], p, no_int)
+            assert_rel(host(m.coefficients), rcoef, what="coef T=%d p=%d" % (T, p))
+            if not no_int:
+                assert_rel(host(m.c), rc, what="c T=%d p=%d" % (T, p))
+        m, resid = Autoregression.fitModelAndRemove(dev(torch, x), p)
+        c, coef = host(m.c), host(m.coefficients)
+        assert_bits(host(resid), np.array([oracle.ar_remove(x[s], c[s], coef[s]) for s in range(6)]),
+                    "fused remove T=%d p=%d" % (T, p))
+
+
+def test_ar_fit_register_path_matches_staged_on_nan(torch, monkeypatch):
+    # NaN anywhere -> NaN model, same as the LDS-staged kernel
+    from sparkts.models import Autoregression
+    x = oracle.gen_ar_panel(8, 4, 2520, 5)
+    x[1, 700] = NaN
+    got = Autoregression.fitModel(dev(torch, x), 5)
+    monkeypatch.setenv("STS_AR_STAGED", "1")
+    ref = Autoregression.fitModel(dev(torch, x), 5)
+    assert np.isnan(host(got.c)[1]) and np.isnan(host(ref.c)[1])
+    assert np.array_equal(np.isnan(host(got.coefficients)), np.isnan(host(ref.coefficients)))
+    ok = [0, 2, 3]
+    assert_rel(host(got.coefficients)[ok], host(ref.coefficients)[ok])
+
+
 def test_ar_fit_long_series_unstaged(torch):
     from sparkts.models import Autoregression
     x = oracle.gen_ar_panel(9, 4, 10000, 5)
