@@ -7,11 +7,14 @@
 //   differencesAtLag                      S/UnivariateTimeSeries.scala:356-376 (dest eq ts)
 //   C2 pipeline fillPrevious -> differencesAtLag(lag) -> EWMA add, fused (one HBM pass)
 //
-// A wave owns 64 series.  Time is processed in chunks of kCH steps: the wave loads a
-// 64 x kCH block through LDS (each load instruction covers 2 series x 256 contiguous
-// bytes, so HBM sees whole lines), transposes it (row stride kCH+1 doubles: the
-// per-lane row reads hit 64 distinct banks), runs each lane's recurrence over the
-// chunk in registers, and stores the block back the same way.
+// A wave owns SPW series (64 by default; 32 for the fused C2 pipeline).  Time is processed
+// in chunks of CH steps: the wave loads an SPW x CH block through LDS (each load
+// instruction covers 64 consecutive steps of one series, 512 contiguous bytes; the next
+// chunk's loads are in flight while the current chunk runs), transposes it (row stride
+// CH+1 doubles: the per-lane row reads hit distinct banks), runs each lane's recurrence
+// over the chunk in registers, and stores the block back the same way.  Measured on the C2
+// shape (1M series x 390 steps): 64-step row segments beat 32 (1.68 vs 1.98 ms) and 128
+// (2.86 ms); the series count per wave (16 / 32 / 64) hardly matters.
 #include "sts_internal.hpp"
 
 #include <hip/hip_runtime.h>
@@ -19,17 +22,22 @@
 namespace sts {
 namespace {
 
-constexpr int kCH = 32;
-constexpr int kRow = kCH + 1;
-
-template <int OP, int H>
+// SPW series per wave, CH steps per chunk: the chunk's SPW x CH block moves through LDS
+// with every load / store instruction covering 64 consecutive steps of ONE series (512
+// contiguous bytes); lanes < SPW then run their series' recurrence over the chunk.
+// Longer row segments (fewer series, longer chunks) keep HBM pages open: C2's 1M series
+// x 390 steps are only 3 KB each.
+template <int OP, int H, int SPW = 64, int CH = 32>
 __global__ __launch_bounds__(64) void recur_kernel(RecurArgs a) {
-    __shared__ double tile[64 * kRow];
+    constexpr int kRow = CH + 1;
+    constexpr int NLD = SPW * CH / 64;            // load instructions per chunk per lane
+    static_assert(SPW * CH % 64 == 0 && (CH % 64 == 0 || 64 % CH == 0), "chunk shape");
+    __shared__ double tile[SPW * kRow];
     const int lane = threadIdx.x;
-    const int64_t s0 = (int64_t)blockIdx.x * 64;
-    const int64_t sl = s0 + lane;                 // this lane's series
-    const bool live = sl < a.S;
-    const int ns = (a.S - s0 < 64) ? (int)(a.S - s0) : 64;
+    const int64_t s0 = (int64_t)blockIdx.x * SPW;
+    const int64_t sl = s0 + lane;                 // this lane's series (lanes < SPW)
+    const bool live = lane < SPW && sl < a.S;
+    const int ns = (a.S - s0 < SPW) ? (int)(a.S - s0) : SPW;
     const int64_t T = a.T;
 
     // per-series parameters
@@ -56,26 +64,25 @@ __global__ __launch_bounds__(64) void recur_kernel(RecurArgs a) {
     double e = 0.0;                                // EWMA state
     double carry = __builtin_nan("");              // fillPrevious carry
 
-    // blocks move through LDS: all 32 row segments of a block are loaded before any is
-    // stored (lanes 0-31 take row 2i, lanes 32-63 row 2i+1: whole 256-B row segments)
-    const int col = lane & 31;
-    for (int64_t tc = 0; tc < T; tc += kCH) {
-        const int len = (T - tc < kCH) ? (int)(T - tc) : kCH;
-        const double* base = a.in + (s0 + (lane >> 5)) * a.ld_in + tc + col;
+    // load instruction i of a chunk: row (i * 64 + lane) / CH, column (i * 64 + lane) % CH
+    double pre[NLD];
+    auto fetch = [&](int64_t tc) {
+        const int len = (T - tc < CH) ? (int)(T - tc) : CH;
 #pragma unroll
-        for (int h = 0; h < 2; h++) {      // two batches of 16 loads in flight
-            double pre[16];
-#pragma unroll
-            for (int i = 0; i < 16; i++) {
-                const int row = 2 * (16 * h + i) + (lane >> 5);
-                pre[i] = (row < ns && col < len) ? base[(int64_t)(2 * (16 * h + i)) * a.ld_in] : 0.0;
-            }
-#pragma unroll
-            for (int i = 0; i < 16; i++) {
-                const int row = 2 * (16 * h + i) + (lane >> 5);
-                if (row < ns && col < len) tile[row * kRow + col] = pre[i];
-            }
+        for (int i = 0; i < NLD; i++) {
+            const int row = (i * 64 + lane) / CH, col = (i * 64 + lane) % CH;
+            pre[i] = (row < ns && col < len) ? a.in[(s0 + row) * a.ld_in + tc + col] : 0.0;
         }
+    };
+    fetch(0);
+    for (int64_t tc = 0; tc < T; tc += CH) {
+        const int len = (T - tc < CH) ? (int)(T - tc) : CH;
+#pragma unroll
+        for (int i = 0; i < NLD; i++) {
+            const int row = (i * 64 + lane) / CH, col = (i * 64 + lane) % CH;
+            if (row < ns && col < len) tile[row * kRow + col] = pre[i];
+        }
+        if (tc + CH < T) fetch(tc + CH);   // next chunk in flight during this one
         __syncthreads();
         if (live) {
             double* myrow = tile + lane * kRow;
@@ -130,13 +137,10 @@ __global__ __launch_bounds__(64) void recur_kernel(RecurArgs a) {
             }
         }
         __syncthreads();
-        {
-            double* obase = a.out + (s0 + (lane >> 5)) * a.ld_out + tc + col;
-#pragma unroll 8
-            for (int i = 0; i < 32; i++) {
-                const int row = 2 * i + (lane >> 5);
-                if (row < ns && col < len) obase[(int64_t)(2 * i) * a.ld_out] = tile[row * kRow + col];
-            }
+#pragma unroll
+        for (int i = 0; i < NLD; i++) {
+            const int row = (i * 64 + lane) / CH, col = (i * 64 + lane) % CH;
+            if (row < ns && col < len) a.out[(s0 + row) * a.ld_out + tc + col] = tile[row * kRow + col];
         }
         __syncthreads();
     }
@@ -205,7 +209,20 @@ hipError_t launch_recur(RecurOp op, const RecurArgs& a, hipStream_t st) {
     case kArAdd: return launch_h<kArAdd>(a, a.p, st);
     case kArRemoveInplace: return launch_h<kArRemoveInplace>(a, a.p, st);
     case kDiffInplace: return launch_h<kDiffInplace>(a, a.lag, st);
-    case kFillDiffEwma: return launch_h<kFillDiffEwma>(a, a.lag, st);
+    case kFillDiffEwma:
+#ifndef STS_FDE_SPW
+#define STS_FDE_SPW 32
+#define STS_FDE_CH 64
+#endif
+        if (a.lag <= 8) {   // C2 shape: 32 series x 64-step chunks per wave (A/B: r01 notes)
+            dim3 g((unsigned)((a.S + STS_FDE_SPW - 1) / STS_FDE_SPW)), b(64);
+            if (a.lag <= 1) hipLaunchKernelGGL((recur_kernel<kFillDiffEwma, 1, STS_FDE_SPW, STS_FDE_CH>), g, b, 0, st, a);
+            else if (a.lag <= 2) hipLaunchKernelGGL((recur_kernel<kFillDiffEwma, 2, STS_FDE_SPW, STS_FDE_CH>), g, b, 0, st, a);
+            else if (a.lag <= 4) hipLaunchKernelGGL((recur_kernel<kFillDiffEwma, 4, STS_FDE_SPW, STS_FDE_CH>), g, b, 0, st, a);
+            else hipLaunchKernelGGL((recur_kernel<kFillDiffEwma, 8, STS_FDE_SPW, STS_FDE_CH>), g, b, 0, st, a);
+            return hipGetLastError();
+        }
+        return launch_h<kFillDiffEwma>(a, a.lag, st);
     }
     return hipErrorInvalidValue;
 }

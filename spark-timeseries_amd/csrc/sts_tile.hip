@@ -35,8 +35,25 @@
 #define STS_MFMA_PIPE 0   // experiment knob: software-pipelined MFMA operand loads
 #endif
 
+#ifndef STS_LDS_BARRIER
+#define STS_LDS_BARRIER 1
+#endif
+
 namespace sts {
 namespace {
+
+// Workgroup barrier ordering LDS only.  The tile kernel never reads global data another
+// thread of the kernel wrote, so global loads (the register prefetch) and stores need no
+// ordering here -- and a fence on all address spaces would pin them in program order.
+__device__ __forceinline__ void lds_barrier() {
+#if STS_LDS_BARRIER
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+#else
+    __syncthreads();
+#endif
+}
 
 typedef double d4 __attribute__((ext_vector_type(4)));
 
@@ -176,9 +193,9 @@ __global__ __launch_bounds__(kThreads, 3) void tile_kernel(TileArgs a, int metho
             }
             if (lane == 0) sh_d[0] = x0;
         }
-        __syncthreads();
+        lds_barrier();
         c0 = sh_d[0];
-        __syncthreads();
+        lds_barrier();
     }
 
     // register prefetch of one INTERIOR extended tile [e0, e0 + EW); the first and last tile
@@ -259,7 +276,7 @@ __global__ __launch_bounds__(kThreads, 3) void tile_kernel(TileArgs a, int metho
         }
         const bool have_next = (k + 1 < k_end) && interior(k + 1);
         STAMP(0);
-        __syncthreads();
+        lds_barrier();
         STAMP(1);
 
         // positions to produce: [qA, qB) (E-relative); the ACF needs REACH steps past the tile
@@ -279,7 +296,7 @@ __global__ __launch_bounds__(kThreads, 3) void tile_kernel(TileArgs a, int metho
                 }
             }
             STAMP(2);
-            __syncthreads();
+            lds_barrier();
         }
         STAMP(3);
 
@@ -352,7 +369,7 @@ __global__ __launch_bounds__(kThreads, 3) void tile_kernel(TileArgs a, int metho
             }
         }
         STAMP(4);
-        __syncthreads();
+        lds_barrier();
         STAMP(5);
 
         // ---- 4. impute the compacted NaN positions, all lanes busy; F goes back into
@@ -425,7 +442,7 @@ __global__ __launch_bounds__(kThreads, 3) void tile_kernel(TileArgs a, int metho
             }
         }
         STAMP(6);
-        __syncthreads();
+        lds_barrier();
         STAMP(7);
 
         // ---- 5. filled output + lag matrix (16-B stores), then y = F - F(0) in place
@@ -510,7 +527,7 @@ __global__ __launch_bounds__(kThreads, 3) void tile_kernel(TileArgs a, int metho
         STAMP(8);
 
         if constexpr (NT > 0) {
-            __syncthreads();
+            lds_barrier();
             STAMP(9);
             // ---- 6. lag products on MFMA ----
             constexpr int CPW = TW / 64 / kWaves;   // 64-step chunks per wave
@@ -596,7 +613,7 @@ __global__ __launch_bounds__(kThreads, 3) void tile_kernel(TileArgs a, int metho
         }
         have = have_next;
         STAMP(10);
-        __syncthreads();   // vals / mask / lists are reused by the next tile
+        lds_barrier();   // vals / mask / lists are reused by the next tile
         STAMP(11);
     }
 #undef STS_ISSUE
@@ -622,23 +639,23 @@ __global__ __launch_bounds__(kThreads, 3) void tile_kernel(TileArgs a, int metho
             for (int t = 1; t < NA; t++) D += U[t];
 #pragma unroll
             for (int r = 0; r < 4; r++) scr[((lane >> 4) + 4 * r) * 16 + (lane & 15)] = D[r];
-            __syncthreads();
+            lds_barrier();
 #pragma unroll
             for (int j = 0; j < 16; j++) {
                 const int i = 16 * (j / QS) + (16 - QS) + (j % QS) - lane;   // entry (i, j) holds lag h(j) - i
                 if (i >= 0 && i < 16) lagacc += scr[i * 16 + j];
             }
-            __syncthreads();
+            lds_barrier();
         } else {
 #pragma unroll
             for (int t = 0; t < NT; t++) {
 #pragma unroll
                 for (int r = 0; r < 4; r++) scr[((lane >> 4) + 4 * r) * 16 + (lane & 15)] = U[t][r];
-                __syncthreads();
+                lds_barrier();
 #pragma unroll
                 for (int b = 0; b < 16; b++)
                     if (((b + lane) >> 4) == t) lagacc += scr[b * 16 + ((b + lane) & 15)];
-                __syncthreads();
+                lds_barrier();
             }
         }
 #pragma unroll
@@ -646,7 +663,7 @@ __global__ __launch_bounds__(kThreads, 3) void tile_kernel(TileArgs a, int metho
         double* wsum = vals + kWaves * 256;
         wsum[wave * kPartStride + lane] = lagacc;
         if (lane == 0) wsum[wave * kPartStride + 64] = sy;
-        __syncthreads();
+        lds_barrier();
         if (wave == 0) {
             double* part = a.partials + ch * kPartStride;
             double tot = 0.0;
