@@ -161,7 +161,7 @@ def main():
     if args.workload == "c5":            # + the lag matrix: 8 * P bytes per row, (T - P) rows per series
         bytes_per_step += 8.0 * P * (T - P) * S
     kernel = {"c3": "sts::tile_kernel<4096,4,shifted> (fill linear + ACF partials, FP64 MFMA)",
-              "c1": "sts::tile_kernel<4096,2,shifted> (fill linear + ACF partials, FP64 MFMA)",
+              "c1": "sts::seg_kernel<2> (wave-private series segments: fill linear + ACF partials, FP64 MFMA)",
               "c5": "sts::tile_kernel<4096,0> (fill nearest + lag-matrix columns)",
               "c2": "sts::recur_kernel<kFillDiffEwma> (fillPrevious -> differencesAtLag(1) -> EWMA add, lane per series)",
               "c4": "sts::ar_fit_kernel (AR(5) Gram on FP64 MFMA + solve + fused remove)"}[args.workload]

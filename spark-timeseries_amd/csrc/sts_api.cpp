@@ -169,12 +169,17 @@ hipError_t timed(hipStream_t st, F&& launch) {
 int run_tile(const double* in, double* out, double* lagmat, int64_t S, int64_t T, int64_t ld_in, int64_t ld_out,
              int method, int K, double* acf, int max_lag, int inc, int32_t* err, hipStream_t st, const char* name) {
     if (S == 0 || T == 0) return STS_OK;
-    // the workgroup tile kernel serves every call; the wave-private segment kernel is an
-    // opt-in alternative (STS_TILE_KERNEL=seg: aligned panels, no lag matrix, K <= 60)
+    // short series (T <= 16384: C1, the 10-year daily panels) go to the wave-private
+    // segment kernel (2x faster there: one wave per series, no barriers), long ones to the
+    // workgroup tile kernel (faster from T = 32768: C3, C5).  The segment kernel needs a
+    // 16-B aligned panel, no lag matrix and K <= 60.  STS_TILE_KERNEL=tile|seg forces one
+    // (A/B runs, tools/kbench.py).
     const char* force = std::getenv("STS_TILE_KERNEL");
-    const bool seg = force && !std::strcmp(force, "seg") && !lagmat && sts::seg_nt(K) >= 0 &&
-                     (reinterpret_cast<uintptr_t>(in) & 15) == 0 && (ld_in % 2) == 0 &&
-                     (!out || ((reinterpret_cast<uintptr_t>(out) & 15) == 0 && ld_out % 2 == 0)) && T < 0x7fff0000LL;
+    const bool seg_ok = !lagmat && sts::seg_nt(K) >= 0 && (reinterpret_cast<uintptr_t>(in) & 15) == 0 &&
+                        (ld_in % 2) == 0 &&
+                        (!out || ((reinterpret_cast<uintptr_t>(out) & 15) == 0 && ld_out % 2 == 0)) &&
+                        T < 0x7fff0000LL;
+    const bool seg = seg_ok && (force ? !std::strcmp(force, "seg") : T <= 16384);
     const int tw = seg ? sts::kSegW : (K > 0) ? 4096 : tile_width(T);
     sts::TileArgs a{};
     a.in = in;

@@ -234,6 +234,31 @@ def test_fill_autocorr_fused(torch, method):
         assert_rel(host(acf), racf, what=method)
 
 
+@pytest.mark.parametrize("kernel", ["tile", "seg"])
+@pytest.mark.parametrize("method", ["linear", "previous", "next", "nearest"])
+def test_fill_autocorr_both_kernels(torch, monkeypatch, kernel, method):
+    # both imputation kernels, whatever the length-based dispatch picks: the workgroup
+    # tile kernel and the wave-private segment kernel (STS_TILE_KERNEL forces one)
+    from sparkts import TimeSeriesRDD
+    from sparkts import UnivariateTimeSeries as uts
+    monkeypatch.setenv("STS_TILE_KERNEL", kernel)
+    rng = np.random.default_rng(zlib.crc32(("both%s%s" % (kernel, method)).encode()))
+    for S, T, K in [(7, 600, 20), (5, 2520, 60), (3, 16384 + 77, 24), (2, 70000, 60), (2, 513, 0)]:
+        x = random_panel(rng, S, T, 0.07, runs=True)
+        if method == "nearest":
+            x[:, 1] = 100.0
+        if K > 0:
+            filled, acf = TimeSeriesRDD(None, None, dev(torch, x)).fillAndAutocorr(method, K)
+            rf, racf, err = oracle.panel_fill_autocorr(x, method, K)
+            assert (err == 0).all()
+            assert_bits(host(filled.data), rf, "%s %s T=%d" % (kernel, method, T))
+            assert_rel(host(acf), racf, what="%s %s T=%d K=%d" % (kernel, method, T, K))
+        else:
+            got = host(uts.fillts(dev(torch, x), method))
+            ref, _ = oracle.panel_fill(x, method)
+            assert_bits(got, ref, "%s %s T=%d" % (kernel, method, T))
+
+
 def test_fill_autocorr_c3_length(torch):
     # C3 series length (982,800 minute bars), a few series: fused fill("linear") + ACF(60)
     S, T, K = 3, 982_800, 60

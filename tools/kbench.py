@@ -45,10 +45,7 @@ def main():
         kern, meth, K = case.split(":")
         K = int(K)
         code = METHODS[meth]
-        if kern == "tile":
-            os.environ["STS_TILE_KERNEL"] = "tile"
-        else:
-            os.environ.pop("STS_TILE_KERNEL", None)
+        os.environ["STS_TILE_KERNEL"] = kern     # "tile" (default path) or "seg" (opt-in)
         filled = out.data_ptr() if code >= 0 else None
 
         def call():
