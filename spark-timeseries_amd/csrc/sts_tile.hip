@@ -35,6 +35,10 @@
 #define STS_MFMA_PIPE 0   // experiment knob: software-pipelined MFMA operand loads
 #endif
 
+#ifndef STS_MFMA_UNROLL
+#define STS_MFMA_UNROLL 1 // fully unrolled full-range MFMA phase (A/B: ~1.5 % faster)
+#endif
+
 #ifndef STS_LDS_BARRIER
 #define STS_LDS_BARRIER 1
 #endif
@@ -565,6 +569,37 @@ __global__ __launch_bounds__(kThreads, 3) void tile_kernel(TileArgs a, int metho
                 // wave 0 of the first tile also runs chunk -1 (the look-back, y = 0), whose
                 // shifted windows hold the series' first QS t steps
                 if (k == 0 && wave == 0) chunk_mfma(vals);
+#if STS_MFMA_UNROLL
+                if (cend - c == CPW) {
+                    // full chunk range, unrolled: per-lane LDS indices made opaque once per
+                    // tile (else LICM hoists all 16 x 2NT of them out of the tile loop and
+                    // spills), chunk offsets (72 doubles per padded chunk) fold into the
+                    // ds_read immediates
+                    int ia[NT], ib[NT];
+                    const int cb = px(qA + 64 * c);
+#pragma unroll
+                    for (int t = 0; t < NT; t++) {
+                        ia[t] = cb + oa[t];
+                        ib[t] = cb + ob[t];
+                        asm volatile("" : "+v"(ia[t]), "+v"(ib[t]));
+                    }
+#pragma unroll
+                    for (int cc = 0; cc < CPW; cc++) {
+                        double av[NT], bv[NT];
+#pragma unroll
+                        for (int t = 0; t < NT; t++) {
+                            av[t] = vals[ia[t] + 72 * cc];
+                            bv[t] = vals[ib[t] + 72 * cc];
+                        }
+#pragma unroll
+                        for (int t = 0; t < NT; t++)
+                            U[t % NA] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[t], bv[t], U[t % NA], 0, 0, 0);
+                        sy += av[0];
+                        __builtin_amdgcn_sched_barrier(0);   // one chunk's operands live at a time
+                    }
+                    c = cend;
+                }
+#endif
 #if STS_MFMA_PIPE
                 // software pipeline: chunk c + 1's operands load while chunk c's MFMAs run
                 if (c < cend) {
