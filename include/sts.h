@@ -60,7 +60,9 @@ typedef enum sts_status {
     STS_ERR_NOT_ENOUGH_DATA = 7,    /* commons-math3 MathIllegalArgumentException
                                        NOT_ENOUGH_DATA_FOR_NUMBER_OF_PREDICTORS              */
     STS_ERR_SINGULAR = 8,           /* commons-math3 SingularMatrixException                 */
-    STS_ERR_NO_DEVICE = 9           /* no gfx950 device visible                              */
+    STS_ERR_NO_DEVICE = 9,          /* no gfx950 device visible                              */
+    STS_ERR_TOO_MANY_EVALUATIONS = 10, /* commons-math3 TooManyEvaluationsException (EWMA fit) */
+    STS_ERR_TOO_MANY_ITERATIONS = 11   /* commons-math3 TooManyIterationsException (EWMA fit)  */
 } sts_status;
 
 /* Fill methods of UnivariateTimeSeries.fillts (S/UnivariateTimeSeries.scala:141-150). */
@@ -129,6 +131,20 @@ int sts_ewma_add(const double* in, double* out, int64_t S, int64_t T, int64_t ld
 int sts_ewma_remove(const double* in, double* out, int64_t S, int64_t T, int64_t ld_in,
                     int64_t ld_out, const double* smoothing, void* stream);
 
+/* ---- f1: EWMA.fitModel(ts) (S/models/EWMA.scala:44-68), every series of a panel in one
+ * call.  smoothing[s] receives the fitted parameter.  The optimizer is commons-math3 3.4.1's
+ * NonLinearConjugateGradientOptimizer (Fletcher-Reeves, SimpleValueChecker(1e-6, 1e-6), line
+ * search = BracketFinder + BrentOptimizer, start 0.94, MaxIter / MaxEval 10000), run per
+ * series on the device; every sse / gradient evaluation is the reference's sequential loop
+ * (bit-exact), so the fit follows the reference's optimizer path.  A series the optimizer
+ * cannot fit (any NaN: every sse is NaN) gets NaN and STS_ERR_TOO_MANY_EVALUATIONS. */
+int sts_ewma_fit(const double* in, int64_t S, int64_t T, int64_t ld, double* smoothing,
+                 int32_t* err_per_series, void* stream);
+/* EWMAModel(smoothing[s]).sse(ts) (:80-95) and .gradient(ts) (:102-123) per series, one
+ * pass; sse or gradient may be NULL.  Bit-exact. */
+int sts_ewma_sse_gradient(const double* in, int64_t S, int64_t T, int64_t ld,
+                          const double* smoothing, double* sse, double* gradient, void* stream);
+
 /* ---- a11: Autoregression.fitModel(ts, p, noIntercept) (S/models/Autoregression.scala:38-53).
  * c[s] and coef[s*p + j] receive the model; 1 <= p <= 31.  T - p < p + 1 ->
  * STS_ERR_NOT_ENOUGH_DATA.  1e-10 relative to a Householder-QR OLS. */
@@ -183,6 +199,8 @@ int sts_ewma_add_host(const double* in, double* out, int64_t S, int64_t T, int64
                       const double* smoothing);
 int sts_ewma_remove_host(const double* in, double* out, int64_t S, int64_t T, int64_t ld,
                          const double* smoothing);
+int sts_ewma_fit_host(const double* in, int64_t S, int64_t T, int64_t ld, double* smoothing,
+                      int32_t* err_per_series);
 int sts_ar_fit_host(const double* in, int64_t S, int64_t T, int64_t ld, int p, int no_intercept,
                     double* c, double* coef, int32_t* err_per_series);
 int sts_ar_remove_host(const double* in, double* out, int64_t S, int64_t T, int64_t ld,

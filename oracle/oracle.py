@@ -21,6 +21,7 @@ LIB_PATH = os.path.join(HERE, "_build", "libsts_oracle.so")
 
 OK, ERR_BAD_ARG, ERR_ALL_NAN, ERR_UNSUPPORTED_METHOD = 0, 1, 2, 3
 ERR_REQUIREMENT, ERR_NOT_ENOUGH_DATA, ERR_SINGULAR = 5, 7, 8
+ERR_TOO_MANY_EVALUATIONS, ERR_TOO_MANY_ITERATIONS = 10, 11
 FILL_METHODS = {"linear": 0, "nearest": 1, "next": 2, "previous": 3}
 
 _lib = None
@@ -59,6 +60,10 @@ def lib():
             "orc_panel_fill_autocorr": (ctypes.c_int, [_dp, _dp, _i64, _i64, _i64, ctypes.c_int, ctypes.c_int, _dp, i32p, ctypes.c_int]),
             "orc_panel_fill_diff_ewma": (ctypes.c_int, [_dp, _dp, _i64, _i64, _i64, ctypes.c_double, ctypes.c_int]),
             "orc_panel_ar_fit_remove": (ctypes.c_int, [_dp, _dp, _i64, _i64, _i64, ctypes.c_int, ctypes.c_int, _dp, _dp, ctypes.c_int]),
+            "orc_ewma_sse": (ctypes.c_double, [_dp, _i64, ctypes.c_double]),
+            "orc_ewma_gradient": (ctypes.c_double, [_dp, _i64, ctypes.c_double]),
+            "orc_ewma_fit": (ctypes.c_int, [_dp, _i64, _dp, ctypes.POINTER(ctypes.c_int64)]),
+            "orc_panel_ewma_fit": (ctypes.c_int, [_dp, _i64, _i64, _i64, _dp, i32p, ctypes.c_int]),
             "orc_gen_value": (ctypes.c_double, [ctypes.c_uint64, _i64, _i64, _i64]),
             "orc_nan_threshold": (ctypes.c_uint32, [ctypes.c_double]),
             "orc_gen_panel": (None, [ctypes.c_uint64, _i64, _i64, _i64, _i64, ctypes.c_double, _dp]),
@@ -188,6 +193,21 @@ def ar_fit(ts, p: int, no_intercept: bool = False):
     return float(c[0]), coef
 
 
+def ewma_sse(ts, s: float) -> float:
+    ts = _vec(ts); return lib().orc_ewma_sse(_p(ts), ts.size, s)
+
+
+def ewma_gradient(ts, s: float) -> float:
+    ts = _vec(ts); return lib().orc_ewma_gradient(_p(ts), ts.size, s)
+
+
+def ewma_fit(ts):
+    """EWMA.fitModel (S/models/EWMA.scala:44-68) -> (status, smoothing, evaluations)."""
+    ts = _vec(ts); sm = np.zeros(1); ev = ctypes.c_int64(0)
+    st = lib().orc_ewma_fit(_p(ts), ts.size, _p(sm), ctypes.byref(ev))
+    return st, float(sm[0]), int(ev.value)
+
+
 # ---------------- panel drivers ----------------
 
 def _panel(x):
@@ -221,6 +241,12 @@ def panel_ar_fit_remove(x, p: int, no_intercept=False, threads: int = 1):
     x = _panel(x); S, T = x.shape; out = np.empty_like(x); c = np.empty(S); coef = np.empty((S, p))
     lib().orc_panel_ar_fit_remove(_p(x), _p(out), S, T, T, p, int(no_intercept), _p(c), _p(coef), threads)
     return out, c, coef
+
+
+def panel_ewma_fit(x, threads: int = 1):
+    x = _panel(x); S, T = x.shape; sm = np.empty(S); err = np.zeros(S, np.int32)
+    lib().orc_panel_ewma_fit(_p(x), S, T, T, _p(sm), err.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), threads)
+    return sm, err
 
 
 # ---------------- generator ----------------

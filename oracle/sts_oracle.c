@@ -312,6 +312,257 @@ int orc_ar_fit(const double* ts, int64_t n, int p, int no_intercept, double* c, 
     return ORC_OK;
 }
 
+/* ---------------- EWMA.fitModel (S/models/EWMA.scala:44-68) ----------------
+ *
+ * EWMAModel.sse (:80-95) and .gradient (:102-123) restated statement by statement.
+ * The optimizer is commons-math3 3.4.1 (pom.xml:396-400; not vendored in /root/reference),
+ * restated from its published algorithm:
+ *   NonLinearConjugateGradientOptimizer(FLETCHER_REEVES, SimpleValueChecker(1e-6, 1e-6))
+ *     -> LineSearch(relTol 1e-8, absTol 1e-8, initialBracketingRange 1e-8)
+ *        = BracketFinder(growLimit 100, maxEvaluations 500).search(f, MIN, 0, 1e-8)
+ *          + BrentOptimizer(rel 1e-15, abs Double.MIN_VALUE,
+ *                           SimpleUnivariateValueChecker(1e-8, 1e-8))
+ *   InitialGuess 0.94, MaxIter 10000, MaxEval 10000 (:60-62).
+ * One parameter (n = 1): iterations % n == 0 always resets the search direction to the
+ * steepest descent, so beta never matters.  Parity is pinned only by
+ * T/models/EWMASuite.scala:54-63 (the oil series -> truncated smoothing 89).
+ */
+double orc_ewma_sse(const double* ts, int64_t n, double s) {
+    /* smoothed = addTimeDependentEffects(ts, zeros) (:82-84), then :86-92 */
+    double sm = (n > 0) ? ts[0] : 0.0, sq = 0.0;
+    for (int64_t i = 0; i < n - 1; i++) {
+        const double error = ts[i + 1] - sm;     /* ts(i + 1) - smoothed(i) */
+        sq += error * error;
+        sm = s * ts[i + 1] + (1 - s) * sm;       /* smoothed(i + 1), EWMA.scala:140 */
+    }
+    return sq;
+}
+
+double orc_ewma_gradient(const double* ts, int64_t n, double s) {
+    double sm = (n > 0) ? ts[0] : 0.0;           /* smoothed(i) */
+    double prevSmoothed = (n > 0) ? ts[0] : 0.0, prevDSda = 0.0, dSda = 0.0, dJda = 0.0;
+    for (int64_t i = 0; i < n - 1; i++) {
+        const double error = ts[i + 1] - sm;
+        dSda = ts[i] - prevSmoothed + (1 - s) * prevDSda;
+        dJda += error * dSda;
+        prevDSda = dSda;
+        prevSmoothed = sm;
+        sm = s * ts[i + 1] + (1 - s) * sm;
+    }
+    return 2 * dJda;
+}
+
+typedef struct { double x, v; } pv_t;   /* (Univariate)PointValuePair */
+
+/* commons-math3 Precision.equals(x, y) = equals(x, y, 1 ulp), NaN never equal */
+static int cm_precision_equals(double x, double y) {
+    int64_t xi, yi;
+    memcpy(&xi, &x, 8);
+    memcpy(&yi, &y, 8);
+    int eq;
+    if (((xi ^ yi) & INT64_MIN) == 0) {
+        int64_t d = xi - yi;
+        eq = (d < 0 ? -d : d) <= 1;
+    } else {
+        int64_t dp, dm;
+        if (xi < yi) { dp = yi; dm = (int64_t)((uint64_t)xi - (uint64_t)INT64_MIN); }
+        else { dp = xi; dm = (int64_t)((uint64_t)yi - (uint64_t)INT64_MIN); }
+        eq = (dp > 1) ? 0 : (dm <= 1 - dp);
+    }
+    return eq && !isnan(x) && !isnan(y);
+}
+
+/* objective with the main optimizer's evaluation counter (MaxEval 10000) */
+typedef struct { const double* ts; int64_t n; int64_t evals; int too_many; } ewma_obj_t;
+static double ewma_value(ewma_obj_t* o, double s) {
+    if (++o->evals > 10000) o->too_many = 1;
+    return o->too_many ? NAN : orc_ewma_sse(o->ts, o->n, s);
+}
+
+#define CM_GOLD 1.618034
+#define CM_EPS_MIN 1e-21
+
+/* LineSearch.search (n = 1): f(alpha) = value(point + alpha * dir) */
+static double cm_line_search(ewma_obj_t* o, double point, double dir, int* err) {
+    /* BracketFinder.search(f, MINIMIZE, 0, 1e-8); its own counter: 500 evaluations */
+    int bev = 0;
+#define F(a) (++bev > 500 ? (*err = 1, NAN) : ewma_value(o, point + (a) * dir))
+    double xA = 0, xB = 1e-8;
+    double fA = F(xA), fB = F(xB);
+    if (*err || o->too_many) return NAN;
+    if (fA < fB) {
+        double t = xA; xA = xB; xB = t;
+        t = fA; fA = fB; fB = t;
+    }
+    double xC = xB + CM_GOLD * (xB - xA);
+    double fC = F(xC);
+    while (fC < fB) {
+        if (*err || o->too_many) return NAN;
+        double tmp1 = (xB - xA) * (fB - fC);
+        double tmp2 = (xB - xC) * (fB - fA);
+        double val = tmp2 - tmp1;
+        double denom = fabs(val) < CM_EPS_MIN ? 2 * CM_EPS_MIN : val;
+        double w = xB - ((xB - xC) * tmp2 - (xB - xA) * tmp1) / (2 * denom);
+        double wLim = xB + 100 * (xC - xB);
+        double fW;
+        if ((w - xC) * (xB - w) > 0) {
+            fW = F(w);
+            if (fW < fC) {
+                xA = xB; xB = w; fA = fB; fB = fW;
+                break;
+            } else if (fW > fB) {
+                xC = w; fC = fW;
+                break;
+            }
+            w = xC + CM_GOLD * (xC - xB);
+            fW = F(w);
+        } else if ((w - wLim) * (wLim - xC) >= 0) {
+            w = wLim;
+            fW = F(w);
+        } else if ((w - wLim) * (xC - w) > 0) {
+            fW = F(w);
+            if (fW < fC) {
+                xB = xC; xC = w; w = xC + CM_GOLD * (xC - xB);
+                fB = fC; fC = fW;
+                fW = F(w);
+            }
+        } else {
+            w = xC + CM_GOLD * (xC - xB);
+            fW = F(w);
+        }
+        xA = xB; fA = fB; xB = xC; fB = fC; xC = w; fC = fW;
+    }
+#undef F
+    if (*err || o->too_many) return NAN;
+    double lo = xA, mid = xB, hi = xC;
+    if (lo > hi) { double t = lo; lo = hi; hi = t; }
+    if (!(lo < hi) || !(mid >= lo && mid <= hi)) { *err = 2; return NAN; }  /* SearchInterval */
+
+    /* BrentOptimizer.doOptimize, MINIMIZE, start = mid */
+    const double rel = 1e-15, absT = 4.9e-324;
+    const double GS = 0.5 * (3 - sqrt(5.0));
+    double a = lo, b = hi;
+    double x = mid, v = x, w = x, d = 0, e = 0;
+    double fx = ewma_value(o, x);
+    double fv = fx, fw = fx;
+    pv_t previous = {0, 0}, current = {x, fx}, best = current;
+    int have_prev = 0;
+    for (;;) {
+        if (o->too_many) return NAN;
+        const double m = 0.5 * (a + b);
+        const double tol1 = rel * fabs(x) + absT;
+        const double tol2 = 2 * tol1;
+        const int stop = fabs(x - m) <= tol2 - 0.5 * (b - a);
+        if (stop) {
+            /* best(best, best(previous, current)) */
+            pv_t bb = current;
+            if (have_prev) bb = (previous.v <= current.v) ? previous : current;
+            return (best.v <= bb.v) ? best.x : bb.x;
+        }
+        double p = 0, q = 0, r = 0, u = 0;
+        if (fabs(e) > tol1) {
+            r = (x - w) * (fv - fx);
+            q = (x - v) * (fw - fx);
+            p = (x - v) * q - (x - w) * r;
+            q = 2 * (q - r);
+            if (q > 0) p = -p;
+            else q = -q;
+            r = e;
+            e = d;
+            if (p > q * (a - x) && p < q * (b - x) && fabs(p) < fabs(0.5 * q * r)) {
+                d = p / q;
+                u = x + d;
+                if (u - a < tol2 || b - u < tol2) d = (x <= m) ? tol1 : -tol1;
+            } else {
+                e = (x < m) ? b - x : a - x;
+                d = GS * e;
+            }
+        } else {
+            e = (x < m) ? b - x : a - x;
+            d = GS * e;
+        }
+        if (fabs(d) < tol1) u = (d >= 0) ? x + tol1 : x - tol1;
+        else u = x + d;
+        double fu = ewma_value(o, u);
+        previous = current;
+        have_prev = 1;
+        current.x = u;
+        current.v = fu;
+        {
+            pv_t bb = (previous.v <= current.v) ? previous : current;
+            best = (best.v <= bb.v) ? best : bb;
+        }
+        /* SimpleUnivariateValueChecker(1e-8, 1e-8) */
+        {
+            const double pvv = previous.v, cvv = current.v;
+            const double diff = fabs(pvv - cvv);
+            const double size = fmax(fabs(pvv), fabs(cvv));
+            if (diff <= size * 1e-8 || diff <= 1e-8) return best.x;
+        }
+        if (fu <= fx) {
+            if (u < x) b = x;
+            else a = x;
+            v = w; fv = fw;
+            w = x; fw = fx;
+            x = u; fx = fu;
+        } else {
+            if (u < x) a = u;
+            else b = u;
+            if (fu <= fw || cm_precision_equals(w, x)) {
+                v = w; fv = fw;
+                w = u; fw = fu;
+            } else if (fu <= fv || cm_precision_equals(v, x) || cm_precision_equals(v, w)) {
+                v = u; fv = fu;
+            }
+        }
+    }
+}
+
+int orc_ewma_fit(const double* ts, int64_t n, double* smoothing, int64_t* evaluations) {
+    ewma_obj_t o = {ts, n, 0, 0};
+    double point = 0.94;                               /* InitialGuess(Array(.94)) */
+    double r = -orc_ewma_gradient(ts, n, point);       /* MINIMIZE: r = -gradient */
+    double dir = r;                                    /* IdentityPreconditioner */
+    int have = 0;
+    double cur_v = 0;
+    int st = ORC_OK;
+    for (int64_t iter = 1;; iter++) {
+        if (iter > 10000) { st = ORC_ERR_TOO_MANY_ITERATIONS; break; }
+        const double objective = ewma_value(&o, point);
+        if (o.too_many) { st = ORC_ERR_TOO_MANY_EVALUATIONS; break; }
+        if (have) {
+            /* SimpleValueChecker(1e-6, 1e-6) */
+            const double diff = fabs(cur_v - objective);
+            const double size = fmax(fabs(cur_v), fabs(objective));
+            if (diff <= size * 1e-6 || diff <= 1e-6) break;
+        }
+        have = 1;
+        cur_v = objective;
+        int lerr = 0;
+        const double step = cm_line_search(&o, point, dir, &lerr);
+        if (o.too_many || lerr == 1) { st = ORC_ERR_TOO_MANY_EVALUATIONS; break; }
+        if (lerr == 2) { st = ORC_ERR_BAD_ARG; break; }
+        point += step * dir;
+        r = -orc_ewma_gradient(ts, n, point);
+        dir = r;                                       /* iterations % 1 == 0: reset */
+    }
+    if (evaluations) *evaluations = o.evals;
+    *smoothing = (st == ORC_OK) ? point : NAN;
+    return st;
+}
+
+int orc_panel_ewma_fit(const double* in, int64_t S, int64_t T, int64_t ld, double* smoothing,
+                       int32_t* err, int threads) {
+    int any = 0;
+#pragma omp parallel for schedule(dynamic, 64) num_threads(threads > 0 ? threads : 1) reduction(| : any)
+    for (int64_t q = 0; q < S; q++) {
+        int st = orc_ewma_fit(in + q * ld, T, smoothing + q, NULL);
+        if (err) err[q] = st;
+        any |= (st != ORC_OK);
+    }
+    return any ? ORC_ERR_TOO_MANY_EVALUATIONS : ORC_OK;
+}
+
 /* ---------------- panel drivers: one "partition" per thread (local[N]) ---------------- */
 
 static int clamp_threads(int threads) { return threads > 0 ? threads : 1; }

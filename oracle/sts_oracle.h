@@ -31,6 +31,8 @@ extern "C" {
 #define ORC_ERR_REQUIREMENT 5
 #define ORC_ERR_NOT_ENOUGH_DATA 7
 #define ORC_ERR_SINGULAR 8
+#define ORC_ERR_TOO_MANY_EVALUATIONS 10
+#define ORC_ERR_TOO_MANY_ITERATIONS 11
 
 /* fill methods (same numbering as include/sts.h) */
 #define ORC_FILL_LINEAR 0
@@ -55,6 +57,9 @@ void orc_ewma_remove(const double* ts, double* dest, int64_t n, double s);
 void orc_ar_remove(const double* ts, double* dest, int64_t n, double c, const double* coef, int p);
 void orc_ar_add(const double* ts, double* dest, int64_t n, double c, const double* coef, int p);
 int  orc_ar_fit(const double* ts, int64_t n, int p, int no_intercept, double* c, double* coef);
+double orc_ewma_sse(const double* ts, int64_t n, double s);
+double orc_ewma_gradient(const double* ts, int64_t n, double s);
+int  orc_ewma_fit(const double* ts, int64_t n, double* smoothing, int64_t* evaluations);
 int  orc_ols_householder(const double* y, const double* x /* m x k row-major */, int64_t m,
                          int k, int no_intercept, double* beta /* k(+1) */);
 
@@ -67,6 +72,9 @@ int orc_panel_fill_diff_ewma(const double* in, double* out, int64_t S, int64_t T
                              double s, int threads);
 int orc_panel_ar_fit_remove(const double* in, double* out, int64_t S, int64_t T, int64_t ld,
                             int p, int no_intercept, double* c, double* coef, int threads);
+
+int orc_panel_ewma_fit(const double* in, int64_t S, int64_t T, int64_t ld, double* smoothing,
+                       int32_t* err, int threads);
 
 /* ---- synthetic generator; bit-identical to the device generator ---- */
 void   orc_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]);

@@ -119,6 +119,8 @@ struct ErrSink {
         for (int64_t s = 0; s < S; s++) {
             if (h[(size_t)s] == STS_ERR_ALL_NAN) return fail(STS_ERR_ALL_NAN, "Input is all NaNs! (series %lld)", (long long)s);
             if (h[(size_t)s] == STS_ERR_SINGULAR) return fail(STS_ERR_SINGULAR, "singular AR design matrix (series %lld)", (long long)s);
+            if (h[(size_t)s] == STS_ERR_TOO_MANY_EVALUATIONS)
+                return fail(STS_ERR_TOO_MANY_EVALUATIONS, "TooManyEvaluationsException: illegal state: maximal count (10000) exceeded: evaluations (series %lld)", (long long)s);
             if (h[(size_t)s] != 0) return fail(h[(size_t)s], "%s failed for series %lld", what, (long long)s);
         }
         return STS_OK;
@@ -491,6 +493,39 @@ int sts_ar_fit_remove(const double* in, double* out, int64_t S, int64_t T, int64
     if (!out) return fail(STS_ERR_BAD_ARG, "ar_fit_remove: null output");
     return ar_fit_common(in, out, S, T, ld_in, ld_out, p, no_intercept, c, coef, err_per_series, stream,
                          "ar_fit_remove");
+}
+
+int sts_ewma_fit(const double* in, int64_t S, int64_t T, int64_t ld, double* smoothing, int32_t* err_per_series,
+                 void* stream) {
+    int r;
+    if ((r = check_panel(in, S, T, ld, "EWMA.fitModel"))) return r;
+    if (S > 0 && T < 1) return fail(STS_ERR_BAD_ARG, "EWMA.fitModel: empty series (ts(0) does not exist)");
+    if (S > 0 && !smoothing) return fail(STS_ERR_BAD_ARG, "EWMA.fitModel: null output");
+    if (S == 0) return STS_OK;
+    if ((r = ensure_device())) return r;
+    hipStream_t st = as_stream(stream);
+    ErrSink es(err_per_series, S, st);
+    if ((r = es.prepare())) return r;
+    sts::EwmaFitArgs a{};
+    a.in = in; a.S = S; a.T = T; a.ld = ld; a.smoothing = smoothing; a.err = es.dev;
+    HIP_TRY(timed(st, [&] { return sts::launch_ewma_fit(a, true, st); }), "EWMA.fitModel");
+    return es.finish("EWMA.fitModel");
+}
+
+int sts_ewma_sse_gradient(const double* in, int64_t S, int64_t T, int64_t ld, const double* smoothing, double* sse,
+                          double* gradient, void* stream) {
+    int r;
+    if ((r = check_panel(in, S, T, ld, "EWMAModel.sse"))) return r;
+    if (S > 0 && T < 1) return fail(STS_ERR_BAD_ARG, "EWMAModel.sse: empty series (ts(0) does not exist)");
+    if (S > 0 && !smoothing) return fail(STS_ERR_BAD_ARG, "EWMAModel.sse: null smoothing");
+    if (S == 0 || (!sse && !gradient)) return STS_OK;
+    if ((r = ensure_device())) return r;
+    hipStream_t st = as_stream(stream);
+    sts::EwmaFitArgs a{};
+    a.in = in; a.S = S; a.T = T; a.ld = ld; a.smoothing = const_cast<double*>(smoothing);
+    a.sse = sse; a.grad = gradient;
+    HIP_TRY(timed(st, [&] { return sts::launch_ewma_fit(a, false, st); }), "EWMAModel.sse/gradient");
+    return STS_OK;
 }
 
 int sts_fill_diff_ewma(const double* in, double* out, int64_t S, int64_t T, int64_t ld_in, int64_t ld_out, int method,

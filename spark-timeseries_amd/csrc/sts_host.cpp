@@ -116,6 +116,18 @@ int sts_ewma_remove_host(const double* in, double* out, int64_t S, int64_t T, in
     return ewma_host(false, in, out, S, T, ld, sm);
 }
 
+int sts_ewma_fit_host(const double* in, int64_t S, int64_t T, int64_t ld, double* smoothing, int32_t* err) {
+    Dev di, ds, de;
+    int r;
+    if ((r = up(di, in, panel_bytes(S, ld))) || (r = up(ds, nullptr, (size_t)S * sizeof(double))) ||
+        (r = up(de, nullptr, (size_t)S * sizeof(int32_t))))
+        return finish(r);
+    r = sts_ewma_fit(di.as<double>(), S, T, ld, ds.as<double>(), err ? de.as<int32_t>() : nullptr, kStream);
+    if (r == STS_OK) r = down(smoothing, ds, (size_t)S * sizeof(double));
+    if (r == STS_OK) r = down(err, de, (size_t)S * sizeof(int32_t));
+    return finish(r);
+}
+
 int sts_ar_fit_host(const double* in, int64_t S, int64_t T, int64_t ld, int p, int no_intercept, double* c,
                     double* coef, int32_t* err) {
     Dev di, dc, dk, de;

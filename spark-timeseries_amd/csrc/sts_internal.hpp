@@ -91,6 +91,18 @@ struct ArArgs {
 };
 hipError_t launch_ar_fit(const ArArgs& a, hipStream_t st);
 
+// EWMA.fitModel and EWMAModel.sse / gradient (sts_ewma_fit.hip)
+struct EwmaFitArgs {
+    const double* in;
+    int64_t S, T, ld;
+    double* smoothing;    // fit: output; sse / gradient: input (per series)
+    double* sse;          // sse / gradient outputs (may be null)
+    double* grad;
+    int32_t* err;         // fit: per-series status (may be null)
+    int32_t* evals;       // fit: objective evaluations commons-math3 counted (may be null)
+};
+hipError_t launch_ewma_fit(const EwmaFitArgs& a, bool fit, hipStream_t st);
+
 // generators (sts_gen.hip)
 hipError_t launch_gen_panel(double* out, int64_t s0, int64_t S, int64_t T, int64_t ld,
                             uint64_t seed, uint32_t nan_thr, hipStream_t st);

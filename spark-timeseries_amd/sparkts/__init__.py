@@ -9,5 +9,6 @@ there is no CPU fallback.
 """
 from . import UnivariateTimeSeries  # noqa: F401
 from .errors import (DeviceError, IllegalArgumentException, MathIllegalArgumentException,  # noqa: F401
-                     NullPointerException, SingularMatrixException, UnsupportedOperationException)
+                     NullPointerException, SingularMatrixException, TooManyEvaluationsException,
+                     TooManyIterationsException, UnsupportedOperationException)
 from .timeseriesrdd import TimeSeriesRDD  # noqa: F401

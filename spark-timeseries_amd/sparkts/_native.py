@@ -45,6 +45,8 @@ SIGNATURES = {
                                      _c_vp, _c_vp]),
     "sts_ar_fit_remove": (_c_int, [_c_vp, _c_vp, _c_i64, _c_i64, _c_i64, _c_i64, _c_int, _c_int, _c_vp, _c_vp,
                                    _c_vp, _c_vp]),
+    "sts_ewma_fit": (_c_int, [_c_vp, _c_i64, _c_i64, _c_i64, _c_vp, _c_vp, _c_vp]),
+    "sts_ewma_sse_gradient": (_c_int, [_c_vp, _c_i64, _c_i64, _c_i64, _c_vp, _c_vp, _c_vp, _c_vp]),
     "sts_gen_panel": (_c_int, [_c_vp, _c_i64, _c_i64, _c_i64, _c_i64, ctypes.c_uint64, _c_dbl, _c_vp]),
     "sts_gen_ar_panel": (_c_int, [_c_vp, _c_vp, _c_vp, _c_i64, _c_i64, _c_i64, _c_i64, ctypes.c_uint64, _c_int, _c_vp]),
     "sts_fill_host": (_c_int, [_c_vp, _c_vp, _c_i64, _c_i64, _c_i64, _c_int, _c_vp]),
@@ -53,6 +55,7 @@ SIGNATURES = {
     "sts_lag_matrix_host": (_c_int, [_c_vp, _c_vp, _c_i64, _c_i64, _c_i64, _c_int, _c_int]),
     "sts_ewma_add_host": (_c_int, [_c_vp, _c_vp, _c_i64, _c_i64, _c_i64, _c_vp]),
     "sts_ewma_remove_host": (_c_int, [_c_vp, _c_vp, _c_i64, _c_i64, _c_i64, _c_vp]),
+    "sts_ewma_fit_host": (_c_int, [_c_vp, _c_i64, _c_i64, _c_i64, _c_vp, _c_vp]),
     "sts_ar_fit_host": (_c_int, [_c_vp, _c_i64, _c_i64, _c_i64, _c_int, _c_int, _c_vp, _c_vp, _c_vp]),
     "sts_ar_remove_host": (_c_int, [_c_vp, _c_vp, _c_i64, _c_i64, _c_i64, _c_vp, _c_vp, _c_int]),
     "sts_ar_add_host": (_c_int, [_c_vp, _c_vp, _c_i64, _c_i64, _c_i64, _c_vp, _c_vp, _c_int]),

@@ -16,6 +16,8 @@ STS_ERR_NULL_DEST = 6
 STS_ERR_NOT_ENOUGH_DATA = 7
 STS_ERR_SINGULAR = 8
 STS_ERR_NO_DEVICE = 9
+STS_ERR_TOO_MANY_EVALUATIONS = 10
+STS_ERR_TOO_MANY_ITERATIONS = 11
 
 
 class IllegalArgumentException(ValueError):
@@ -36,6 +38,14 @@ class MathIllegalArgumentException(ValueError):
 
 class SingularMatrixException(ArithmeticError):
     """commons-math3 SingularMatrixException."""
+
+
+class TooManyEvaluationsException(RuntimeError):
+    """commons-math3 TooManyEvaluationsException (EWMA.fitModel: MaxEval 10000 exceeded)."""
+
+
+class TooManyIterationsException(RuntimeError):
+    """commons-math3 TooManyIterationsException (EWMA.fitModel: MaxIter 10000 exceeded)."""
 
 
 class DeviceError(RuntimeError):
@@ -66,4 +76,8 @@ def raise_for_status(status: int, what: str = "") -> None:
         raise SingularMatrixException(msg)
     if status == STS_ERR_BAD_ARG:
         raise IllegalArgumentException(msg)
+    if status == STS_ERR_TOO_MANY_EVALUATIONS:
+        raise TooManyEvaluationsException(msg)
+    if status == STS_ERR_TOO_MANY_ITERATIONS:
+        raise TooManyIterationsException(msg)
     raise DeviceError("%s (status %d)" % (msg, status))

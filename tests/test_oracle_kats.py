@@ -191,6 +191,52 @@ def test_ewma_remove_kat():
     assert int(orig[-1]) == 10
 
 
+# ---- T/models/EWMASuite.scala:54-63 (fitting EWMA model) ----
+
+OIL = [446.7, 454.5, 455.7, 423.6, 456.3, 440.6, 425.3, 485.1, 506.0, 526.8, 514.3, 494.2]
+
+
+def test_ewma_fit_oil_kat():
+    # the reference's only pin of the commons-math3 optimizer restatement: (s * 100).toInt == 89
+    st, s, evals = oracle.ewma_fit(OIL)
+    assert st == oracle.OK
+    assert int(s * 100.0) == 89
+    assert evals > 0
+
+
+def test_ewma_sse_gradient_consistent():
+    # EWMAModel.gradient (:102-123) is MINUS the derivative of EWMAModel.sse (:80-95):
+    # d(error^2)/ds = -2 * error * dS/ds, and the reference accumulates +error * dSda.
+    # Restated as the reference has it (the line search then walks backwards along the
+    # search direction: BracketFinder accepts negative steps).
+    rng = np.random.default_rng(3)
+    x = np.cumsum(rng.standard_normal(300)) + 50
+    for s in (0.1, 0.5, 0.9, 1.2):
+        h = 1e-6
+        fd = (oracle.ewma_sse(x, s + h) - oracle.ewma_sse(x, s - h)) / (2 * h)
+        g = oracle.ewma_gradient(x, s)
+        assert abs(fd + g) <= 1e-5 * max(1.0, abs(g))
+
+
+def test_ewma_fit_nan_series_never_converges():
+    # a NaN makes every sse NaN: commons-math3 ends in TooManyEvaluationsException
+    x = np.ones(10)
+    x[3] = np.nan
+    st, s, evals = oracle.ewma_fit(x)
+    assert st == oracle.ERR_TOO_MANY_EVALUATIONS and math.isnan(s) and evals == 10001
+
+
+def test_ewma_fit_is_a_minimum():
+    rng = np.random.default_rng(4)
+    for T in (50, 390):
+        x = np.cumsum(rng.standard_normal(T)) + 100
+        st, s, _ = oracle.ewma_fit(x)
+        assert st == oracle.OK
+        grid = np.linspace(0.01, 2.0, 400)
+        best = grid[int(np.argmin([oracle.ewma_sse(x, g) for g in grid]))]
+        assert abs(s - best) < 0.02   # SimpleValueChecker(1e-6, 1e-6) stops near, not at, the minimum
+
+
 # ---- T/models/AutoregressionSuite.scala:25-51 ----
 
 def test_ar1_fit():

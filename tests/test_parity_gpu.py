@@ -381,6 +381,74 @@ def test_ewma_panels(torch):
         EWMAModel(0.2).removeTimeDependentEffects(dev(torch, [1.0, 2.0]))
 
 
+# ---------------- EWMA.fitModel: bit-exact ----------------
+# Every sse / gradient evaluation is the reference's sequential loop, so the device
+# optimizer takes the oracle's (commons-math3 restatement's) exact path: smoothing values
+# and statuses are compared BIT-EXACT.
+
+OIL = [446.7, 454.5, 455.7, 423.6, 456.3, 440.6, 425.3, 485.1, 506.0, 526.8, 514.3, 494.2]
+
+
+def test_ewma_fit_oil_kat(torch):
+    # T/models/EWMASuite.scala:54-63
+    from sparkts.models import EWMA
+    m = EWMA.fitModel(dev(torch, OIL))
+    assert int(m.smoothing * 100.0) == 89
+    st, ref, _ = oracle.ewma_fit(OIL)
+    assert_bits(np.array([m.smoothing]), np.array([ref]), "oil")
+    mh = EWMA.fitModel(np.array(OIL))          # host-staging (JNI) path
+    assert_bits(np.array([mh.smoothing]), np.array([ref]), "oil host")
+
+
+@pytest.mark.parametrize("T", [2, 3, 12, 63, 64, 65, 390, 1000])
+def test_ewma_fit_panels(torch, T):
+    from sparkts.models import EWMA
+    rng = np.random.default_rng(T)
+    S = 70   # three waves of 32 series, the last one partial
+    x = np.cumsum(rng.standard_normal((S, T)), axis=1) + 100 + rng.uniform(-5, 5, (S, 1))
+    x[5] = 3.0                                  # constant series
+    x[6] = rng.standard_normal(T)               # white noise
+    err = torch.zeros(S, dtype=torch.int32, device="cuda:0")
+    m = EWMA.fitModel(dev(torch, x), errors=err)
+    ref_s, ref_err = oracle.panel_ewma_fit(x, threads=8)
+    assert np.array_equal(host(err), ref_err)
+    assert_bits(host(m.smoothing), ref_s, "EWMA.fitModel T=%d" % T)
+
+
+def test_ewma_fit_nan_and_short(torch):
+    from sparkts.models import EWMA
+    from sparkts.errors import TooManyEvaluationsException
+    x = np.cumsum(np.random.default_rng(1).standard_normal((40, 50)), axis=1)
+    x[3, 0] = NaN
+    x[17, 49] = NaN
+    x[20, 25] = NaN
+    err = torch.zeros(40, dtype=torch.int32, device="cuda:0")
+    m = EWMA.fitModel(dev(torch, x), errors=err)
+    ref_s, ref_err = oracle.panel_ewma_fit(x, threads=8)
+    assert np.array_equal(host(err), ref_err)
+    assert set(np.flatnonzero(ref_err)) == {3, 17, 20}
+    assert_bits(host(m.smoothing), ref_s, "nan panel")
+    with pytest.raises(TooManyEvaluationsException):
+        EWMA.fitModel(dev(torch, x))
+    # T = 1: sse = 0 everywhere, the optimizer stops at its start point
+    one = EWMA.fitModel(dev(torch, [5.0]))
+    assert one.smoothing == oracle.ewma_fit([5.0])[1]
+
+
+def test_ewma_sse_gradient(torch):
+    from sparkts.models import EWMAModel
+    from sparkts.models.EWMA import gradient, sse
+    rng = np.random.default_rng(11)
+    for S, T in [(1, 1), (33, 2), (64, 390), (5, 3000)]:
+        x = rng.standard_normal((S, T)) + 10
+        s = rng.uniform(0.05, 1.5, S)
+        xd = dev(torch, x)
+        f = host(sse(EWMAModel(dev(torch, s)), xd))
+        g = host(gradient(EWMAModel(dev(torch, s)), xd))
+        assert_bits(f, np.array([oracle.ewma_sse(r, v) for r, v in zip(x, s)]), "sse")
+        assert_bits(g, np.array([oracle.ewma_gradient(r, v) for r, v in zip(x, s)]), "gradient")
+
+
 # ---------------- AR (a11-a13) ----------------
 
 def test_ar_fit_reference_suite(torch):
