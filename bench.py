@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """bench.py -- series-elements/s and % HBM roofline of the fused fill + ACF hot path.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c3|c2|c4|c5|c1]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c3|c2|c4|c5|c1|ewma_fit]
 
 Default workload (the BASELINE.json metric "fill+lag+ACF", config C3): every rank owns
 a C3 shard of 12,500 series x 982,800 minute bars (fp64, 5 % NaN, Philox synthetic,
@@ -35,6 +35,9 @@ WORKLOADS = {
     "c2": (1_000_000, 390, 0.05, 2,
            "C2: fillPrevious -> differencesAtLag(1) -> EWMA(0.2).add, 1,000,000 series x 390 steps"),
     "c4": (500_000, 2_520, 0.0, 4, "C4: AR(5) fit + removeTimeDependentEffects, 500,000 series x 2,520 steps"),
+    "ewma_fit": (1_000_000, 390, 0.0, 6,
+                 "EWMA.fitModel (SURVEY.md 8(f) rank 1): commons-math3 NLCG + bracket + Brent per series, "
+                 "1,000,000 series x 390 steps (the C2 shape)"),
     "c5": (1_250, 10_000_000, 0.30, 5,
            "C5 shard: fill('nearest') + lag(10, false), 1,250 series x 10,000,000 steps per GPU (N=8 -> C5's "
            "10k x 10M); lag matrices written into a reused scratch slab, 10 series per call"),
@@ -97,6 +100,8 @@ def main():
     else:
         raise_for_status(lib.sts_gen_panel(x.data_ptr(), s0, S, T, T, seed, nan_p, sp), "gen")
     smooth = torch.full((S,), 0.2, dtype=torch.float64, device=dev)
+    if args.workload == "ewma_fit":
+        smooth = torch.empty((S,), dtype=torch.float64, device=dev)
     if args.workload == "c5":
         P, LB = 10, 10            # lag(10, includeOriginal = false); series per call
         lagbuf = torch.empty((LB, P, T - P), dtype=torch.float64, device=dev)
@@ -117,6 +122,11 @@ def main():
                 raise_for_status(lib.sts_fill_lag_matrix(x[b0].data_ptr(), out[b0].data_ptr(), lagbuf.data_ptr(), nb,
                                                          T, T, T, 1, P, 0, err[b0:].data_ptr(), sp),
                                  "fill_lag_matrix")
+        elif args.workload == "ewma_fit":
+            raise_for_status(lib.sts_ewma_fit(x.data_ptr(), S, T, T, smooth.data_ptr(), err.data_ptr(), sp),
+                             "EWMA.fitModel")
+            if world > 1:
+                all_gather_results(smooth[:, None])
         elif args.workload == "c4":
             raise_for_status(lib.sts_ar_fit_remove(x.data_ptr(), out.data_ptr(), S, T, T, T, p_ar, 0,
                                                    c_fit.data_ptr(), coef_fit.data_ptr(), err.data_ptr(), sp),
@@ -160,11 +170,15 @@ def main():
     bytes_per_step = 16.0 * S * T        # 8 B read + 8 B written per element
     if args.workload == "c5":            # + the lag matrix: 8 * P bytes per row, (T - P) rows per series
         bytes_per_step += 8.0 * P * (T - P) * S
+    if args.workload == "ewma_fit":      # the series read once + one parameter written (algorithmic)
+        bytes_per_step = 8.0 * S * T + 8.0 * S
     kernel = {"c3": "sts::tile_kernel<4096,4,shifted> (fill linear + ACF partials, FP64 MFMA)",
               "c1": "sts::seg_kernel<2> (wave-private series segments: fill linear + ACF partials, FP64 MFMA)",
               "c5": "sts::tile_kernel<4096,0> (fill nearest + lag-matrix columns)",
               "c2": "sts::recur_kernel<kFillDiffEwma> (fillPrevious -> differencesAtLag(1) -> EWMA add, lane per series)",
-              "c4": "sts::ar_fit_kernel (AR(5) Gram on FP64 MFMA + solve + fused remove)"}[args.workload]
+              "c4": "sts::ar_fit_kernel (AR(5) Gram on FP64 MFMA + solve + fused remove)",
+              "ewma_fit": "sts::ewma_fit_kernel<32,64> (lane-per-series commons-math3 optimizer; one sse+gradient "
+                          "pass over the wave's series block per optimizer request)"}[args.workload]
     roofline = None
     if launches[0] > 0:
         avg_ms = kern_ms[0] / launches[0]
@@ -178,7 +192,7 @@ def main():
 
     cpu = None
     if rank == 0 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(args, S, T, K, seed, nan_p, out, acf, p_ar)
+        cpu = cpu_baseline(args, S, T, K, seed, nan_p, out, acf, p_ar, smooth)
 
     if rank == 0:
         line = {
@@ -189,7 +203,8 @@ def main():
             "data": "synthetic: Philox4x32-10 counter-based panel generated in HBM (SURVEY.md 8(d)), %g NaN" % nan_p,
             "config": {"workload": desc, "series_per_gpu": S, "steps_per_series": T,
                        "numLags": K if args.workload in ("c3", "c1") else None,
-                       "fill": {"c3": "linear", "c1": "linear", "c2": "previous", "c4": None, "c5": "nearest"}[args.workload],
+                       "fill": {"c3": "linear", "c1": "linear", "c2": "previous", "c4": None, "c5": "nearest",
+                                "ewma_fit": None}[args.workload],
                        "parallelism": "dp%d (series sharded by key, one process per GPU)" % world},
             "roofline": roofline,
             "cpu_baseline": cpu,
@@ -214,7 +229,7 @@ def measured_traffic(workload, S, T):
     return rec.get("traffic_bytes_per_launch")
 
 
-def cpu_baseline(args, S, T, K, seed, nan_p, out, acf, p_ar):
+def cpu_baseline(args, S, T, K, seed, nan_p, out, acf, p_ar, smooth=None):
     """The oracle (CPU restatement of the reference loops, oracle/) on a bounded sample of
     the same workload, one series per thread like Spark local[N].  The sample series are
     the rank-0 series 0..n-1, so their GPU results are also checked here."""
@@ -241,11 +256,13 @@ def cpu_baseline(args, S, T, K, seed, nan_p, out, acf, p_ar):
             rf, _ = oracle.panel_fill(xs, "nearest", threads=threads)
             for r in rf:
                 oracle.lag(r, 10, False)
+        elif args.workload == "ewma_fit":
+            rf, _ = oracle.panel_ewma_fit(xs, threads=threads)
         else:
             rf, _, _ = oracle.panel_ar_fit_remove(xs, p_ar, threads=threads)
         elapsed += time.perf_counter() - t0
         if s_next == 0:
-            g = out[:n].cpu().numpy()
+            g = (smooth[:n] if args.workload == "ewma_fit" else out[:n]).cpu().numpy()
             if args.workload != "c4":
                 exact = bool(np.array_equal(np.isnan(g), np.isnan(rf)) and
                              np.array_equal(np.nan_to_num(g), np.nan_to_num(rf)))

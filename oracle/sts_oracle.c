@@ -443,7 +443,7 @@ static double cm_line_search(ewma_obj_t* o, double point, double dir, int* err) 
     const double GS = 0.5 * (3 - sqrt(5.0));
     double a = lo, b = hi;
     double x = mid, v = x, w = x, d = 0, e = 0;
-    double fx = ewma_value(o, x);
+    double fx = ewma_value(o, point + x * dir);
     double fv = fx, fw = fx;
     pv_t previous = {0, 0}, current = {x, fx}, best = current;
     int have_prev = 0;
@@ -483,7 +483,7 @@ static double cm_line_search(ewma_obj_t* o, double point, double dir, int* err) 
         }
         if (fabs(d) < tol1) u = (d >= 0) ? x + tol1 : x - tol1;
         else u = x + d;
-        double fu = ewma_value(o, u);
+        double fu = ewma_value(o, point + u * dir);
         previous = current;
         have_prev = 1;
         current.x = u;
