@@ -131,7 +131,7 @@ constexpr double kBrentAbs = 4.9406564584124654e-324;   // LineSearch.ABS_TOL_UN
     STS_COUNT()
 
 // Runs lane o's optimizer until its next uncached request (o.status stays -1) or the end.
-STS_HD inline void ewma_advance(EwmaOpt& o) {
+__attribute__((noinline)) STS_HD void ewma_advance(EwmaOpt& o) {
     switch (o.pc) {
     case 0:
         o.point = 0.94;                                   // InitialGuess(Array(.94))
