@@ -145,6 +145,37 @@ int sts_ewma_fit(const double* in, int64_t S, int64_t T, int64_t ld, double* smo
 int sts_ewma_sse_gradient(const double* in, int64_t S, int64_t T, int64_t ld,
                           const double* smoothing, double* sse, double* gradient, void* stream);
 
+/* ---- f2: TimeSeriesRDD.seriesStats() (S/TimeSeriesRDD.scala:204-206): Spark 1.3.1
+ * StatCounter over each series' values, NaN included, merged in order
+ * (delta = v - mu; n += 1; mu += delta / n; m2 += delta * (v - mu); max / min via
+ * java.lang.Math).  stats[s*4 + 0..3] = (mean, m2, max, min); count = T for every series
+ * (variance = m2 / n etc. are derived exactly as StatCounter does).  Bit-exact. */
+int sts_series_stats(const double* in, int64_t S, int64_t T, int64_t ld, double* stats,
+                     void* stream);
+
+/* ---- f3: TimeSeriesRDD.removeInstantsWithNaNs() (S/TimeSeriesRDD.scala:131-152) in three
+ * steps, so partitions on different GPUs can combine their NaN flags in between (an
+ * all-reduce MAX of `flags`, the reference's aggregate(merge, comb) of Boolean arrays):
+ *   sts_nan_instants     flags[t] = 1 where any series of the panel is NaN at t (flags are
+ *                        only ever set: zero them first; repeated calls OR together);
+ *   sts_active_instants  active[0 .. *n_active) = the instants with flags[t] == 0, in
+ *                        increasing order; n_active is a device int64;
+ *   sts_gather_instants  out[s*ld_out + j] = in[s*ld_in + active[j]], j < n_active.
+ * Bit-exact (copies). */
+int sts_nan_instants(const double* in, int64_t S, int64_t T, int64_t ld, uint8_t* flags,
+                     void* stream);
+int sts_active_instants(const uint8_t* flags, int64_t T, int64_t* active, int64_t* n_active,
+                        void* stream);
+int sts_gather_instants(const double* in, double* out, int64_t S, int64_t ld_in, int64_t ld_out,
+                        const int64_t* active, int64_t n_active, void* stream);
+
+/* ---- f4: TimeSeriesRDD.toInstants (S/TimeSeriesRDD.scala:215-324), the local step: the
+ * panel transpose out[t*ld_out + s] = in[s*ld_in + t] -- one record per instant holding
+ * every series' value in partition (series) order.  Across GPUs the instants are
+ * re-partitioned by time with an all-to-all (sparkts.TimeSeriesRDD.toInstants).  Bit-exact. */
+int sts_to_instants(const double* in, double* out, int64_t S, int64_t T, int64_t ld_in,
+                    int64_t ld_out, void* stream);
+
 /* ---- a11: Autoregression.fitModel(ts, p, noIntercept) (S/models/Autoregression.scala:38-53).
  * c[s] and coef[s*p + j] receive the model; 1 <= p <= 31.  T - p < p + 1 ->
  * STS_ERR_NOT_ENOUGH_DATA.  1e-10 relative to a Householder-QR OLS. */

@@ -64,6 +64,9 @@ def lib():
             "orc_ewma_gradient": (ctypes.c_double, [_dp, _i64, ctypes.c_double]),
             "orc_ewma_fit": (ctypes.c_int, [_dp, _i64, _dp, ctypes.POINTER(ctypes.c_int64)]),
             "orc_panel_ewma_fit": (ctypes.c_int, [_dp, _i64, _i64, _i64, _dp, i32p, ctypes.c_int]),
+            "orc_stat_counter": (None, [_dp, _i64, _dp]),
+            "orc_remove_instants_with_nans": (_i64, [_dp, _i64, _i64, _i64, _dp, ctypes.POINTER(ctypes.c_int64)]),
+            "orc_to_instants": (None, [_dp, _i64, _i64, _i64, _dp]),
             "orc_gen_value": (ctypes.c_double, [ctypes.c_uint64, _i64, _i64, _i64]),
             "orc_nan_threshold": (ctypes.c_uint32, [ctypes.c_double]),
             "orc_gen_panel": (None, [ctypes.c_uint64, _i64, _i64, _i64, _i64, ctypes.c_double, _dp]),
@@ -206,6 +209,26 @@ def ewma_fit(ts):
     ts = _vec(ts); sm = np.zeros(1); ev = ctypes.c_int64(0)
     st = lib().orc_ewma_fit(_p(ts), ts.size, _p(sm), ctypes.byref(ev))
     return st, float(sm[0]), int(ev.value)
+
+
+def stat_counter(ts):
+    """Spark StatCounter over the series values -> (count, mean, m2, max, min)."""
+    ts = _vec(ts); out = np.zeros(4); lib().orc_stat_counter(_p(ts), ts.size, _p(out))
+    return (ts.size,) + tuple(float(v) for v in out)
+
+
+def remove_instants_with_nans(x):
+    """TimeSeriesRDD.removeInstantsWithNaNs over one panel -> (out (S, n), active (n,))."""
+    x = np.ascontiguousarray(x, dtype=np.float64); S, T = x.shape
+    out = np.empty(S * T); active = np.empty(max(T, 1), np.int64)
+    n = lib().orc_remove_instants_with_nans(_p(x), S, T, T, _p(out),
+                                            active.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)))
+    return out[: S * n].reshape(S, n), active[:n]
+
+
+def to_instants(x):
+    x = np.ascontiguousarray(x, dtype=np.float64); S, T = x.shape
+    out = np.empty((T, S)); lib().orc_to_instants(_p(x), S, T, T, _p(out)); return out
 
 
 # ---------------- panel drivers ----------------

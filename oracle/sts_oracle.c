@@ -563,6 +563,67 @@ int orc_panel_ewma_fit(const double* in, int64_t S, int64_t T, int64_t ld, doubl
     return any ? ORC_ERR_TOO_MANY_EVALUATIONS : ORC_OK;
 }
 
+/* ---------------- TimeSeriesRDD.seriesStats / removeInstantsWithNaNs / toInstants ---------------- */
+
+/* java.lang.Math.max / min (Scala math.max / min): NaN propagates; signed zeros ordered */
+static double jmax(double a, double b) {
+    if (a != a) return a;
+    if (a == 0.0 && b == 0.0 && signbit(a)) return b;
+    return (a >= b) ? a : b;
+}
+static double jmin(double a, double b) {
+    if (a != a) return a;
+    if (a == 0.0 && b == 0.0 && signbit(b)) return b;
+    return (a <= b) ? a : b;
+}
+
+/* S/TimeSeriesRDD.scala:204-206: new StatCounter(series.valuesIterator).  Spark 1.3.1
+ * StatCounter (spark-core, not vendored) restated: n = 0, mu = 0, m2 = 0, max = -Inf,
+ * min = +Inf, then per value merge(value): delta = value - mu; n += 1; mu += delta / n;
+ * m2 += delta * (value - mu); maxValue = math.max(maxValue, value); minValue = math.min(...).
+ * out = (mu, m2, max, min); count = n. */
+void orc_stat_counter(const double* ts, int64_t n, double out[4]) {
+    int64_t cnt = 0;
+    double mu = 0.0, m2 = 0.0, mx = -INFINITY, mn = INFINITY;
+    for (int64_t i = 0; i < n; i++) {
+        const double value = ts[i];
+        const double delta = value - mu;
+        cnt += 1;
+        mu += delta / (double)cnt;
+        m2 += delta * (value - mu);
+        mx = jmax(mx, value);
+        mn = jmin(mn, value);
+    }
+    out[0] = mu;
+    out[1] = m2;
+    out[2] = mx;
+    out[3] = mn;
+}
+
+/* S/TimeSeriesRDD.scala:131-152: nans = aggregate(zero)(merge: arr(i) |= rec(i).isNaN,
+ * comb: OR); activeIndices = indices with !nans; every series -> its values at activeIndices.
+ * Returns the number of active instants; out is S x n_active (ld n_active), active[] the kept
+ * positions. */
+int64_t orc_remove_instants_with_nans(const double* in, int64_t S, int64_t T, int64_t ld, double* out,
+                                      int64_t* active) {
+    unsigned char* nans = (unsigned char*)calloc((size_t)(T > 0 ? T : 1), 1);
+    for (int64_t s = 0; s < S; s++)
+        for (int64_t i = 0; i < T; i++) nans[i] |= isnan(in[s * ld + i]) ? 1 : 0;
+    int64_t na = 0;
+    for (int64_t i = 0; i < T; i++)
+        if (!nans[i]) active[na++] = i;
+    for (int64_t s = 0; s < S; s++)
+        for (int64_t j = 0; j < na; j++) out[s * na + j] = in[s * ld + active[j]];
+    free(nans);
+    return na;
+}
+
+/* S/TimeSeriesRDD.scala:215-324: one record per instant, values in series order */
+void orc_to_instants(const double* in, int64_t S, int64_t T, int64_t ld, double* out) {
+    for (int64_t t = 0; t < T; t++)
+        for (int64_t s = 0; s < S; s++) out[t * S + s] = in[s * ld + t];
+}
+
 /* ---------------- panel drivers: one "partition" per thread (local[N]) ---------------- */
 
 static int clamp_threads(int threads) { return threads > 0 ? threads : 1; }

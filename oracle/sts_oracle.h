@@ -60,6 +60,10 @@ int  orc_ar_fit(const double* ts, int64_t n, int p, int no_intercept, double* c,
 double orc_ewma_sse(const double* ts, int64_t n, double s);
 double orc_ewma_gradient(const double* ts, int64_t n, double s);
 int  orc_ewma_fit(const double* ts, int64_t n, double* smoothing, int64_t* evaluations);
+void orc_stat_counter(const double* ts, int64_t n, double out[4]);
+int64_t orc_remove_instants_with_nans(const double* in, int64_t S, int64_t T, int64_t ld, double* out,
+                                      int64_t* active);
+void orc_to_instants(const double* in, int64_t S, int64_t T, int64_t ld, double* out);
 int  orc_ols_householder(const double* y, const double* x /* m x k row-major */, int64_t m,
                          int k, int no_intercept, double* beta /* k(+1) */);
 

@@ -528,6 +528,65 @@ int sts_ewma_sse_gradient(const double* in, int64_t S, int64_t T, int64_t ld, co
     return STS_OK;
 }
 
+int sts_series_stats(const double* in, int64_t S, int64_t T, int64_t ld, double* stats, void* stream) {
+    int r;
+    if ((r = check_panel(in, S, T, ld, "seriesStats"))) return r;
+    if (S > 0 && !stats) return fail(STS_ERR_BAD_ARG, "seriesStats: null output");
+    if (S == 0) return STS_OK;
+    if ((r = ensure_device())) return r;
+    hipStream_t st = as_stream(stream);
+    HIP_TRY(timed(st, [&] { return sts::launch_series_stats(in, stats, S, T, ld, st); }), "seriesStats");
+    return STS_OK;
+}
+
+int sts_nan_instants(const double* in, int64_t S, int64_t T, int64_t ld, uint8_t* flags, void* stream) {
+    int r;
+    if ((r = check_panel(in, S, T, ld, "removeInstantsWithNaNs"))) return r;
+    if (T > 0 && !flags) return fail(STS_ERR_BAD_ARG, "removeInstantsWithNaNs: null flags");
+    if (S * T == 0) return STS_OK;
+    if ((r = ensure_device())) return r;
+    hipStream_t st = as_stream(stream);
+    HIP_TRY(timed(st, [&] { return sts::launch_nan_instants(in, flags, S, T, ld, st); }), "nan_instants");
+    return STS_OK;
+}
+
+int sts_active_instants(const uint8_t* flags, int64_t T, int64_t* active, int64_t* n_active, void* stream) {
+    if (T < 0) return fail(STS_ERR_BAD_ARG, "active_instants: negative T");
+    if (!n_active || (T > 0 && (!flags || !active))) return fail(STS_ERR_BAD_ARG, "active_instants: null pointer");
+    int r;
+    if ((r = ensure_device())) return r;
+    hipStream_t st = as_stream(stream);
+    Scratch sc(st);
+    HIP_TRY(sc.alloc((size_t)sts::active_scratch_elems(T) * sizeof(int64_t)), "hipMallocAsync(active scratch)");
+    HIP_TRY(sts::launch_active_instants(flags, T, active, n_active, static_cast<int64_t*>(sc.p), st), "active_instants");
+    return STS_OK;
+}
+
+int sts_gather_instants(const double* in, double* out, int64_t S, int64_t ld_in, int64_t ld_out, const int64_t* active,
+                        int64_t n_active, void* stream) {
+    if (S < 0 || n_active < 0 || ld_out < n_active) return fail(STS_ERR_BAD_ARG, "gather_instants: bad shape");
+    if (S * n_active > 0 && (!in || !out || !active)) return fail(STS_ERR_BAD_ARG, "gather_instants: null pointer");
+    if (S * n_active == 0) return STS_OK;
+    int r;
+    if ((r = ensure_device())) return r;
+    hipStream_t st = as_stream(stream);
+    HIP_TRY(timed(st, [&] { return sts::launch_gather_instants(in, out, active, n_active, S, ld_in, ld_out, st); }),
+            "gather_instants");
+    return STS_OK;
+}
+
+int sts_to_instants(const double* in, double* out, int64_t S, int64_t T, int64_t ld_in, int64_t ld_out, void* stream) {
+    int r;
+    if ((r = check_panel(in, S, T, ld_in, "toInstants"))) return r;
+    if (ld_out < S) return fail(STS_ERR_BAD_ARG, "toInstants: ld_out %lld < S=%lld", (long long)ld_out, (long long)S);
+    if (S * T > 0 && !out) return fail(STS_ERR_BAD_ARG, "toInstants: null output");
+    if (S * T == 0) return STS_OK;
+    if ((r = ensure_device())) return r;
+    hipStream_t st = as_stream(stream);
+    HIP_TRY(timed(st, [&] { return sts::launch_transpose(in, out, S, T, ld_in, ld_out, st); }), "toInstants");
+    return STS_OK;
+}
+
 int sts_fill_diff_ewma(const double* in, double* out, int64_t S, int64_t T, int64_t ld_in, int64_t ld_out, int method,
                        int lag, const double* smoothing, int32_t* err_per_series, void* stream) {
     int r;

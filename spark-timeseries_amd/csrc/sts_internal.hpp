@@ -103,6 +103,17 @@ struct EwmaFitArgs {
 };
 hipError_t launch_ewma_fit(const EwmaFitArgs& a, bool fit, hipStream_t st);
 
+// seriesStats / removeInstantsWithNaNs / toInstants (sts_instants.hip)
+hipError_t launch_series_stats(const double* in, double* out, int64_t S, int64_t T, int64_t ld, hipStream_t st);
+hipError_t launch_nan_instants(const double* in, uint8_t* flags, int64_t S, int64_t T, int64_t ld, hipStream_t st);
+int64_t active_scratch_elems(int64_t T);
+hipError_t launch_active_instants(const uint8_t* flags, int64_t T, int64_t* active, int64_t* n_active,
+                                  int64_t* scratch, hipStream_t st);
+hipError_t launch_gather_instants(const double* in, double* out, const int64_t* active, int64_t n_active, int64_t S,
+                                  int64_t ld_in, int64_t ld_out, hipStream_t st);
+hipError_t launch_transpose(const double* in, double* out, int64_t S, int64_t T, int64_t ld_in, int64_t ld_out,
+                            hipStream_t st);
+
 // generators (sts_gen.hip)
 hipError_t launch_gen_panel(double* out, int64_t s0, int64_t S, int64_t T, int64_t ld,
                             uint64_t seed, uint32_t nan_thr, hipStream_t st);

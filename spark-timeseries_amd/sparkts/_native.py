@@ -47,6 +47,11 @@ SIGNATURES = {
                                    _c_vp, _c_vp]),
     "sts_ewma_fit": (_c_int, [_c_vp, _c_i64, _c_i64, _c_i64, _c_vp, _c_vp, _c_vp]),
     "sts_ewma_sse_gradient": (_c_int, [_c_vp, _c_i64, _c_i64, _c_i64, _c_vp, _c_vp, _c_vp, _c_vp]),
+    "sts_series_stats": (_c_int, [_c_vp, _c_i64, _c_i64, _c_i64, _c_vp, _c_vp]),
+    "sts_nan_instants": (_c_int, [_c_vp, _c_i64, _c_i64, _c_i64, _c_vp, _c_vp]),
+    "sts_active_instants": (_c_int, [_c_vp, _c_i64, _c_vp, _c_vp, _c_vp]),
+    "sts_gather_instants": (_c_int, [_c_vp, _c_vp, _c_i64, _c_i64, _c_i64, _c_vp, _c_i64, _c_vp]),
+    "sts_to_instants": (_c_int, [_c_vp, _c_vp, _c_i64, _c_i64, _c_i64, _c_i64, _c_vp]),
     "sts_gen_panel": (_c_int, [_c_vp, _c_i64, _c_i64, _c_i64, _c_i64, ctypes.c_uint64, _c_dbl, _c_vp]),
     "sts_gen_ar_panel": (_c_int, [_c_vp, _c_vp, _c_vp, _c_i64, _c_i64, _c_i64, _c_i64, ctypes.c_uint64, _c_int, _c_vp]),
     "sts_fill_host": (_c_int, [_c_vp, _c_vp, _c_i64, _c_i64, _c_i64, _c_int, _c_vp]),

@@ -61,6 +61,73 @@ class TimeSeriesRDD:
                                     p.stream), "fill_autocorr")
         return TimeSeriesRDD(self.index, self.keys, filled), acf
 
+    # --- S/TimeSeriesRDD.scala:204-206 ---
+    def seriesStats(self) -> "StatCounters":
+        """map(kt => new StatCounter(kt._2.valuesIterator)) over the partition: one lane-per-
+        series Welford pass on the device, in StatCounter.merge's order (bit-exact)."""
+        p = Panel(self.data)
+        if not p.device:
+            raise TypeError("seriesStats runs on device-resident partitions (torch GPU tensors)")
+        import torch
+        st = torch.empty((p.S, 4), dtype=torch.float64, device=p.t.device)
+        check(_native.lib().sts_series_stats(ptr(p.t), p.S, p.T, p.ld, ptr(st), p.stream), "seriesStats")
+        return StatCounters(p.T, st)
+
+    # --- S/TimeSeriesRDD.scala:131-152 ---
+    def removeInstantsWithNaNs(self, group=None) -> "TimeSeriesRDD":
+        """Drop every instant at which ANY series of the whole RDD is NaN.  The reference
+        aggregates per-partition Boolean arrays with OR on the driver; here every rank
+        flags its own partition on the device and the flags are combined with an
+        all-reduce (MAX on uint8 = OR; RCCL over xGMI on the GPU box), then each partition
+        is compacted locally.  Returns the new RDD; its index is self.index[active] when the
+        index is indexable, else the kept positions."""
+        import torch
+        p = Panel(self.data)
+        if not p.device:
+            raise TypeError("removeInstantsWithNaNs runs on device-resident partitions (torch GPU tensors)")
+        lib = _native.lib()
+        flags = torch.zeros((p.T,), dtype=torch.uint8, device=p.t.device)
+        check(lib.sts_nan_instants(ptr(p.t), p.S, p.T, p.ld, ptr(flags), p.stream), "removeInstantsWithNaNs")
+        flags = all_reduce_nan_flags(flags, group)
+        active = torch.empty((max(p.T, 1),), dtype=torch.int64, device=p.t.device)
+        n_dev = torch.zeros((1,), dtype=torch.int64, device=p.t.device)
+        check(lib.sts_active_instants(ptr(flags), p.T, ptr(active), ptr(n_dev), p.stream), "active_instants")
+        n = int(n_dev.item())
+        out = torch.empty((p.S, n), dtype=torch.float64, device=p.t.device)
+        check(lib.sts_gather_instants(ptr(p.t), ptr(out), p.S, p.ld, n, ptr(active), n, p.stream), "gather_instants")
+        kept = active[:n]
+        index = self.index
+        if index is not None:
+            try:
+                index = index[kept.cpu().numpy()]
+            except (TypeError, IndexError, KeyError):
+                index = kept.cpu().numpy()
+        else:
+            index = kept.cpu().numpy()
+        return TimeSeriesRDD(index, self.keys, p.out(out))
+
+    # --- S/TimeSeriesRDD.scala:215-324 ---
+    def toInstants(self, group=None):
+        """One record per instant with every series' value, series in key (partition)
+        order, instants in time order.  Locally a transpose kernel; across ranks the
+        instants are re-partitioned by time with an all-to-all (RCCL over xGMI), so rank r
+        returns instants [t0_r, t1_r) (shard_range over T) of ALL series -- Spark's
+        toInstants shuffle.  Returns (index slice, (T_r, S_total) tensor)."""
+        import torch
+        p = Panel(self.data)
+        if not p.device:
+            raise TypeError("toInstants runs on device-resident partitions (torch GPU tensors)")
+        inst = torch.empty((p.T, p.S), dtype=torch.float64, device=p.t.device)
+        check(_native.lib().sts_to_instants(ptr(p.t), ptr(inst), p.S, p.T, p.ld, p.S, p.stream), "toInstants")
+        got, (t0, t1) = exchange_instants(inst, group)
+        index = self.index
+        if index is not None:
+            try:
+                index = index[t0:t1]
+            except (TypeError, IndexError, KeyError):
+                index = None
+        return index, got
+
     def collectAsTimeSeries(self):
         """(index, keys, (T, S) column-major matrix) like S/TimeSeriesRDD.scala:62-74."""
         d = self.data.cpu().numpy() if hasattr(self.data, "cpu") else self.data
@@ -68,6 +135,81 @@ class TimeSeriesRDD:
 
     def count(self) -> int:
         return int(self.data.shape[0])
+
+
+class StatCounters:
+    """Per-series org.apache.spark.util.StatCounter values of a partition: count n (= T),
+    mean, m2 from the device pass; the derived statistics follow StatCounter's own formulas."""
+
+    def __init__(self, n: int, stats):
+        self.n = n
+        self.stats = stats   # (S, 4): mean, m2, max, min
+
+    def count(self):
+        return self.n
+
+    def mean(self):
+        return self.stats[:, 0]
+
+    def sum(self):
+        return self.n * self.stats[:, 0]
+
+    def max(self):
+        return self.stats[:, 2]
+
+    def min(self):
+        return self.stats[:, 3]
+
+    def variance(self):
+        return self.stats[:, 1] / self.n if self.n else self.stats[:, 1] * float("nan")
+
+    def sampleVariance(self):
+        return self.stats[:, 1] / (self.n - 1) if self.n > 1 else self.stats[:, 1] * float("nan")
+
+    def stdev(self):
+        return self.variance() ** 0.5
+
+    def sampleStdev(self):
+        return self.sampleVariance() ** 0.5
+
+
+def all_reduce_nan_flags(flags, group=None):
+    """OR the per-instant NaN flags (uint8) of every partition: all-reduce MAX (RCCL has
+    no bitwise OR; MAX on 0/1 bytes is the same).  The reference's
+    aggregate(zero)(merge, comb) (S/TimeSeriesRDD.scala:132-144)."""
+    import torch.distributed as dist
+    if dist.is_available() and dist.is_initialized():
+        dist.all_reduce(flags, op=dist.ReduceOp.MAX, group=group)
+    return flags
+
+
+def exchange_instants(local, group=None):
+    """Re-partition instant-major data by time: `local` is this rank's (T, S_r) block
+    (every instant, this partition's series).  Returns ((T_r, S_total) for instants
+    [t0, t1) = shard_range(T, rank, world), (t0, t1)); one all-to-all."""
+    import torch
+    import torch.distributed as dist
+    T, S_r = int(local.shape[0]), int(local.shape[1])
+    if not (dist.is_available() and dist.is_initialized()):
+        return local, (0, T)
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    n = torch.tensor([S_r], device=local.device, dtype=torch.int64)
+    sizes = [torch.zeros_like(n) for _ in range(world)]
+    dist.all_gather(sizes, n, group=group)
+    s_all = [int(x.item()) for x in sizes]
+    bounds = [shard_range(T, q, world) for q in range(world)]
+    send = local.contiguous().reshape(-1)            # rows [t0_q, t1_q) are contiguous
+    in_split = [(b - a) * S_r for a, b in bounds]
+    t0, t1 = bounds[rank]
+    out_split = [(t1 - t0) * s for s in s_all]
+    recv = local.new_empty((sum(out_split),))
+    dist.all_to_all_single(recv, send, out_split, in_split, group=group)
+    blocks, off = [], 0
+    for s, m in zip(s_all, out_split):
+        blocks.append(recv[off: off + m].reshape(t1 - t0, s))
+        off += m
+    return torch.cat(blocks, dim=1), (t0, t1)
 
 
 def all_gather_results(local, group=None):

@@ -13,7 +13,7 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from sparkts.timeseriesrdd import all_gather_results, shard_range
+from sparkts.timeseriesrdd import all_gather_results, all_reduce_nan_flags, exchange_instants, shard_range
 
 
 def test_shard_range_covers_keys_in_order():
@@ -62,3 +62,46 @@ def test_all_gather_results_two_ranks(n):
         assert p.exitcode == 0
     want = [[float(i)] * 3 for i in range(n)]
     assert res[0] == want and res[1] == want
+
+
+def _worker_instants(rank, world, port, S, T, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    full = torch.arange(S * T, dtype=torch.float64).reshape(S, T)      # global panel, series-major
+    a, b = shard_range(S, rank, world)
+    # removeInstantsWithNaNs: rank r flags the instants its partition has NaN at
+    flags = torch.zeros(T, dtype=torch.uint8)
+    flags[(rank * 3) % T] = 1
+    flags = all_reduce_nan_flags(flags)
+    # toInstants: local transpose of the partition, then the all-to-all by time
+    got, (t0, t1) = exchange_instants(full[a:b].t().contiguous())
+    q.put((rank, flags.tolist(), (t0, t1), got.numpy().tolist()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("S,T", [(5, 4), (7, 9), (3, 1)])
+def test_instant_collectives_two_ranks(S, T):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_instants, args=(r, 2, port, S, T, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in procs:
+        r, flags, rng, got = q.get(timeout=120)
+        res[r] = (flags, rng, got)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    want_flags = [0] * T
+    for r in range(2):
+        want_flags[(r * 3) % T] = 1
+    full = torch.arange(S * T, dtype=torch.float64).reshape(S, T)
+    for r in range(2):
+        flags, (t0, t1), got = res[r]
+        assert flags == want_flags
+        assert (t0, t1) == shard_range(T, r, 2)
+        assert got == full.t()[t0:t1].tolist()

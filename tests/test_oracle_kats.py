@@ -292,3 +292,33 @@ def test_generator_deterministic_and_nan_rate():
     assert same(a[2:], c)
     v = a[~np.isnan(a)]
     assert v.min() > 99.0 and v.max() < 112.0
+
+
+# ---- T/TimeSeriesRDDSuite.scala:210-231 (removeInstantsWithNaNs), :71-89 (toInstants) ----
+
+def test_remove_instants_with_nans_kat():
+    x = np.array([[1.0, 2.0, 3.0, 4.0], [5.0, np.nan, 7.0, 8.0], [9.0, 10.0, 11.0, np.nan]])
+    out, active = oracle.remove_instants_with_nans(x)
+    assert active.tolist() == [0, 2]          # index irregular(2015-4-9, 2015-4-11)
+    assert same(out, [[1.0, 3.0], [5.0, 7.0], [9.0, 11.0]])
+
+
+def test_to_instants_kat():
+    series = np.array([np.arange(x, x + 4, dtype=np.float64) for x in range(0, 20, 4)])   # a..e
+    inst = oracle.to_instants(series)
+    for t in range(4):
+        assert same(inst[t], np.arange(t, 20, 4, dtype=np.float64))
+
+
+def test_stat_counter():
+    # Spark StatCounter: count 4, mean 2.5, variance m2 / n = 1.25
+    n, mu, m2, mx, mn = oracle.stat_counter([1.0, 2.0, 3.0, 4.0])
+    assert (n, mu, m2 / n, mx, mn) == (4, 2.5, 1.25, 4.0, 1.0)
+    # NaN propagates through mean, m2, max and min (java.lang.Math.max / min)
+    _, mu, m2, mx, mn = oracle.stat_counter([1.0, np.nan, 3.0])
+    assert all(math.isnan(v) for v in (mu, m2, mx, mn))
+    # signed zeros: max(-0.0, 0.0) = 0.0, min(0.0, -0.0) = -0.0
+    _, _, _, mx, mn = oracle.stat_counter([-0.0, 0.0])
+    assert mx == 0.0 and not math.copysign(1.0, mx) < 0 and math.copysign(1.0, mn) < 0
+    _, mu, m2, mx, mn = oracle.stat_counter([])
+    assert (mu, m2, mx, mn) == (0.0, 0.0, -math.inf, math.inf)

@@ -622,3 +622,63 @@ def test_generator_matches_cpu(torch):
     phi = torch.empty((S, 5), dtype=torch.float64, device="cuda:0")
     assert lib.sts_gen_ar_panel(out.data_ptr(), c.data_ptr(), phi.data_ptr(), 5, S, T, T, 77, 5, None) == 0
     assert_bits(host(out), oracle.gen_ar_panel(77, S, T, 5, s0=5))
+
+
+# ---------------- seriesStats / removeInstantsWithNaNs / toInstants ----------------
+
+def test_series_stats(torch):
+    from sparkts.timeseriesrdd import TimeSeriesRDD
+    rng = np.random.default_rng(21)
+    for S, T in [(1, 1), (3, 2), (33, 64), (70, 390), (5, 5000)]:
+        x = rng.standard_normal((S, T)) * 10 + 3
+        if S > 2:
+            x[1, T // 2] = NaN
+            x[2, :] = -0.0
+            x[2, 0] = 0.0
+        if S > 10 and T > 3:
+            x[7, 1] = np.inf
+            x[8, 2] = -np.inf
+        st = TimeSeriesRDD(None, None, dev(torch, x)).seriesStats()
+        ref = np.array([oracle.stat_counter(r)[1:] for r in x])
+        assert st.count() == T
+        assert_bits(host(st.mean()), ref[:, 0], "mean")
+        assert_bits(host(st.stats[:, 1]), ref[:, 1], "m2")
+        assert_bits(host(st.max()), ref[:, 2], "max")
+        assert_bits(host(st.min()), ref[:, 3], "min")
+
+
+def test_remove_instants_with_nans_kat(torch):
+    # T/TimeSeriesRDDSuite.scala:210-231
+    from sparkts.timeseriesrdd import TimeSeriesRDD
+    x = np.array([[1.0, 2.0, 3.0, 4.0], [5.0, NaN, 7.0, 8.0], [9.0, 10.0, 11.0, NaN]])
+    idx = np.array(["2015-04-09", "2015-04-10", "2015-04-11", "2015-04-12"])
+    r = TimeSeriesRDD(idx, ["1.0", "5.0", "9.0"], dev(torch, x)).removeInstantsWithNaNs()
+    assert list(r.index) == ["2015-04-09", "2015-04-11"]
+    assert_bits(host(r.data), np.array([[1.0, 3.0], [5.0, 7.0], [9.0, 11.0]]), "kat")
+
+
+@pytest.mark.parametrize("S,T,p", [(1, 1, 0.0), (5, 100, 0.01), (64, 5000, 0.0005), (300, 20000, 0.00005),
+                                   (4, 9000, 1.0)])
+def test_remove_instants_with_nans_panels(torch, S, T, p):
+    from sparkts.timeseriesrdd import TimeSeriesRDD
+    rng = np.random.default_rng(S * 7 + T)
+    x = rng.standard_normal((S, T))
+    x[rng.random((S, T)) < p] = NaN
+    r = TimeSeriesRDD(None, None, dev(torch, x)).removeInstantsWithNaNs()
+    ref, active = oracle.remove_instants_with_nans(x)
+    assert np.array_equal(r.index, active)
+    assert_bits(host(r.data).reshape(ref.shape), ref, "removeInstantsWithNaNs")
+
+
+def test_to_instants(torch):
+    # T/TimeSeriesRDDSuite.scala:71-89
+    from sparkts.timeseriesrdd import TimeSeriesRDD
+    series = np.array([np.arange(v, v + 4, dtype=np.float64) for v in range(0, 20, 4)])
+    _, inst = TimeSeriesRDD(None, list("abcde"), dev(torch, series)).toInstants()
+    for t in range(4):
+        assert_bits(host(inst[t]), np.arange(t, 20, 4, dtype=np.float64), "kat")
+    rng = np.random.default_rng(5)
+    for S, T in [(1, 7), (65, 63), (130, 1000), (3, 70000)]:
+        x = rng.standard_normal((S, T))
+        _, inst = TimeSeriesRDD(None, None, dev(torch, x)).toInstants()
+        assert_bits(host(inst), oracle.to_instants(x), "toInstants %dx%d" % (S, T))
