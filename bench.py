@@ -38,6 +38,12 @@ WORKLOADS = {
     "ewma_fit": (1_000_000, 390, 0.0, 6,
                  "EWMA.fitModel (SURVEY.md 8(f) rank 1): commons-math3 NLCG + bracket + Brent per series, "
                  "1,000,000 series x 390 steps (the C2 shape)"),
+    "stats": (1_000_000, 390, 0.0, 7, "TimeSeriesRDD.seriesStats (Spark StatCounter per series), "
+              "1,000,000 series x 390 steps (the C2 shape)"),
+    "nan_instants": (1_000_000, 390, 0.0, 8,
+                     "TimeSeriesRDD.removeInstantsWithNaNs, 1,000,000 series x 390 steps with NaNs at 39 "
+                     "instants (flags + compaction + gather)"),
+    "to_instants": (1_000_000, 390, 0.0, 9, "TimeSeriesRDD.toInstants local transpose, 1,000,000 series x 390 steps"),
     "c5": (1_250, 10_000_000, 0.30, 5,
            "C5 shard: fill('nearest') + lag(10, false), 1,250 series x 10,000,000 steps per GPU (N=8 -> C5's "
            "10k x 10M); lag matrices written into a reused scratch slab, 10 series per call"),
@@ -102,6 +108,16 @@ def main():
     smooth = torch.full((S,), 0.2, dtype=torch.float64, device=dev)
     if args.workload == "ewma_fit":
         smooth = torch.empty((S,), dtype=torch.float64, device=dev)
+    if args.workload == "stats":
+        stats = torch.empty((S, 4), dtype=torch.float64, device=dev)
+    if args.workload == "nan_instants":
+        x[::997, ::10] = float("nan")              # every 10th instant has a NaN somewhere
+        flags = torch.zeros(T, dtype=torch.uint8, device=dev)
+        active = torch.empty(T, dtype=torch.int64, device=dev)
+        n_act = torch.zeros(1, dtype=torch.int64, device=dev)
+        n_keep = T - len(range(0, T, 10))
+    if args.workload == "to_instants":
+        inst = torch.empty((T, S), dtype=torch.float64, device=dev)
     if args.workload == "c5":
         P, LB = 10, 10            # lag(10, includeOriginal = false); series per call
         lagbuf = torch.empty((LB, P, T - P), dtype=torch.float64, device=dev)
@@ -122,6 +138,20 @@ def main():
                 raise_for_status(lib.sts_fill_lag_matrix(x[b0].data_ptr(), out[b0].data_ptr(), lagbuf.data_ptr(), nb,
                                                          T, T, T, 1, P, 0, err[b0:].data_ptr(), sp),
                                  "fill_lag_matrix")
+        elif args.workload == "stats":
+            raise_for_status(lib.sts_series_stats(x.data_ptr(), S, T, T, stats.data_ptr(), sp), "seriesStats")
+        elif args.workload == "nan_instants":
+            flags.zero_()
+            raise_for_status(lib.sts_nan_instants(x.data_ptr(), S, T, T, flags.data_ptr(), sp), "nan_instants")
+            if world > 1:
+                dist.all_reduce(flags, op=dist.ReduceOp.MAX)
+            raise_for_status(lib.sts_active_instants(flags.data_ptr(), T, active.data_ptr(), n_act.data_ptr(), sp),
+                             "active_instants")
+            # the kept count is known to the driver after one sync; the bench reuses it
+            raise_for_status(lib.sts_gather_instants(x.data_ptr(), out.data_ptr(), S, T, n_keep, active.data_ptr(),
+                                                     n_keep, sp), "gather_instants")
+        elif args.workload == "to_instants":
+            raise_for_status(lib.sts_to_instants(x.data_ptr(), inst.data_ptr(), S, T, T, S, sp), "toInstants")
         elif args.workload == "ewma_fit":
             raise_for_status(lib.sts_ewma_fit(x.data_ptr(), S, T, T, smooth.data_ptr(), err.data_ptr(), sp),
                              "EWMA.fitModel")
@@ -172,11 +202,18 @@ def main():
         bytes_per_step += 8.0 * P * (T - P) * S
     if args.workload == "ewma_fit":      # the series read once + one parameter written (algorithmic)
         bytes_per_step = 8.0 * S * T + 8.0 * S
+    if args.workload == "stats":         # read once + 4 doubles per series
+        bytes_per_step = 8.0 * S * T + 32.0 * S
+    if args.workload == "nan_instants":  # flag pass reads everything; the gather reads + writes kept values
+        bytes_per_step = 8.0 * S * T + 16.0 * S * n_keep
     kernel = {"c3": "sts::tile_kernel<4096,4,shifted> (fill linear + ACF partials, FP64 MFMA)",
               "c1": "sts::seg_kernel<2> (wave-private series segments: fill linear + ACF partials, FP64 MFMA)",
               "c5": "sts::tile_kernel<4096,0> (fill nearest + lag-matrix columns)",
               "c2": "sts::recur_kernel<kFillDiffEwma> (fillPrevious -> differencesAtLag(1) -> EWMA add, lane per series)",
               "c4": "sts::ar_fit_kernel (AR(5) Gram on FP64 MFMA + solve + fused remove)",
+              "stats": "sts::stats_kernel<64,32> (StatCounter.merge per lane, LDS-staged series block)",
+              "nan_instants": "sts::nan_instants_kernel + sts::gather_instants_kernel",
+              "to_instants": "sts::transpose_kernel (64x64 LDS tiles)",
               "ewma_fit": "sts::ewma_fit_kernel<32,64> (lane-per-series commons-math3 optimizer; one sse+gradient "
                           "pass over the wave's series block per optimizer request)"}[args.workload]
     roofline = None
@@ -204,7 +241,8 @@ def main():
             "config": {"workload": desc, "series_per_gpu": S, "steps_per_series": T,
                        "numLags": K if args.workload in ("c3", "c1") else None,
                        "fill": {"c3": "linear", "c1": "linear", "c2": "previous", "c4": None, "c5": "nearest",
-                                "ewma_fit": None}[args.workload],
+                                "ewma_fit": None, "stats": None, "nan_instants": None,
+                                "to_instants": None}[args.workload],
                        "parallelism": "dp%d (series sharded by key, one process per GPU)" % world},
             "roofline": roofline,
             "cpu_baseline": cpu,
@@ -238,6 +276,8 @@ def cpu_baseline(args, S, T, K, seed, nan_p, out, acf, p_ar, smooth=None):
     import oracle
     threads = max(1, min(16, os.cpu_count() or 1))
     per_round = threads
+    if args.workload in ("stats", "nan_instants", "to_instants"):
+        threads, per_round = 1, 4096     # single-threaded restatements (one partition)
     done, elapsed, s_next = 0, 0.0, 0
     worst_rel, exact = 0.0, True
     while elapsed < args.cpu_seconds and s_next < S:
@@ -258,10 +298,19 @@ def cpu_baseline(args, S, T, K, seed, nan_p, out, acf, p_ar, smooth=None):
                 oracle.lag(r, 10, False)
         elif args.workload == "ewma_fit":
             rf, _ = oracle.panel_ewma_fit(xs, threads=threads)
+        elif args.workload in ("stats", "nan_instants", "to_instants"):
+            rf = None
+            if args.workload == "stats":
+                for r in xs:
+                    oracle.stat_counter(r)
+            elif args.workload == "nan_instants":
+                oracle.remove_instants_with_nans(xs)
+            else:
+                oracle.to_instants(xs)
         else:
             rf, _, _ = oracle.panel_ar_fit_remove(xs, p_ar, threads=threads)
         elapsed += time.perf_counter() - t0
-        if s_next == 0:
+        if s_next == 0 and rf is not None:
             g = (smooth[:n] if args.workload == "ewma_fit" else out[:n]).cpu().numpy()
             if args.workload != "c4":
                 exact = bool(np.array_equal(np.isnan(g), np.isnan(rf)) and

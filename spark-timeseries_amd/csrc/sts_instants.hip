@@ -195,7 +195,7 @@ __global__ __launch_bounds__(256) void transpose_kernel(const double* __restrict
 
 hipError_t launch_series_stats(const double* in, double* out, int64_t S, int64_t T, int64_t ld, hipStream_t st) {
     if (S <= 0) return hipSuccess;
-    constexpr int SPW = 32, CH = 64;
+    constexpr int SPW = 64, CH = 32;   // A/B on 1M x 390: 1.00 ms vs 1.44 (32 x 64), 1.96 (16 x 64)
     hipLaunchKernelGGL((stats_kernel<SPW, CH>), dim3((unsigned)((S + SPW - 1) / SPW)), dim3(64), 0, st, in, out, S, T,
                        ld);
     return hipGetLastError();
