@@ -39,6 +39,8 @@ void throw_for(JNIEnv* env, int status) {
     case STS_ERR_NULL_DEST: cls = "java/lang/NullPointerException"; break;
     case STS_ERR_NOT_ENOUGH_DATA: cls = "org/apache/commons/math3/exception/MathIllegalArgumentException"; break;
     case STS_ERR_SINGULAR: cls = "org/apache/commons/math3/linear/SingularMatrixException"; break;
+    case STS_ERR_TOO_MANY_EVALUATIONS: cls = "org/apache/commons/math3/exception/TooManyEvaluationsException"; break;
+    case STS_ERR_TOO_MANY_ITERATIONS: cls = "org/apache/commons/math3/exception/TooManyIterationsException"; break;
     default: break;
     }
     jclass c = env->FindClass(cls);
@@ -124,6 +126,17 @@ JNIEXPORT void JNICALL Java_com_cloudera_sparkts_StsNative_ewma(JNIEnv* env, jcl
 }
 
 // Autoregression.fitModel(ts, maxLag, noIntercept) (S/models/Autoregression.scala:38-53)
+// EWMA.fitModel over a partition panel (S/models/EWMA.scala:44-68)
+JNIEXPORT void JNICALL Java_com_cloudera_sparkts_StsNative_ewmaFit(JNIEnv* env, jclass, jdoubleArray in, jlong S,
+                                                                    jlong T, jdoubleArray smoothing) {
+    int st;
+    {
+        Pinned pi(env, in), ps(env, smoothing);
+        st = sts_ewma_fit_host(pi.d(), S, T, T, ps.d(), nullptr);
+    }
+    throw_for(env, st);
+}
+
 JNIEXPORT void JNICALL Java_com_cloudera_sparkts_StsNative_arFit(JNIEnv* env, jclass, jdoubleArray in, jlong S,
                                                                   jlong T, jint p, jboolean noIntercept,
                                                                   jdoubleArray c, jdoubleArray coef) {
