@@ -44,6 +44,9 @@ WORKLOADS = {
                      "TimeSeriesRDD.removeInstantsWithNaNs, 1,000,000 series x 390 steps with NaNs at 39 "
                      "instants (flags + compaction + gather)"),
     "to_instants": (1_000_000, 390, 0.0, 9, "TimeSeriesRDD.toInstants local transpose, 1,000,000 series x 390 steps"),
+    "wire_decode": (1_000_000, 390, 0.05, 10,
+                    "Python wire format -> HBM panel (S/PythonConnector.scala:47-90): byte-swap decode of "
+                    "1,000,000 records x 390 doubles already staged in HBM"),
     "c5": (1_250, 10_000_000, 0.30, 5,
            "C5 shard: fill('nearest') + lag(10, false), 1,250 series x 10,000,000 steps per GPU (N=8 -> C5's "
            "10k x 10M); lag matrices written into a reused scratch slab, 10 series per call"),
@@ -118,6 +121,12 @@ def main():
         n_keep = T - len(range(0, T, 10))
     if args.workload == "to_instants":
         inst = torch.empty((T, S), dtype=torch.float64, device=dev)
+    if args.workload == "wire_decode":   # records "k%07d": 16-B headers, 8-B aligned value blocks
+        rec = 16 + 8 * T
+        val_off = (torch.arange(S, dtype=torch.int64, device=dev) * rec + 16).contiguous()
+        wire = torch.zeros(S * rec, dtype=torch.uint8, device=dev)
+        raise_for_status(lib.sts_wire_encode(x.data_ptr(), S, T, T, val_off.data_ptr(), wire.data_ptr(), sp),
+                         "wire_encode")
     if args.workload == "c5":
         P, LB = 10, 10            # lag(10, includeOriginal = false); series per call
         lagbuf = torch.empty((LB, P, T - P), dtype=torch.float64, device=dev)
@@ -150,6 +159,9 @@ def main():
             # the kept count is known to the driver after one sync; the bench reuses it
             raise_for_status(lib.sts_gather_instants(x.data_ptr(), out.data_ptr(), S, T, n_keep, active.data_ptr(),
                                                      n_keep, sp), "gather_instants")
+        elif args.workload == "wire_decode":
+            raise_for_status(lib.sts_wire_decode(wire.data_ptr(), val_off.data_ptr(), S, T, out.data_ptr(), T, sp),
+                             "wire_decode")
         elif args.workload == "to_instants":
             raise_for_status(lib.sts_to_instants(x.data_ptr(), inst.data_ptr(), S, T, T, S, sp), "toInstants")
         elif args.workload == "ewma_fit":
@@ -214,6 +226,7 @@ def main():
               "stats": "sts::stats_kernel<64,32> (StatCounter.merge per lane, LDS-staged series block)",
               "nan_instants": "sts::nan_instants_kernel + sts::gather_instants_kernel",
               "to_instants": "sts::transpose_kernel (64x64 LDS tiles)",
+              "wire_decode": "sts::wire_decode_kernel (big-endian value blocks -> panel)",
               "ewma_fit": "sts::ewma_fit_kernel<32,64> (lane-per-series commons-math3 optimizer; one sse+gradient "
                           "pass over the wave's series block per optimizer request)"}[args.workload]
     roofline = None
@@ -242,7 +255,7 @@ def main():
                        "numLags": K if args.workload in ("c3", "c1") else None,
                        "fill": {"c3": "linear", "c1": "linear", "c2": "previous", "c4": None, "c5": "nearest",
                                 "ewma_fit": None, "stats": None, "nan_instants": None,
-                                "to_instants": None}[args.workload],
+                                "to_instants": None, "wire_decode": None}[args.workload],
                        "parallelism": "dp%d (series sharded by key, one process per GPU)" % world},
             "roofline": roofline,
             "cpu_baseline": cpu,
@@ -276,7 +289,7 @@ def cpu_baseline(args, S, T, K, seed, nan_p, out, acf, p_ar, smooth=None):
     import oracle
     threads = max(1, min(16, os.cpu_count() or 1))
     per_round = threads
-    if args.workload in ("stats", "nan_instants", "to_instants"):
+    if args.workload in ("stats", "nan_instants", "to_instants", "wire_decode"):
         threads, per_round = 1, 4096     # single-threaded restatements (one partition)
     done, elapsed, s_next = 0, 0.0, 0
     worst_rel, exact = 0.0, True
@@ -286,6 +299,8 @@ def cpu_baseline(args, S, T, K, seed, nan_p, out, acf, p_ar, smooth=None):
             xs = oracle.gen_ar_panel(seed, n, T, p_ar, s0=s_next)
         else:
             xs = oracle.gen_panel(seed, n, T, nan_p, s0=s_next)
+        if args.workload == "wire_decode":
+            wire_bytes = oracle.wire_records(["k%07d" % i for i in range(n)], xs)
         t0 = time.perf_counter()
         if args.workload in ("c3", "c1"):
             rf, racf, _ = oracle.panel_fill_autocorr(xs, "linear", K, threads=threads)
@@ -298,15 +313,22 @@ def cpu_baseline(args, S, T, K, seed, nan_p, out, acf, p_ar, smooth=None):
                 oracle.lag(r, 10, False)
         elif args.workload == "ewma_fit":
             rf, _ = oracle.panel_ewma_fit(xs, threads=threads)
-        elif args.workload in ("stats", "nan_instants", "to_instants"):
+        elif args.workload in ("stats", "nan_instants", "to_instants", "wire_decode"):
             rf = None
             if args.workload == "stats":
                 for r in xs:
                     oracle.stat_counter(r)
             elif args.workload == "nan_instants":
                 oracle.remove_instants_with_nans(xs)
-            else:
+            elif args.workload == "to_instants":
                 oracle.to_instants(xs)
+            else:   # BytesToKeyAndSeries per record: header walk + big-endian doubles
+                pos = 0
+                for _ in range(n):
+                    kl = int.from_bytes(wire_bytes[pos: pos + 4], "big")
+                    vn = int.from_bytes(wire_bytes[pos + 4 + kl: pos + 8 + kl], "big")
+                    np.frombuffer(wire_bytes, dtype=">f8", count=vn, offset=pos + 8 + kl).astype(np.float64)
+                    pos += 8 + kl + 8 * vn
         else:
             rf, _, _ = oracle.panel_ar_fit_remove(xs, p_ar, threads=threads)
         elapsed += time.perf_counter() - t0

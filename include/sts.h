@@ -176,6 +176,42 @@ int sts_gather_instants(const double* in, double* out, int64_t S, int64_t ld_in,
 int sts_to_instants(const double* in, double* out, int64_t S, int64_t T, int64_t ld_in,
                     int64_t ld_out, void* stream);
 
+/* ---- f5: ingest / egress formats -- the step before the hot path (staging a partition
+ * into the HBM panel) and the way back.
+ *
+ * Python wire format (S/PythonConnector.scala:47-90 BytesToKeyAndSeries / KeyAndSeriesToBytes,
+ * python/sparkts/timeseriesrdd.py:239-290): a record is int32 BE keyLen | keyLen UTF-8 bytes |
+ * int32 BE n | n x float64 BE; `bytes` holds records back to back.
+ *   sts_wire_scan (HOST memory, no device): walks the headers; fills key_off / key_len /
+ *     val_off (byte offsets) for up to max_records records, *n_records and *T.  Every record
+ *     must hold the same n (one shared index): otherwise STS_ERR_BAD_ARG, as is a truncated
+ *     or overrunning record.
+ *   sts_wire_decode (device): panel[s*ld + t] = the BE double at bytes[val_off[s] + 8t].
+ *   sts_wire_encode (device): the inverse, value blocks only (headers are the caller's).
+ * Bit-exact (byte permutations). */
+int sts_wire_scan(const uint8_t* bytes, int64_t nbytes, int64_t max_records, int64_t* n_records,
+                  int64_t* T, int64_t* key_off, int32_t* key_len, int64_t* val_off);
+int sts_wire_decode(const uint8_t* bytes, const int64_t* val_off, int64_t S, int64_t T,
+                    double* panel, int64_t ld, void* stream);
+int sts_wire_encode(const double* panel, int64_t S, int64_t T, int64_t ld, const int64_t* val_off,
+                    uint8_t* bytes, void* stream);
+/* timeSeriesRDDFromObservations (S/TimeSeriesRDD.scala:493-542): panel (S x T, ld) = NaN, then
+ * observation i writes value[i] at (series_id[i], loc[i]) -- loc = targetIndex.locAtDateTime
+ * of its timestamp, negative = not in the index (dropped, :529-535).  Among observations of
+ * one cell the LAST in input order wins (the reference keeps the last in its (key, time) sort
+ * order).  Device arrays. */
+int sts_observations_to_panel(const int32_t* series_id, const int64_t* loc, const double* value,
+                              int64_t n_obs, double* panel, int64_t S, int64_t T, int64_t ld,
+                              void* stream);
+/* timeSeriesRDDFromCsv (S/TimeSeriesRDD.scala:547-561), the per-line parse
+ * `key,v1,...,vn` (HOST memory): up to max_records lines of `text`; values go row-major into
+ * `values` (capacity values_cap doubles, ld = T), keys as (key_off, key_len) into text.
+ * Numbers parse as java.lang.Double.parseDouble does for decimal / NaN / Infinity tokens.
+ * Every line must hold the same number of values. */
+int sts_csv_parse(const char* text, int64_t len, int64_t max_records, int64_t* n_records,
+                  int64_t* T, int64_t* key_off, int32_t* key_len, double* values,
+                  int64_t values_cap);
+
 /* ---- a11: Autoregression.fitModel(ts, p, noIntercept) (S/models/Autoregression.scala:38-53).
  * c[s] and coef[s*p + j] receive the model; 1 <= p <= 31.  T - p < p + 1 ->
  * STS_ERR_NOT_ENOUGH_DATA.  1e-10 relative to a Householder-QR OLS. */

@@ -231,6 +231,36 @@ def to_instants(x):
     out = np.empty((T, S)); lib().orc_to_instants(_p(x), S, T, T, _p(out)); return out
 
 
+def observations_to_panel(target_index, keys, timestamps, values):
+    """S/TimeSeriesRDD.scala:493-542 restated in Python (small cases): sort observations by
+    (key, timestamp) -- a stable sort, so equal (key, timestamp) pairs keep input order --
+    then per key a NaN series with series(locAtDateTime(ts)) = value for every sample whose
+    timestamp is in the index.  Returns (sorted keys, (S, T) panel)."""
+    idx = {int(t): i for i, t in enumerate(target_index)}
+    obs = sorted(range(len(keys)), key=lambda i: (keys[i], int(timestamps[i])))
+    out = {}
+    for i in obs:
+        row = out.setdefault(keys[i], np.full(len(target_index), np.nan))
+        loc = idx.get(int(timestamps[i]), -1)
+        if loc >= 0:
+            row[loc] = values[i]
+    ks = sorted(out)
+    return ks, np.array([out[k] for k in ks]).reshape(len(ks), len(target_index))
+
+
+def wire_records(keys, panel) -> bytes:
+    """KeyAndSeriesToBytes / python _TimeSeriesSerializer.dumps (python/sparkts/timeseriesrdd.py:
+    244-256): int32 BE keyLen, UTF-8 key, int32 BE n, n x '!d'."""
+    import struct
+    out = bytearray()
+    for k, row in zip(keys, panel):
+        kb = k.encode("utf-8")
+        out += struct.pack("!i", len(kb)) + kb + struct.pack("!i", len(row))
+        for v in row:
+            out += struct.pack("!d", v)
+    return bytes(out)
+
+
 # ---------------- panel drivers ----------------
 
 def _panel(x):

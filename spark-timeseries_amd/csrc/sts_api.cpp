@@ -587,6 +587,157 @@ int sts_to_instants(const double* in, double* out, int64_t S, int64_t T, int64_t
     return STS_OK;
 }
 
+static inline int64_t be32(const uint8_t* p) {
+    return (int64_t)(int32_t)(((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | (uint32_t)p[3]);
+}
+
+int sts_wire_scan(const uint8_t* bytes, int64_t nbytes, int64_t max_records, int64_t* n_records, int64_t* T,
+                  int64_t* key_off, int32_t* key_len, int64_t* val_off) {
+    if (!n_records || !T || nbytes < 0 || (nbytes > 0 && !bytes)) return fail(STS_ERR_BAD_ARG, "wire_scan: bad arguments");
+    int64_t pos = 0, n = 0, len = -1;
+    while (pos < nbytes) {
+        if (pos + 4 > nbytes) return fail(STS_ERR_BAD_ARG, "wire_scan: truncated key length at byte %lld", (long long)pos);
+        const int64_t kl = be32(bytes + pos);
+        if (kl < 0 || pos + 4 + kl + 4 > nbytes)
+            return fail(STS_ERR_BAD_ARG, "wire_scan: bad key length %lld at byte %lld", (long long)kl, (long long)pos);
+        const int64_t vn = be32(bytes + pos + 4 + kl);
+        if (vn < 0 || pos + 8 + kl + 8 * vn > nbytes)
+            return fail(STS_ERR_BAD_ARG, "wire_scan: bad series length %lld at byte %lld", (long long)vn, (long long)pos);
+        if (len >= 0 && vn != len)
+            return fail(STS_ERR_BAD_ARG, "wire_scan: record %lld holds %lld values, record 0 holds %lld (one shared index)",
+                        (long long)n, (long long)vn, (long long)len);
+        len = vn;
+        if (n < max_records) {
+            if (key_off) key_off[n] = pos + 4;
+            if (key_len) key_len[n] = (int32_t)kl;
+            if (val_off) val_off[n] = pos + 8 + kl;
+        }
+        n++;
+        pos += 8 + kl + 8 * vn;
+    }
+    *n_records = n;
+    *T = len < 0 ? 0 : len;
+    return n > max_records ? fail(STS_ERR_BAD_ARG, "wire_scan: %lld records > capacity %lld", (long long)n,
+                                  (long long)max_records)
+                           : STS_OK;
+}
+
+int sts_wire_decode(const uint8_t* bytes, const int64_t* val_off, int64_t S, int64_t T, double* panel, int64_t ld,
+                    void* stream) {
+    int r;
+    if ((r = check_panel(panel, S, T, ld, "wire_decode"))) return r;
+    if (S * T > 0 && (!bytes || !val_off)) return fail(STS_ERR_BAD_ARG, "wire_decode: null pointer");
+    if (S * T == 0) return STS_OK;
+    if ((r = ensure_device())) return r;
+    hipStream_t st = as_stream(stream);
+    HIP_TRY(timed(st, [&] { return sts::launch_wire_decode(bytes, val_off, panel, S, T, ld, st); }), "wire_decode");
+    return STS_OK;
+}
+
+int sts_wire_encode(const double* panel, int64_t S, int64_t T, int64_t ld, const int64_t* val_off, uint8_t* bytes,
+                    void* stream) {
+    int r;
+    if ((r = check_panel(panel, S, T, ld, "wire_encode"))) return r;
+    if (S * T > 0 && (!bytes || !val_off)) return fail(STS_ERR_BAD_ARG, "wire_encode: null pointer");
+    if (S * T == 0) return STS_OK;
+    if ((r = ensure_device())) return r;
+    hipStream_t st = as_stream(stream);
+    HIP_TRY(timed(st, [&] { return sts::launch_wire_encode(panel, S, T, ld, val_off, bytes, st); }), "wire_encode");
+    return STS_OK;
+}
+
+int sts_observations_to_panel(const int32_t* series_id, const int64_t* loc, const double* value, int64_t n_obs,
+                              double* panel, int64_t S, int64_t T, int64_t ld, void* stream) {
+    int r;
+    if ((r = check_panel(panel, S, T, ld, "timeSeriesRDDFromObservations"))) return r;
+    if (n_obs < 0 || (n_obs > 0 && (!series_id || !loc || !value)))
+        return fail(STS_ERR_BAD_ARG, "timeSeriesRDDFromObservations: bad observation arrays");
+    if (S * T == 0) return STS_OK;
+    if ((r = ensure_device())) return r;
+    hipStream_t st = as_stream(stream);
+    Scratch win(st);
+    HIP_TRY(win.alloc((size_t)(n_obs > 0 ? n_obs : 1)), "hipMallocAsync(obs flags)");
+    HIP_TRY(timed(st, [&] {
+                return sts::launch_observations(series_id, loc, value, n_obs, panel, S, T, ld,
+                                                static_cast<unsigned char*>(win.p), st);
+            }),
+            "timeSeriesRDDFromObservations");
+    return STS_OK;
+}
+
+// java.lang.Double.parseDouble for the tokens Double.toString writes (decimal, optional
+// exponent, NaN, Infinity, -Infinity); surrounding whitespace is trimmed like Java's.
+static bool parse_java_double(const char* b, const char* e, double* out) {
+    while (b < e && (unsigned char)*b <= ' ') b++;
+    while (e > b && (unsigned char)e[-1] <= ' ') e--;
+    const size_t n = (size_t)(e - b);
+    if (n == 0 || n > 400) return false;
+    char buf[401];
+    std::memcpy(buf, b, n);
+    buf[n] = 0;
+    const char* q = buf;
+    const bool neg = (*q == '-'), sgn = (neg || *q == '+');
+    if (sgn) q++;
+    if (!std::strcmp(q, "NaN")) { *out = NAN; return true; }
+    if (!std::strcmp(q, "Infinity")) { *out = neg ? -INFINITY : INFINITY; return true; }
+    for (const char* c = q; *c; c++)   // decimal digits, '.', exponent (strtod would also take hex / "inf")
+        if (!((*c >= '0' && *c <= '9') || *c == '.' || *c == 'e' || *c == 'E' || *c == '+' || *c == '-' ||
+              *c == 'd' || *c == 'D' || *c == 'f' || *c == 'F'))
+            return false;
+    if (n > 0 && (buf[n - 1] == 'd' || buf[n - 1] == 'D' || buf[n - 1] == 'f' || buf[n - 1] == 'F')) buf[n - 1] = 0;
+    char* end = nullptr;
+    *out = std::strtod(buf, &end);   // correctly rounded (glibc), as parseDouble is
+    return end && *end == 0 && end != q;
+}
+
+int sts_csv_parse(const char* text, int64_t len, int64_t max_records, int64_t* n_records, int64_t* T,
+                  int64_t* key_off, int32_t* key_len, double* values, int64_t values_cap) {
+    if (!n_records || !T || len < 0 || (len > 0 && !text)) return fail(STS_ERR_BAD_ARG, "csv_parse: bad arguments");
+    int64_t pos = 0, n = 0, width = -1;
+    while (pos < len) {
+        int64_t eol = pos;
+        while (eol < len && text[eol] != '\n') eol++;
+        int64_t end = eol;
+        if (end > pos && text[end - 1] == '\r') end--;
+        if (end > pos) {   // sc.textFile skips nothing, but an empty trailing line is no record
+            int64_t c = pos;
+            while (c < end && text[c] != ',') c++;
+            int64_t cnt = 0;
+            int64_t f = c;
+            while (f < end) {   // tokens.tail
+                const int64_t g0 = f + 1;
+                int64_t g = g0;
+                while (g < end && text[g] != ',') g++;
+                double v;
+                if (!parse_java_double(text + g0, text + g, &v))
+                    return fail(STS_ERR_BAD_ARG, "csv_parse: NumberFormatException at line %lld: \"%.*s\"", (long long)n,
+                                (int)(g - g0 > 64 ? 64 : g - g0), text + g0);
+                if (n < max_records && values && width >= 0 && n * width + cnt < values_cap) values[n * width + cnt] = v;
+                else if (n < max_records && values && width < 0 && cnt < values_cap) values[cnt] = v;
+                cnt++;
+                f = g;
+            }
+            if (width >= 0 && cnt != width)
+                return fail(STS_ERR_BAD_ARG, "csv_parse: line %lld holds %lld values, line 0 holds %lld", (long long)n,
+                            (long long)cnt, (long long)width);
+            width = cnt;
+            if ((n + 1) * width > values_cap && values)
+                return fail(STS_ERR_BAD_ARG, "csv_parse: values capacity %lld exceeded", (long long)values_cap);
+            if (n < max_records) {
+                if (key_off) key_off[n] = pos;
+                if (key_len) key_len[n] = (int32_t)(c - pos);
+            }
+            n++;
+        }
+        pos = eol + 1;
+    }
+    *n_records = n;
+    *T = width < 0 ? 0 : width;
+    return n > max_records ? fail(STS_ERR_BAD_ARG, "csv_parse: %lld lines > capacity %lld", (long long)n,
+                                  (long long)max_records)
+                           : STS_OK;
+}
+
 int sts_fill_diff_ewma(const double* in, double* out, int64_t S, int64_t T, int64_t ld_in, int64_t ld_out, int method,
                        int lag, const double* smoothing, int32_t* err_per_series, void* stream) {
     int r;

@@ -114,6 +114,14 @@ hipError_t launch_gather_instants(const double* in, double* out, const int64_t* 
 hipError_t launch_transpose(const double* in, double* out, int64_t S, int64_t T, int64_t ld_in, int64_t ld_out,
                             hipStream_t st);
 
+// ingest formats (sts_ingest.hip)
+hipError_t launch_wire_decode(const unsigned char* bytes, const int64_t* val_off, double* panel, int64_t S, int64_t T,
+                              int64_t ld, hipStream_t st);
+hipError_t launch_wire_encode(const double* panel, int64_t S, int64_t T, int64_t ld, const int64_t* val_off,
+                              unsigned char* bytes, hipStream_t st);
+hipError_t launch_observations(const int32_t* sid, const int64_t* loc, const double* val, int64_t n, double* panel,
+                               int64_t S, int64_t T, int64_t ld, unsigned char* win, hipStream_t st);
+
 // generators (sts_gen.hip)
 hipError_t launch_gen_panel(double* out, int64_t s0, int64_t S, int64_t T, int64_t ld,
                             uint64_t seed, uint32_t nan_thr, hipStream_t st);

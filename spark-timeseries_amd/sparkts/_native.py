@@ -52,6 +52,11 @@ SIGNATURES = {
     "sts_active_instants": (_c_int, [_c_vp, _c_i64, _c_vp, _c_vp, _c_vp]),
     "sts_gather_instants": (_c_int, [_c_vp, _c_vp, _c_i64, _c_i64, _c_i64, _c_vp, _c_i64, _c_vp]),
     "sts_to_instants": (_c_int, [_c_vp, _c_vp, _c_i64, _c_i64, _c_i64, _c_i64, _c_vp]),
+    "sts_wire_scan": (_c_int, [_c_vp, _c_i64, _c_i64, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp]),
+    "sts_wire_decode": (_c_int, [_c_vp, _c_vp, _c_i64, _c_i64, _c_vp, _c_i64, _c_vp]),
+    "sts_wire_encode": (_c_int, [_c_vp, _c_i64, _c_i64, _c_i64, _c_vp, _c_vp, _c_vp]),
+    "sts_observations_to_panel": (_c_int, [_c_vp, _c_vp, _c_vp, _c_i64, _c_vp, _c_i64, _c_i64, _c_i64, _c_vp]),
+    "sts_csv_parse": (_c_int, [_c_vp, _c_i64, _c_i64, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_i64]),
     "sts_gen_panel": (_c_int, [_c_vp, _c_i64, _c_i64, _c_i64, _c_i64, ctypes.c_uint64, _c_dbl, _c_vp]),
     "sts_gen_ar_panel": (_c_int, [_c_vp, _c_vp, _c_vp, _c_i64, _c_i64, _c_i64, _c_i64, ctypes.c_uint64, _c_int, _c_vp]),
     "sts_fill_host": (_c_int, [_c_vp, _c_vp, _c_i64, _c_i64, _c_i64, _c_int, _c_vp]),

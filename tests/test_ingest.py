@@ -1,0 +1,76 @@
+"""Ingest / egress formats -- host-side parsing on CPU.
+
+The wire-format header walk (sts_wire_scan) and the CSV line parse (sts_csv_parse) run on
+the host and need no device; the byte-swap decode / encode and the observation scatter are
+device kernels (tests/test_parity_gpu.py).  Records are produced with the reference's own
+serializer semantics (python/sparkts/timeseriesrdd.py:244-256, restated in oracle.wire_records).
+"""
+import math
+import struct
+
+import numpy as np
+import pytest
+
+import oracle
+from sparkts import io as sio
+from sparkts.errors import IllegalArgumentException
+
+
+def test_wire_scan_offsets():
+    rng = np.random.default_rng(0)
+    keys = ["a", "AAPL", "", "ключ", "x" * 37]
+    panel = rng.standard_normal((5, 11))
+    panel[1, 3] = np.nan
+    data = oracle.wire_records(keys, panel)
+    got_keys, T, val_off = sio.wire_scan(data)
+    assert got_keys == keys and T == 11
+    buf = np.frombuffer(data, np.uint8)
+    for s in range(5):
+        vals = np.frombuffer(buf[val_off[s]: val_off[s] + 8 * T].tobytes(), dtype=">f8")
+        assert np.array_equal(vals.astype(np.float64).view(np.uint64), panel[s].view(np.uint64))
+
+
+def test_wire_scan_rejects_ragged_and_truncated():
+    good = oracle.wire_records(["a", "b"], np.zeros((2, 3)))
+    ragged = oracle.wire_records(["a"], np.zeros((1, 3))) + oracle.wire_records(["b"], np.zeros((1, 4)))
+    with pytest.raises(IllegalArgumentException):
+        sio.wire_scan(ragged)
+    with pytest.raises(IllegalArgumentException):
+        sio.wire_scan(good[:-3])
+    keys, T, off = sio.wire_scan(b"")
+    assert keys == [] and T == 0 and len(off) == 0
+
+
+def test_csv_parse_java_tokens():
+    text = b"k1,1.0,2.5,NaN\nk2,-Infinity,1.0E-5,3\r\nk3,Infinity,-0.0,12345678.9\n"
+    keys, vals = sio.csv_parse(text)
+    assert keys == ["k1", "k2", "k3"]
+    want = [[1.0, 2.5, math.nan], [-math.inf, 1e-5, 3.0], [math.inf, -0.0, 12345678.9]]
+    assert np.array_equal(np.nan_to_num(vals), np.nan_to_num(np.array(want)))
+    assert math.copysign(1.0, vals[2, 1]) < 0
+    with pytest.raises(IllegalArgumentException):
+        sio.csv_parse(b"k1,1.0,abc\n")
+    with pytest.raises(IllegalArgumentException):
+        sio.csv_parse(b"k1,1.0,2.0\nk2,1.0\n")
+
+
+def test_java_double_to_string_round_trips():
+    rng = np.random.default_rng(1)
+    vals = list(rng.standard_normal(200) * 10.0 ** rng.integers(-12, 12, 200)) + [1.0, 0.001, 1e7, 1e-3, 123.0]
+    for v in vals:
+        s = sio.java_double_to_string(float(v))
+        assert float(s.replace("E", "e")) == v, (v, s)
+    assert sio.java_double_to_string(1e7) == "1.0E7"
+    assert sio.java_double_to_string(1e-4) == "1.0E-4"
+    assert sio.java_double_to_string(1234567.0) == "1234567.0"
+    assert sio.java_double_to_string(float("nan")) == "NaN"
+    assert sio.java_double_to_string(-float("inf")) == "-Infinity"
+
+
+def test_observations_restatement_kat():
+    # later samples of one (key, timestamp) win; timestamps outside the index are dropped
+    idx = [10, 20, 30]
+    keys, panel = oracle.observations_to_panel(idx, ["b", "a", "b", "a", "b"], [20, 10, 20, 99, 30],
+                                               [1.0, 2.0, 3.0, 4.0, 5.0])
+    assert keys == ["a", "b"]
+    assert np.array_equal(np.nan_to_num(panel, nan=-1), [[2.0, -1, -1], [-1, 3.0, 5.0]])

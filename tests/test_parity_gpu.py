@@ -682,3 +682,51 @@ def test_to_instants(torch):
         x = rng.standard_normal((S, T))
         _, inst = TimeSeriesRDD(None, None, dev(torch, x)).toInstants()
         assert_bits(host(inst), oracle.to_instants(x), "toInstants %dx%d" % (S, T))
+
+
+# ---------------- ingest / egress formats: bit-exact ----------------
+
+def test_wire_decode_encode_round_trip(torch):
+    from sparkts import io as sio
+    rng = np.random.default_rng(31)
+    for S, T in [(1, 1), (3, 7), (40, 390), (5, 5000)]:
+        keys = ["k%d" % i + "é" * (i % 3) for i in range(S)]     # unaligned value blocks
+        x = rng.standard_normal((S, T)) * 1e3
+        x.ravel()[rng.random(S * T) < 0.05] = NaN
+        if T > 2:
+            x[0, 1] = -0.0
+            x[0, 2] = np.inf
+        data = oracle.wire_records(keys, x)
+        rdd = sio.timeSeriesRDDFromWire(None, data)
+        assert rdd.keys == keys
+        assert_bits(host(rdd.data), x, "wire decode %dx%d" % (S, T))
+        assert sio.toWire(rdd) == data                       # KeyAndSeriesToBytes, byte for byte
+
+
+def test_observations_to_panel(torch):
+    from sparkts import io as sio
+    rng = np.random.default_rng(8)
+    idx = np.arange(0, 5000, 5, dtype=np.int64)             # 1000 instants
+    n = 20000
+    keys = ["s%03d" % k for k in rng.integers(0, 150, n)]
+    ts = rng.integers(0, 5100, n).astype(np.int64)          # some off-grid / past the end: dropped
+    ts[::3] = ts[::3] // 5 * 5                              # many on the grid, duplicates included
+    vals = rng.standard_normal(n)
+    rdd = sio.timeSeriesRDDFromObservations(idx, keys, ts, vals)
+    ref_keys, ref = oracle.observations_to_panel(idx, keys, ts, vals)
+    assert rdd.keys == ref_keys
+    assert_bits(host(rdd.data), ref, "observations")
+
+
+def test_csv_round_trip(torch, tmp_path):
+    from sparkts import io as sio
+    from sparkts.timeseriesrdd import TimeSeriesRDD
+    rng = np.random.default_rng(9)
+    x = rng.standard_normal((12, 50)) * 10.0 ** rng.integers(-8, 9, (12, 50))
+    x[3, 4] = NaN
+    x[5, 6] = -np.inf
+    rdd = TimeSeriesRDD("uniform(2015-04-09,50,1 day)", ["key%d" % i for i in range(12)], dev(torch, x))
+    sio.saveAsCsv(rdd, str(tmp_path / "ts"))
+    back = sio.timeSeriesRDDFromCsv(str(tmp_path / "ts"))
+    assert back.keys == rdd.keys and back.index == rdd.index
+    assert_bits(host(back.data), x, "csv round trip")
