@@ -252,13 +252,12 @@ def wire_records(keys, panel) -> bytes:
     """KeyAndSeriesToBytes / python _TimeSeriesSerializer.dumps (python/sparkts/timeseriesrdd.py:
     244-256): int32 BE keyLen, UTF-8 key, int32 BE n, n x '!d'."""
     import struct
-    out = bytearray()
+    parts = []
     for k, row in zip(keys, panel):
         kb = k.encode("utf-8")
-        out += struct.pack("!i", len(kb)) + kb + struct.pack("!i", len(row))
-        for v in row:
-            out += struct.pack("!d", v)
-    return bytes(out)
+        row = np.asarray(row, dtype=np.float64)
+        parts.append(struct.pack("!i", len(kb)) + kb + struct.pack("!i", row.size) + row.astype(">f8").tobytes())
+    return b"".join(parts)
 
 
 # ---------------- panel drivers ----------------
