@@ -96,14 +96,16 @@ struct ErrSink {
     Scratch scratch;
     int64_t S;
     ErrSink(int32_t* user, int64_t S_, hipStream_t st) : dev(user), scratch(st), S(S_) {}
-    int prepare() {
+    // zero = false: the caller guarantees that the kernel writes every entry, or zeroes it
+    // itself (run_tile)
+    int prepare(bool zero = true) {
         if (!dev) {
             hipError_t e = scratch.alloc((size_t)(S > 0 ? S : 1) * sizeof(int32_t));
             if (e != hipSuccess) return hip_fail(e, "hipMallocAsync(err)");
             dev = static_cast<int32_t*>(scratch.p);
             owned = true;
         }
-        if (S > 0) {
+        if (S > 0 && zero) {
             hipError_t e = hipMemsetAsync(dev, 0, (size_t)S * sizeof(int32_t), scratch.st);
             if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync(err)");
         }
@@ -168,9 +170,15 @@ hipError_t timed(hipStream_t st, F&& launch) {
 }
 
 // fill (+ optional ACF partials / lag matrix) through the tile kernel
+// err: zeroed here unless the chosen kernel writes every entry (the seg kernel with one
+// segment per series); callers prepare their ErrSink with zero = false.
 int run_tile(const double* in, double* out, double* lagmat, int64_t S, int64_t T, int64_t ld_in, int64_t ld_out,
              int method, int K, double* acf, int max_lag, int inc, int32_t* err, hipStream_t st, const char* name) {
-    if (S == 0 || T == 0) return STS_OK;
+    if (S == 0) return STS_OK;
+    if (T == 0) {
+        if (err) HIP_TRY(hipMemsetAsync(err, 0, (size_t)S * sizeof(int32_t), st), "hipMemsetAsync(err)");
+        return STS_OK;
+    }
     // short series (T <= 16384: C1, the 10-year daily panels) go to the wave-private
     // segment kernel (2x faster there: one wave per series, no barriers), long ones to the
     // workgroup tile kernel (faster from T = 32768: C3, C5).  The segment kernel needs a
@@ -200,8 +208,17 @@ int run_tile(const double* in, double* out, double* lagmat, int64_t S, int64_t T
     a.max_lag = max_lag;
     a.include_original = inc;
     if (S * a.chunks_per_series > 0x7fffffffLL) return fail(STS_ERR_BAD_ARG, "%s: panel too large for one launch", name);
+    // one segment per series: the seg kernel writes err[s] for every series and, when the
+    // finalize's general path applies (T > 2K) and the last tile holds >= 64 steps, the
+    // final ACF itself (no partials, no second launch)
+    const bool one_seg = seg && a.chunks_per_series == 1;
+    const int64_t last_len = T - (a.tiles_per_series - 1) * tw;
+    const bool fuse = one_seg && K > 0 && T > 2 * (int64_t)K && last_len >= 64 && !std::getenv("STS_NO_FUSED_ACF");
+    a.err_all = one_seg ? 1 : 0;
+    a.acf_fused = fuse ? acf : nullptr;
+    if (err && !one_seg) HIP_TRY(hipMemsetAsync(err, 0, (size_t)S * sizeof(int32_t), st), "hipMemsetAsync(err)");
     Scratch part(st);
-    if (K > 0) {
+    if (K > 0 && !fuse) {
         hipError_t e = part.alloc((size_t)(S * a.chunks_per_series) * sts::kPartStride * sizeof(double));
         if (e != hipSuccess) return hip_fail(e, "hipMallocAsync(partials)");
         a.partials = static_cast<double*>(part.p);
@@ -210,7 +227,7 @@ int run_tile(const double* in, double* out, double* lagmat, int64_t S, int64_t T
     hipError_t e = seg ? sts::launch_segment(method, a, st) : sts::launch_tile(method, tw, a, st);
     prof_mark(st);
     if (e != hipSuccess) return hip_fail(e, name);
-    if (K > 0) {
+    if (K > 0 && !fuse) {
         sts::FinalizeArgs f{};
         f.F = out ? out : in;
         f.partials = a.partials;
@@ -295,7 +312,7 @@ int sts_fill(const double* in, double* out, int64_t S, int64_t T, int64_t ld_in,
     if ((r = ensure_device())) return r;
     hipStream_t st = as_stream(stream);
     ErrSink es(err_per_series, S, st);
-    if ((r = es.prepare())) return r;
+    if ((r = es.prepare(false))) return r;   // run_tile zeroes err unless its kernel writes all of it
     if ((r = run_tile(in, out, nullptr, S, T, ld_in, ld_out, method, 0, nullptr, 0, 0, es.dev, st, "fill"))) return r;
     return es.finish("fill");
 }
@@ -316,7 +333,9 @@ int sts_fill_autocorr(const double* in, double* filled, int64_t S, int64_t T, in
     if ((r = ensure_device())) return r;
     hipStream_t st = as_stream(stream);
     ErrSink es(err_per_series, S, st);
-    if ((r = es.prepare())) return r;
+    if ((r = es.prepare(false))) return r;   // zeroed by run_tile, or below when it does not run
+    if (S > 0 && (T == 0 || (K == 0 && method == STS_FILL_NONE)))
+        HIP_TRY(hipMemsetAsync(es.dev, 0, (size_t)S * sizeof(int32_t), st), "hipMemsetAsync(err)");
     if (T == 0 && S > 0 && K > 0) {
         std::vector<double> nan((size_t)(S * K), NAN);
         HIP_TRY(hipMemcpyAsync(acf, nan.data(), nan.size() * sizeof(double), hipMemcpyHostToDevice, st), "acf");
@@ -383,7 +402,7 @@ int sts_fill_lag_matrix(const double* in, double* filled, double* lagmat, int64_
     if ((r = ensure_device())) return r;
     hipStream_t st = as_stream(stream);
     ErrSink es(err_per_series, S, st);
-    if ((r = es.prepare())) return r;
+    if ((r = es.prepare(false))) return r;   // run_tile zeroes err unless its kernel writes all of it
     if ((r = run_tile(in, filled, n > 0 ? lagmat : nullptr, S, T, ld_in, ld_out, method, 0, nullptr, max_lag,
                       include_original ? 1 : 0, es.dev, st, "fill_lag_matrix"))) return r;
     return es.finish("fill_lag_matrix");

@@ -29,6 +29,8 @@ struct TileArgs {
     int K;                // ACF lags (0 = no ACF)
     int max_lag;          // lag matrix p
     int include_original; // lag matrix inc
+    double* acf_fused;    // seg kernel, one segment per series: final ACF written directly (S x K)
+    int err_all;          // seg kernel, one segment per series: err[s] written for every series
 };
 
 struct FinalizeArgs {

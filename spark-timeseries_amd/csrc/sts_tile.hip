@@ -43,6 +43,10 @@
 #define STS_LDS_BARRIER 1
 #endif
 
+#ifndef STS_WAVE_SCAN
+#define STS_WAVE_SCAN 0        // every wave runs the word scan into its own LDS copy (no barrier)
+#endif
+
 namespace sts {
 namespace {
 
@@ -158,16 +162,24 @@ __global__ __launch_bounds__(kThreads, 3) void tile_kernel(TileArgs a, int metho
     static_assert(NW <= 128, "word scan handles at most 128 words");
     __shared__ __attribute__((aligned(16))) double vals[EWP];   // padded (px) for the shifted scheme
     __shared__ unsigned long long mask[NW];
-    __shared__ int lastUpTo[NW];     // last valid E-position in words <= w (-1: none)
-    __shared__ int firstFrom[NW];    // first valid E-position in words >= w (kBig: none)
-    __shared__ int wbase[NW + 1];    // NaN-list offset of each word (exclusive prefix count)
-    __shared__ unsigned long long wneed[NW];   // NaN positions to impute, per word
-    __shared__ int sh_i[3];          // lext, next (series positions), NaN count
-    __shared__ double sh_d[3];       // c0, value at lext, value at next
+    constexpr int NSC = STS_WAVE_SCAN ? kWaves : 1;   // copies of the scan results
+    __shared__ int lastUpTo_[NSC][NW];     // last valid E-position in words <= w (-1: none)
+    __shared__ int firstFrom_[NSC][NW];    // first valid E-position in words >= w (kBig: none)
+    __shared__ int wbase_[NSC][NW + 1];    // NaN-list offset of each word (exclusive prefix count)
+    __shared__ unsigned long long wneed_[NSC][NW];   // NaN positions to impute, per word
+    __shared__ int sh_i_[NSC][3];          // lext, next (series positions), NaN count
+    __shared__ double sh_d_[NSC][3];       // c0, value at lext, value at next
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform: scalar loop control
+    const int wsc = STS_WAVE_SCAN ? wave : 0;
+    int* lastUpTo = lastUpTo_[wsc];
+    int* firstFrom = firstFrom_[wsc];
+    int* wbase = wbase_[wsc];
+    unsigned long long* wneed = wneed_[wsc];
+    int* sh_i = sh_i_[wsc];
+    double* sh_d = sh_d_[wsc];
     // one workgroup = one CHUNK of tiles_per_chunk consecutive tiles of one series
     const int64_t nchunk = a.S * a.chunks_per_series;
     const int64_t ch = xcd_remap(blockIdx.x, nchunk);
@@ -195,10 +207,10 @@ __global__ __launch_bounds__(kThreads, 3) void tile_kernel(TileArgs a, int metho
                 const int64_t f = scan_fwd(src, 0, T, lane);
                 x0 = (f < T) ? src[f] : __builtin_nan("");
             }
-            if (lane == 0) sh_d[0] = x0;
+            if (lane == 0) sh_d_[0][0] = x0;
         }
         lds_barrier();
-        c0 = sh_d[0];
+        c0 = sh_d_[0][0];
         lds_barrier();
     }
 
@@ -304,9 +316,10 @@ __global__ __launch_bounds__(kThreads, 3) void tile_kernel(TileArgs a, int metho
         }
         STAMP(3);
 
-        // ---- 3. word scans (wave 0; lane l: words 2l, 2l+1): last valid position up to
-        //      each word, first valid from each word, and the NaN-list offset of each word ----
-        if (wave == 0) {
+        // ---- 3. word scans (wave 0, or every wave into its own copy; lane l: words 2l, 2l+1):
+        //      last valid position up to each word, first valid from each word, and the
+        //      NaN-list offset of each word ----
+        if (STS_WAVE_SCAN || wave == 0) {
             const int w0 = 2 * lane, w1 = 2 * lane + 1;
             const unsigned long long m0 = (w0 < NW) ? mask[w0] : ~0ull;
             const unsigned long long m1 = (w1 < NW) ? mask[w1] : ~0ull;
@@ -373,7 +386,13 @@ __global__ __launch_bounds__(kThreads, 3) void tile_kernel(TileArgs a, int metho
             }
         }
         STAMP(4);
+#if STS_WAVE_SCAN
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");   // own copy: wave-local order
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+#else
         lds_barrier();
+#endif
         STAMP(5);
 
         // ---- 4. impute the compacted NaN positions, all lanes busy; F goes back into
@@ -483,7 +502,10 @@ __global__ __launch_bounds__(kThreads, 3) void tile_kernel(TileArgs a, int metho
                         if (jj >= FY) continue;
                         const bool in = jj * kThreads + kThreads <= NP2 - kHB / 2 ||
                                         tid + jj * kThreads < NP2 - kHB / 2;
-                        if (jj < FS && wr) dp[jj * kThreads] = fv[j];
+                        if (jj < FS && wr) {   // non-temporal: A/B on C3 +1 %
+                            __builtin_nontemporal_store(fv[j].x, &dp[jj * kThreads].x);
+                            __builtin_nontemporal_store(fv[j].y, &dp[jj * kThreads].y);
+                        }
                         if (NT > 0 && in) {
                             double2 y;
                             y.x = fv[j].x - c0;

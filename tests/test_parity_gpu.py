@@ -259,6 +259,43 @@ def test_fill_autocorr_both_kernels(torch, monkeypatch, kernel, method):
             assert_bits(got, ref, "%s %s T=%d" % (kernel, method, T))
 
 
+@pytest.mark.parametrize("T", [121, 512, 575, 576, 1000, 1024, 2520, 4097, 16384])
+def test_fused_acf_finalize_matches_two_kernel_path(torch, monkeypatch, T):
+    # one segment per series: the segment kernel finalizes the ACF itself (no partials, no
+    # second launch) when T > 2K and its last tile holds >= 64 steps; bit-identical to the
+    # separate acf_finalize_kernel, and err is written for every series without a memset
+    from sparkts import TimeSeriesRDD
+    rng = np.random.default_rng(T)
+    x = random_panel(rng, 9, T, 0.05, runs=True)
+    x[4] = 7.0                                            # constant: 0/0 = NaN
+    x[5, 0] = NaN                                         # head NaN -> all-NaN ACF
+    for K in (1, 20, 60):
+        if T <= 2 * K:
+            continue
+        f1, a1 = TimeSeriesRDD(None, None, dev(torch, x)).fillAndAutocorr("linear", K)
+        monkeypatch.setenv("STS_NO_FUSED_ACF", "1")
+        f2, a2 = TimeSeriesRDD(None, None, dev(torch, x)).fillAndAutocorr("linear", K)
+        monkeypatch.delenv("STS_NO_FUSED_ACF")
+        assert_bits(host(a1), host(a2), "fused vs separate finalize T=%d K=%d" % (T, K))
+        assert_bits(host(f1.data), host(f2.data), "filled")
+        _, racf, _ = oracle.panel_fill_autocorr(x, "linear", K)
+        assert_rel(host(a1), racf, what="fused T=%d K=%d" % (T, K))
+    # err written for every series (stale values in the caller's array are overwritten)
+    from sparkts import _native
+    xn = x.copy()
+    xn[2, 1:] = NaN
+    xd = dev(torch, xn)
+    out = torch.empty_like(xd)
+    acf = torch.empty((9, 20), dtype=torch.float64, device="cuda:0")
+    err = torch.full((9,), 99, dtype=torch.int32, device="cuda:0")
+    st = _native.lib().sts_fill_autocorr(xd.data_ptr(), out.data_ptr(), 9, T, T, T, 1, 20, acf.data_ptr(),
+                                         err.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    assert st == 0
+    want = np.zeros(9, np.int32)
+    want[2] = 2                                            # nearest on [x0, NaN, ...]: "Input is all NaNs!"
+    assert np.array_equal(host(err), want)
+
+
 def test_fill_autocorr_c3_length(torch):
     # C3 series length (982,800 minute bars), a few series: fused fill("linear") + ACF(60)
     S, T, K = 3, 982_800, 60
