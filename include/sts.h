@@ -218,6 +218,15 @@ int sts_csv_parse(const char* text, int64_t len, int64_t max_records, int64_t* n
 int sts_ar_fit(const double* in, int64_t S, int64_t T, int64_t ld, int p, int no_intercept,
                double* c, double* coef, int32_t* err_per_series, void* stream);
 
+/* ---- f1b: ARIMA.fitModel(p, d, 0, ts, includeIntercept) -- the AR-only path
+ * (S/models/ARIMA.scala:80-90): differencesOfOrderD(ts, d) (S/UnivariateTimeSeries.scala:
+ * 438-450, ping-pong buffers) with the first d values dropped, then
+ * Autoregression.fitModel(diffed, p, !includeIntercept).  The ARIMAModel's coefficients are
+ * [c (if includeIntercept)] ++ coef.  Differencing bit-exact, the fit 1e-10 relative. */
+int sts_arima_fit_ar(const double* in, int64_t S, int64_t T, int64_t ld, int p, int d,
+                     int include_intercept, double* c, double* coef, int32_t* err_per_series,
+                     void* stream);
+
 /* ---- a12 / a13: ARModel.remove/addTimeDependentEffects (S/models/Autoregression.scala:60-88).
  * out == in reproduces the reference's aliasing semantics.  Bit-exact. */
 int sts_ar_remove(const double* in, double* out, int64_t S, int64_t T, int64_t ld_in,

@@ -757,6 +757,37 @@ int sts_csv_parse(const char* text, int64_t len, int64_t max_records, int64_t* n
                            : STS_OK;
 }
 
+int sts_arima_fit_ar(const double* in, int64_t S, int64_t T, int64_t ld, int p, int d, int include_intercept,
+                     double* c, double* coef, int32_t* err_per_series, void* stream) {
+    int r;
+    if ((r = check_panel(in, S, T, ld, "ARIMA.fitModel"))) return r;
+    if (d < 0 || d > T) return fail(STS_ERR_BAD_ARG, "ARIMA.fitModel: differencing order %d outside [0, T]", d);
+    if (d == 0) return sts_ar_fit(in, S, T, ld, p, include_intercept ? 0 : 1, c, coef, err_per_series, stream);
+    if (p < 1 || p > 31) return fail(STS_ERR_BAD_ARG, "ARIMA.fitModel: AR order %d outside [1, 31]", p);
+    const int64_t Tn = T - d;
+    if (Tn - p < (int64_t)p + 1)
+        return fail(STS_ERR_NOT_ENOUGH_DATA, "ARIMA.fitModel: not enough data (%lld rows) for the number of predictors (%d)",
+                    (long long)(Tn - p), p);
+    if (S == 0) return STS_OK;
+    if ((r = ensure_device())) return r;
+    hipStream_t st = as_stream(stream);
+    // differencesOfOrderD: level i differences level i-1 at lag 1 from index i (ping-pong)
+    Scratch bufA(st), bufB(st);
+    HIP_TRY(bufA.alloc((size_t)(S * T) * sizeof(double)), "hipMallocAsync(arima)");
+    if (d > 1) HIP_TRY(bufB.alloc((size_t)(S * T) * sizeof(double)), "hipMallocAsync(arima)");
+    const double* cur = in;
+    int64_t cur_ld = ld;
+    double* bufs[2] = {static_cast<double*>(bufA.p), static_cast<double*>(bufB.p)};
+    for (int i = 1; i <= d; i++) {
+        double* nxt = bufs[(i - 1) & 1];
+        HIP_TRY(sts::launch_diff(cur, nxt, S, T, cur_ld, T, 1, i, st), "differencesOfOrderD");
+        cur = nxt;
+        cur_ld = T;
+    }
+    // .drop(d), then Autoregression.fitModel(diffed, p, !includeIntercept)
+    return sts_ar_fit(cur + d, S, Tn, T, p, include_intercept ? 0 : 1, c, coef, err_per_series, stream);
+}
+
 int sts_fill_diff_ewma(const double* in, double* out, int64_t S, int64_t T, int64_t ld_in, int64_t ld_out, int method,
                        int lag, const double* smoothing, int32_t* err_per_series, void* stream) {
     int r;

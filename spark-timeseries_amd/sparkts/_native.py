@@ -57,6 +57,7 @@ SIGNATURES = {
     "sts_wire_encode": (_c_int, [_c_vp, _c_i64, _c_i64, _c_i64, _c_vp, _c_vp, _c_vp]),
     "sts_observations_to_panel": (_c_int, [_c_vp, _c_vp, _c_vp, _c_i64, _c_vp, _c_i64, _c_i64, _c_i64, _c_vp]),
     "sts_csv_parse": (_c_int, [_c_vp, _c_i64, _c_i64, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_i64]),
+    "sts_arima_fit_ar": (_c_int, [_c_vp, _c_i64, _c_i64, _c_i64, _c_int, _c_int, _c_int, _c_vp, _c_vp, _c_vp, _c_vp]),
     "sts_gen_panel": (_c_int, [_c_vp, _c_i64, _c_i64, _c_i64, _c_i64, ctypes.c_uint64, _c_dbl, _c_vp]),
     "sts_gen_ar_panel": (_c_int, [_c_vp, _c_vp, _c_vp, _c_i64, _c_i64, _c_i64, _c_i64, ctypes.c_uint64, _c_int, _c_vp]),
     "sts_fill_host": (_c_int, [_c_vp, _c_vp, _c_i64, _c_i64, _c_i64, _c_int, _c_vp]),

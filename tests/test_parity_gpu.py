@@ -767,3 +767,30 @@ def test_csv_round_trip(torch, tmp_path):
     back = sio.timeSeriesRDDFromCsv(str(tmp_path / "ts"))
     assert back.keys == rdd.keys and back.index == rdd.index
     assert_bits(host(back.data), x, "csv round trip")
+
+
+# ---------------- ARIMA(p, d, 0): differencesOfOrderD + AR fit ----------------
+
+@pytest.mark.parametrize("p,d,inc", [(1, 1, True), (2, 1, False), (3, 2, True), (5, 3, True), (9, 1, True)])
+def test_arima_ar_path(torch, p, d, inc):
+    from sparkts.models import ARIMA
+    rng = np.random.default_rng(p * 10 + d)
+    S, T = 37, 800
+    x = np.empty((S, T))
+    for s in range(S):
+        e = rng.standard_normal(T)
+        y = oracle.ar_add(e, 0.3, [0.5 / p] * p, inplace=True)   # stationary AR(p)
+        for _ in range(d):
+            y = np.cumsum(y)                                     # integrate d times
+        x[s] = y + 50.0
+    m = ARIMA.fitModel(p, d, 0, dev(torch, x), includeIntercept=inc)
+    got = host(m.coefficients)
+    ref = []
+    for row in x:
+        diffed = oracle.differences_of_order_d(row, d)[d:]
+        c, coef = oracle.ar_fit(diffed, p, no_intercept=not inc)
+        ref.append(([c] if inc else []) + list(coef))
+    assert_rel(got, np.array(ref), what="ARIMA(%d,%d,0)" % (p, d))
+    from sparkts.errors import UnsupportedOperationException
+    with pytest.raises(UnsupportedOperationException):
+        ARIMA.fitModel(1, 1, 2, dev(torch, x))
