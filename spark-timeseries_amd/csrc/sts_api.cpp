@@ -182,7 +182,7 @@ int run_tile(const double* in, double* out, double* lagmat, int64_t S, int64_t T
     // short series (T <= 16384: C1, the 10-year daily panels) go to the wave-private
     // segment kernel (2x faster there: one wave per series, no barriers), long ones to the
     // workgroup tile kernel (faster from T = 32768: C3, C5).  The segment kernel needs a
-    // 16-B aligned panel, no lag matrix and K <= 60.  STS_TILE_KERNEL=tile|seg forces one
+    // 16-B aligned panel, no lag matrix and K <= 60.  STS_TILE_KERNEL=tile|seg|tile2 forces one
     // (A/B runs, tools/kbench.py).
     const char* force = std::getenv("STS_TILE_KERNEL");
     const bool seg_ok = !lagmat && sts::seg_nt(K) >= 0 && (reinterpret_cast<uintptr_t>(in) & 15) == 0 &&
@@ -224,7 +224,9 @@ int run_tile(const double* in, double* out, double* lagmat, int64_t S, int64_t T
         a.partials = static_cast<double*>(part.p);
     }
     prof_mark(st);
-    hipError_t e = seg ? sts::launch_segment(method, a, st) : sts::launch_tile(method, tw, a, st);
+    const bool t2 = !seg && tw == 4096 && sts::tile2_supported(K, a) && force && !std::strcmp(force, "tile2");
+    hipError_t e = seg ? sts::launch_segment(method, a, st)
+                       : (t2 ? sts::launch_tile2(method, a, st) : sts::launch_tile(method, tw, a, st));
     prof_mark(st);
     if (e != hipSuccess) return hip_fail(e, name);
     if (K > 0 && !fuse) {

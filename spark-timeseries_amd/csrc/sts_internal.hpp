@@ -43,6 +43,9 @@ struct FinalizeArgs {
 
 // launchers (return hipError_t of the launch)
 hipError_t launch_tile(int method, int tw, const TileArgs& a, hipStream_t st);
+// role-split variant (sts_tile2.hip): fill waves and MFMA waves on different tiles
+bool tile2_supported(int K, const TileArgs& a);
+hipError_t launch_tile2(int method, const TileArgs& a, hipStream_t st);
 hipError_t launch_acf_finalize(const FinalizeArgs& a, hipStream_t st);
 
 // Wave-private segment kernel (sts_seg.hip): tiles of kSegW steps, kSegTiles tiles per

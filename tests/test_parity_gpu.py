@@ -234,7 +234,7 @@ def test_fill_autocorr_fused(torch, method):
         assert_rel(host(acf), racf, what=method)
 
 
-@pytest.mark.parametrize("kernel", ["tile", "seg"])
+@pytest.mark.parametrize("kernel", ["tile", "seg", "tile2"])
 @pytest.mark.parametrize("method", ["linear", "previous", "next", "nearest"])
 def test_fill_autocorr_both_kernels(torch, monkeypatch, kernel, method):
     # both imputation kernels, whatever the length-based dispatch picks: the workgroup
