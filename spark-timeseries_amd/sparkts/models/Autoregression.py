@@ -31,7 +31,7 @@ class ARModel(TimeSeriesModel):
         c = p.vec(self.c, p.S, "c")
         if p.device:
             import torch
-            coef_t = torch.as_tensor(np.ascontiguousarray(arr), device=p.t.device)
+            coef_t = torch.as_tensor(np.array(arr, dtype=np.float64, order="C"), device=p.t.device)
         else:
             coef_t = np.ascontiguousarray(arr)
         return c, coef_t, order
