@@ -145,6 +145,46 @@ int sts_ewma_fit(const double* in, int64_t S, int64_t T, int64_t ld, double* smo
 int sts_ewma_sse_gradient(const double* in, int64_t S, int64_t T, int64_t ld,
                           const double* smoothing, double* sse, double* gradient, void* stream);
 
+/* ---- f1: GARCH(1,1) and AR(1)+GARCH(1,1) (S/models/GARCH.scala) ----
+ * GARCH.fitModel (:33-53) per series: commons-math3 NLCG (Fletcher-Reeves) from
+ * (.2, .2, .2) without a GoalType (its maximising branches), MaxIter / MaxEval 10000;
+ * params[s*3 + 0..2] = (omega, alpha, beta).  A series the reference cannot fit gets NaN
+ * params and its status in err_per_series (device, optional; NULL -> the first failure is
+ * returned): STS_ERR_TOO_MANY_EVALUATIONS (e.g. any NaN), STS_ERR_TOO_MANY_ITERATIONS,
+ * STS_ERR_BAD_ARG (invalid line-search interval).  Bit-exact against the restatement
+ * (Math.log evaluated as StrictMath.log / fdlibm). */
+int sts_garch_fit(const double* in, int64_t S, int64_t T, int64_t ld, double* params,
+                  int32_t* err_per_series, void* stream);
+/* GARCHModel(params[s]).logLikelihood(ts) (:80-86) and .gradient(ts) (:94-114) per series,
+ * one pass; gradient[s*3 + 0..2] in the reference's (alpha, beta, omega) order. */
+int sts_garch_loglik_gradient(const double* in, int64_t S, int64_t T, int64_t ld,
+                              const double* params, double* loglik, double* gradient,
+                              void* stream);
+/* GARCHModel.removeTimeDependentEffects / addTimeDependentEffects (:130-159), per-series
+ * omega / alpha / beta.  out == NULL -> STS_ERR_NULL_DEST; out == in is the reference's
+ * dest eq ts (identical here: both read ts(i) before writing dest(i)).  Bit-exact. */
+int sts_garch_remove(const double* in, double* out, int64_t S, int64_t T, int64_t ld_in,
+                     int64_t ld_out, const double* omega, const double* alpha,
+                     const double* beta, void* stream);
+int sts_garch_add(const double* in, double* out, int64_t S, int64_t T, int64_t ld_in,
+                  int64_t ld_out, const double* omega, const double* alpha,
+                  const double* beta, void* stream);
+/* ARGARCHModel.removeTimeDependentEffects / addTimeDependentEffects (:203-234).  remove
+ * with out == in reproduces the reference's read of the overwritten ts(i - 1).  Bit-exact. */
+int sts_argarch_remove(const double* in, double* out, int64_t S, int64_t T, int64_t ld_in,
+                       int64_t ld_out, const double* c, const double* phi, const double* omega,
+                       const double* alpha, const double* beta, void* stream);
+int sts_argarch_add(const double* in, double* out, int64_t S, int64_t T, int64_t ld_in,
+                    int64_t ld_out, const double* c, const double* phi, const double* omega,
+                    const double* alpha, const double* beta, void* stream);
+/* ARGARCH.fitModel (:62-68): Autoregression.fitModel(ts) (AR(1) with intercept, the a11
+ * kernels) -> c[s], phi[s]; its residuals (a12, into a scratch panel) -> GARCH.fitModel ->
+ * params[s*3 + 0..2].  T < 3 -> STS_ERR_NOT_ENOUGH_DATA.  An AR-stage failure keeps its
+ * status.  c / phi within 1e-10 of the Householder-QR restatement; the GARCH stage is
+ * bit-exact given the residuals. */
+int sts_argarch_fit(const double* in, int64_t S, int64_t T, int64_t ld, double* c, double* phi,
+                    double* params, int32_t* err_per_series, void* stream);
+
 /* ---- f2: TimeSeriesRDD.seriesStats() (S/TimeSeriesRDD.scala:204-206): Spark 1.3.1
  * StatCounter over each series' values, NaN included, merged in order
  * (delta = v - mu; n += 1; mu += delta / n; m2 += delta * (v - mu); max / min via
@@ -279,6 +319,10 @@ int sts_ewma_fit_host(const double* in, int64_t S, int64_t T, int64_t ld, double
                       int32_t* err_per_series);
 int sts_ar_fit_host(const double* in, int64_t S, int64_t T, int64_t ld, int p, int no_intercept,
                     double* c, double* coef, int32_t* err_per_series);
+int sts_garch_fit_host(const double* in, int64_t S, int64_t T, int64_t ld, double* params,
+                       int32_t* err_per_series);
+int sts_argarch_fit_host(const double* in, int64_t S, int64_t T, int64_t ld, double* c,
+                         double* phi, double* params, int32_t* err_per_series);
 int sts_ar_remove_host(const double* in, double* out, int64_t S, int64_t T, int64_t ld,
                        const double* c, const double* coef, int p);
 int sts_ar_add_host(const double* in, double* out, int64_t S, int64_t T, int64_t ld,

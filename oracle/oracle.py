@@ -64,6 +64,17 @@ def lib():
             "orc_ewma_gradient": (ctypes.c_double, [_dp, _i64, ctypes.c_double]),
             "orc_ewma_fit": (ctypes.c_int, [_dp, _i64, _dp, ctypes.POINTER(ctypes.c_int64)]),
             "orc_panel_ewma_fit": (ctypes.c_int, [_dp, _i64, _i64, _i64, _dp, i32p, ctypes.c_int]),
+            "orc_fdlibm_log": (ctypes.c_double, [ctypes.c_double]),
+            "orc_garch_loglik": (ctypes.c_double, [_dp, _i64, ctypes.c_double, ctypes.c_double, ctypes.c_double]),
+            "orc_garch_gradient": (None, [_dp, _i64, ctypes.c_double, ctypes.c_double, ctypes.c_double, _dp]),
+            "orc_garch_fit": (ctypes.c_int, [_dp, _i64, _dp, ctypes.POINTER(ctypes.c_int64)]),
+            "orc_argarch_fit": (ctypes.c_int, [_dp, _i64, _dp, ctypes.POINTER(ctypes.c_int64)]),
+            "orc_garch_remove": (None, [_dp, _dp, _i64, ctypes.c_double, ctypes.c_double, ctypes.c_double]),
+            "orc_garch_add": (None, [_dp, _dp, _i64, ctypes.c_double, ctypes.c_double, ctypes.c_double]),
+            "orc_argarch_remove": (None, [_dp, _dp, _i64] + [ctypes.c_double] * 5),
+            "orc_argarch_add": (None, [_dp, _dp, _i64] + [ctypes.c_double] * 5),
+            "orc_panel_garch_fit": (ctypes.c_int, [_dp, _i64, _i64, _i64, _dp, i32p, ctypes.c_int]),
+            "orc_panel_argarch_fit": (ctypes.c_int, [_dp, _i64, _i64, _i64, _dp, i32p, ctypes.c_int]),
             "orc_stat_counter": (None, [_dp, _i64, _dp]),
             "orc_remove_instants_with_nans": (_i64, [_dp, _i64, _i64, _i64, _dp, ctypes.POINTER(ctypes.c_int64)]),
             "orc_to_instants": (None, [_dp, _i64, _i64, _i64, _dp]),
@@ -211,6 +222,57 @@ def ewma_fit(ts):
     return st, float(sm[0]), int(ev.value)
 
 
+def fdlibm_log(x: float) -> float:
+    return lib().orc_fdlibm_log(float(x))
+
+
+def garch_loglik(ts, omega: float, alpha: float, beta: float) -> float:
+    """GARCHModel.logLikelihood (S/models/GARCH.scala:80-86)."""
+    ts = _vec(ts); return lib().orc_garch_loglik(_p(ts), ts.size, omega, alpha, beta)
+
+
+def garch_gradient(ts, omega: float, alpha: float, beta: float):
+    """GARCHModel.gradient (:94-114) -> [alpha, beta, omega] components (the reference's order)."""
+    ts = _vec(ts); g = np.zeros(3); lib().orc_garch_gradient(_p(ts), ts.size, omega, alpha, beta, _p(g))
+    return g
+
+
+def garch_fit(ts):
+    """GARCH.fitModel (:33-53) -> (status, (omega, alpha, beta), evaluations)."""
+    ts = _vec(ts); out = np.zeros(3); ev = ctypes.c_int64(0)
+    st = lib().orc_garch_fit(_p(ts), ts.size, _p(out), ctypes.byref(ev))
+    return st, out, int(ev.value)
+
+
+def argarch_fit(ts):
+    """ARGARCH.fitModel (:62-68) -> (status, (c, phi, omega, alpha, beta), evaluations)."""
+    ts = _vec(ts); out = np.zeros(5); ev = ctypes.c_int64(0)
+    st = lib().orc_argarch_fit(_p(ts), ts.size, _p(out), ctypes.byref(ev))
+    return st, out, int(ev.value)
+
+
+def garch_remove(ts, omega, alpha, beta):
+    ts = _vec(ts); out = np.empty_like(ts); lib().orc_garch_remove(_p(ts), _p(out), ts.size, omega, alpha, beta)
+    return out
+
+
+def garch_add(ts, omega, alpha, beta):
+    ts = _vec(ts); out = np.empty_like(ts); lib().orc_garch_add(_p(ts), _p(out), ts.size, omega, alpha, beta)
+    return out
+
+
+def argarch_remove(ts, c, phi, omega, alpha, beta, inplace=False):
+    ts = _vec(ts); out = ts if inplace else np.empty_like(ts)
+    lib().orc_argarch_remove(_p(ts), _p(out), ts.size, c, phi, omega, alpha, beta)
+    return out
+
+
+def argarch_add(ts, c, phi, omega, alpha, beta):
+    ts = _vec(ts); out = np.empty_like(ts)
+    lib().orc_argarch_add(_p(ts), _p(out), ts.size, c, phi, omega, alpha, beta)
+    return out
+
+
 def stat_counter(ts):
     """Spark StatCounter over the series values -> (count, mean, m2, max, min)."""
     ts = _vec(ts); out = np.zeros(4); lib().orc_stat_counter(_p(ts), ts.size, _p(out))
@@ -299,6 +361,18 @@ def panel_ewma_fit(x, threads: int = 1):
     x = _panel(x); S, T = x.shape; sm = np.empty(S); err = np.zeros(S, np.int32)
     lib().orc_panel_ewma_fit(_p(x), S, T, T, _p(sm), err.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), threads)
     return sm, err
+
+
+def panel_garch_fit(x, threads: int = 1):
+    x = _panel(x); S, T = x.shape; par = np.empty((S, 3)); err = np.zeros(S, np.int32)
+    lib().orc_panel_garch_fit(_p(x), S, T, T, _p(par), err.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), threads)
+    return par, err
+
+
+def panel_argarch_fit(x, threads: int = 1):
+    x = _panel(x); S, T = x.shape; par = np.empty((S, 5)); err = np.zeros(S, np.int32)
+    lib().orc_panel_argarch_fit(_p(x), S, T, T, _p(par), err.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), threads)
+    return par, err
 
 
 # ---------------- generator ----------------

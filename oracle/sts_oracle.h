@@ -67,6 +67,26 @@ void orc_to_instants(const double* in, int64_t S, int64_t T, int64_t ld, double*
 int  orc_ols_householder(const double* y, const double* x /* m x k row-major */, int64_t m,
                          int k, int no_intercept, double* beta /* k(+1) */);
 
+/* ---- GARCH(1,1), AR(1)+GARCH(1,1): sts_oracle_garch.c (S/models/GARCH.scala) ---- */
+double orc_fdlibm_log(double x);   /* StrictMath.log */
+double orc_garch_loglik(const double* ts, int64_t n, double omega, double alpha, double beta);
+void orc_garch_gradient(const double* ts, int64_t n, double omega, double alpha, double beta,
+                        double g[3]);
+int  orc_garch_fit(const double* ts, int64_t n, double params[3] /* omega, alpha, beta */,
+                   int64_t* evaluations);
+int  orc_argarch_fit(const double* ts, int64_t n, double out[5] /* c, phi, omega, alpha, beta */,
+                     int64_t* evaluations);
+void orc_garch_remove(const double* ts, double* dest, int64_t n, double omega, double alpha, double beta);
+void orc_garch_add(const double* ts, double* dest, int64_t n, double omega, double alpha, double beta);
+void orc_argarch_remove(const double* ts, double* dest, int64_t n, double c, double phi,
+                        double omega, double alpha, double beta);
+void orc_argarch_add(const double* ts, double* dest, int64_t n, double c, double phi,
+                     double omega, double alpha, double beta);
+int  orc_panel_garch_fit(const double* in, int64_t S, int64_t T, int64_t ld, double* params,
+                         int32_t* err, int threads);
+int  orc_panel_argarch_fit(const double* in, int64_t S, int64_t T, int64_t ld, double* params,
+                           int32_t* err, int threads);
+
 /* ---- panel drivers (threads = 0 -> 1 thread) ---- */
 int orc_panel_fill(const double* in, double* out, int64_t S, int64_t T, int64_t ld, int method,
                    int32_t* err, int threads);

@@ -549,6 +549,115 @@ int sts_ewma_sse_gradient(const double* in, int64_t S, int64_t T, int64_t ld, co
     return STS_OK;
 }
 
+// ---- GARCH(1,1) / AR(1)+GARCH(1,1): S/models/GARCH.scala ----
+
+int sts_garch_fit(const double* in, int64_t S, int64_t T, int64_t ld, double* params, int32_t* err_per_series,
+                  void* stream) {
+    int r;
+    if ((r = check_panel(in, S, T, ld, "GARCH.fitModel"))) return r;
+    if (S > 0 && !params) return fail(STS_ERR_BAD_ARG, "GARCH.fitModel: null output");
+    if (S == 0) return STS_OK;
+    if ((r = ensure_device())) return r;
+    hipStream_t st = as_stream(stream);
+    ErrSink es(err_per_series, S, st);
+    if ((r = es.prepare())) return r;
+    sts::GarchFitArgs a{};
+    a.in = in; a.S = S; a.T = T; a.ld = ld; a.params = params; a.err = es.dev;
+    HIP_TRY(timed(st, [&] { return sts::launch_garch_fit(a, true, st); }), "GARCH.fitModel");
+    return es.finish("GARCH.fitModel");
+}
+
+int sts_garch_loglik_gradient(const double* in, int64_t S, int64_t T, int64_t ld, const double* params,
+                              double* loglik, double* gradient, void* stream) {
+    int r;
+    if ((r = check_panel(in, S, T, ld, "GARCHModel.logLikelihood"))) return r;
+    if (S > 0 && !params) return fail(STS_ERR_BAD_ARG, "GARCHModel.logLikelihood: null params");
+    if (S == 0 || (!loglik && !gradient)) return STS_OK;
+    if ((r = ensure_device())) return r;
+    hipStream_t st = as_stream(stream);
+    sts::GarchFitArgs a{};
+    a.in = in; a.S = S; a.T = T; a.ld = ld; a.params = const_cast<double*>(params);
+    a.loglik = loglik; a.grad = gradient;
+    HIP_TRY(timed(st, [&] { return sts::launch_garch_fit(a, false, st); }), "GARCHModel.logLikelihood/gradient");
+    return STS_OK;
+}
+
+static int garch_effects(int op, const double* in, double* out, int64_t S, int64_t T, int64_t ld_in, int64_t ld_out,
+                         const double* c, const double* phi, const double* omega, const double* alpha,
+                         const double* beta, void* stream, const char* name) {
+    int r;
+    if ((r = check_panel(in, S, T, ld_in, name))) return r;
+    if (!out) return fail(STS_ERR_NULL_DEST, "%s: dest is null (the reference writes into dest)", name);
+    if ((r = check_panel(out, S, T, ld_out, name))) return r;
+    if (S > 0 && (!omega || !alpha || !beta)) return fail(STS_ERR_BAD_ARG, "%s: null model parameters", name);
+    const bool ar = op != sts::kGarchRemove && op != sts::kGarchAdd;
+    if (S > 0 && ar && (!c || !phi)) return fail(STS_ERR_BAD_ARG, "%s: null model parameters", name);
+    if (S * T == 0) return STS_OK;
+    if (in == out && ld_in != ld_out) return fail(STS_ERR_BAD_ARG, "%s: in place needs ld_in == ld_out", name);
+    if (op == sts::kArgarchRemove && in == out) op = sts::kArgarchRemoveInplace;   // dest eq ts
+    if ((r = ensure_device())) return r;
+    hipStream_t st = as_stream(stream);
+    sts::GarchEffectsArgs a{};
+    a.in = in; a.out = out; a.S = S; a.T = T; a.ld_in = ld_in; a.ld_out = ld_out;
+    a.c = c; a.phi = phi; a.omega = omega; a.alpha = alpha; a.beta = beta;
+    HIP_TRY(timed(st, [&] { return sts::launch_garch_effects(op, a, st); }), name);
+    return STS_OK;
+}
+
+int sts_garch_remove(const double* in, double* out, int64_t S, int64_t T, int64_t ld_in, int64_t ld_out,
+                     const double* omega, const double* alpha, const double* beta, void* stream) {
+    return garch_effects(sts::kGarchRemove, in, out, S, T, ld_in, ld_out, nullptr, nullptr, omega, alpha, beta,
+                         stream, "GARCHModel.removeTimeDependentEffects");
+}
+
+int sts_garch_add(const double* in, double* out, int64_t S, int64_t T, int64_t ld_in, int64_t ld_out,
+                  const double* omega, const double* alpha, const double* beta, void* stream) {
+    return garch_effects(sts::kGarchAdd, in, out, S, T, ld_in, ld_out, nullptr, nullptr, omega, alpha, beta, stream,
+                         "GARCHModel.addTimeDependentEffects");
+}
+
+int sts_argarch_remove(const double* in, double* out, int64_t S, int64_t T, int64_t ld_in, int64_t ld_out,
+                       const double* c, const double* phi, const double* omega, const double* alpha,
+                       const double* beta, void* stream) {
+    return garch_effects(sts::kArgarchRemove, in, out, S, T, ld_in, ld_out, c, phi, omega, alpha, beta, stream,
+                         "ARGARCHModel.removeTimeDependentEffects");
+}
+
+int sts_argarch_add(const double* in, double* out, int64_t S, int64_t T, int64_t ld_in, int64_t ld_out,
+                    const double* c, const double* phi, const double* omega, const double* alpha,
+                    const double* beta, void* stream) {
+    return garch_effects(sts::kArgarchAdd, in, out, S, T, ld_in, ld_out, c, phi, omega, alpha, beta, stream,
+                         "ARGARCHModel.addTimeDependentEffects");
+}
+
+int sts_argarch_fit(const double* in, int64_t S, int64_t T, int64_t ld, double* c, double* phi, double* params,
+                    int32_t* err_per_series, void* stream) {
+    int r;
+    if ((r = check_panel(in, S, T, ld, "ARGARCH.fitModel"))) return r;
+    if (S > 0 && (!c || !phi || !params)) return fail(STS_ERR_BAD_ARG, "ARGARCH.fitModel: null output");
+    if (T - 1 < 2)
+        return fail(STS_ERR_NOT_ENOUGH_DATA, "ARGARCH.fitModel: not enough data (%lld rows) for the number of predictors (1)",
+                    (long long)(T - 1));
+    if (S == 0) return STS_OK;
+    if ((r = ensure_device())) return r;
+    hipStream_t st = as_stream(stream);
+    ErrSink es(err_per_series, S, st);
+    if ((r = es.prepare())) return r;
+    // Autoregression.fitModel(ts) = AR(1) with intercept; residuals into dest = zeros(n)
+    Scratch resid(st);
+    HIP_TRY(resid.alloc((size_t)(S * T) * sizeof(double)), "hipMallocAsync(argarch)");
+    double* rs = static_cast<double*>(resid.p);
+    sts::ArArgs ar{};
+    ar.in = in; ar.out = rs; ar.c = c; ar.coef = phi; ar.err = es.dev;
+    ar.S = S; ar.T = T; ar.ld_in = ld; ar.ld_out = T; ar.p = 1; ar.no_intercept = 0;
+    HIP_TRY(timed(st, [&] { return sts::launch_ar_fit(ar, st); }), "ARGARCH.fitModel (AR stage)");
+    // GARCH.fitModel(residuals); an AR-stage failure keeps its status
+    sts::GarchFitArgs g{};
+    g.in = rs; g.S = S; g.T = T; g.ld = T; g.params = params; g.err = es.dev; g.keep_err = 1;
+    HIP_TRY(timed(st, [&] { return sts::launch_garch_fit(g, true, st); }), "ARGARCH.fitModel (GARCH stage)");
+    return es.finish("ARGARCH.fitModel");
+}
+
 int sts_series_stats(const double* in, int64_t S, int64_t T, int64_t ld, double* stats, void* stream) {
     int r;
     if ((r = check_panel(in, S, T, ld, "seriesStats"))) return r;

@@ -144,6 +144,35 @@ int sts_ar_fit_host(const double* in, int64_t S, int64_t T, int64_t ld, int p, i
     return finish(r);
 }
 
+int sts_garch_fit_host(const double* in, int64_t S, int64_t T, int64_t ld, double* params, int32_t* err) {
+    Dev di, dp, de;
+    int r;
+    if ((r = up(di, in, panel_bytes(S, ld))) || (r = up(dp, nullptr, (size_t)S * 3 * sizeof(double))) ||
+        (r = up(de, nullptr, (size_t)S * sizeof(int32_t))))
+        return finish(r);
+    r = sts_garch_fit(di.as<double>(), S, T, ld, dp.as<double>(), err ? de.as<int32_t>() : nullptr, kStream);
+    if (r == STS_OK) r = down(params, dp, (size_t)S * 3 * sizeof(double));
+    if (r == STS_OK) r = down(err, de, (size_t)S * sizeof(int32_t));
+    return finish(r);
+}
+
+int sts_argarch_fit_host(const double* in, int64_t S, int64_t T, int64_t ld, double* c, double* phi,
+                         double* params, int32_t* err) {
+    Dev di, dc, dphi, dp, de;
+    int r;
+    if ((r = up(di, in, panel_bytes(S, ld))) || (r = up(dc, nullptr, (size_t)S * sizeof(double))) ||
+        (r = up(dphi, nullptr, (size_t)S * sizeof(double))) ||
+        (r = up(dp, nullptr, (size_t)S * 3 * sizeof(double))) || (r = up(de, nullptr, (size_t)S * sizeof(int32_t))))
+        return finish(r);
+    r = sts_argarch_fit(di.as<double>(), S, T, ld, dc.as<double>(), dphi.as<double>(), dp.as<double>(),
+                        err ? de.as<int32_t>() : nullptr, kStream);
+    if (r == STS_OK) r = down(c, dc, (size_t)S * sizeof(double));
+    if (r == STS_OK) r = down(phi, dphi, (size_t)S * sizeof(double));
+    if (r == STS_OK) r = down(params, dp, (size_t)S * 3 * sizeof(double));
+    if (r == STS_OK) r = down(err, de, (size_t)S * sizeof(int32_t));
+    return finish(r);
+}
+
 static int ar_host(bool add, const double* in, double* out, int64_t S, int64_t T, int64_t ld, const double* c,
                    const double* coef, int p) {
     Dev di, dout, dc, dk;

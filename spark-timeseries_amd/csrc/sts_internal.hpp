@@ -108,6 +108,28 @@ struct EwmaFitArgs {
 };
 hipError_t launch_ewma_fit(const EwmaFitArgs& a, bool fit, hipStream_t st);
 
+// GARCH.fitModel / GARCHModel.logLikelihood + gradient and the GARCH / ARGARCH
+// time-dependent effects (sts_garch.hip)
+struct GarchFitArgs {
+    const double* in;
+    int64_t S, T, ld;
+    double* params;       // S x 3 (omega, alpha, beta): fit output / evaluation input
+    int32_t* err;         // fit: per-series status (optional)
+    int keep_err;         // fit: leave a nonzero err entry as it is (ARGARCH: the AR stage's)
+    int32_t* evals;       // fit: commons-math3 evaluation count (optional)
+    double* loglik;       // evaluation: S
+    double* grad;         // evaluation: S x 3, the reference's (alpha, beta, omega) order
+};
+hipError_t launch_garch_fit(const GarchFitArgs& a, bool fit, hipStream_t st);
+enum GarchOp { kGarchRemove = 0, kGarchAdd = 1, kArgarchRemove = 2, kArgarchRemoveInplace = 3, kArgarchAdd = 4 };
+struct GarchEffectsArgs {
+    const double* in;
+    double* out;
+    int64_t S, T, ld_in, ld_out;
+    const double *c, *phi, *omega, *alpha, *beta;   // per series (c, phi: ARGARCH only)
+};
+hipError_t launch_garch_effects(int op, const GarchEffectsArgs& a, hipStream_t st);
+
 // seriesStats / removeInstantsWithNaNs / toInstants (sts_instants.hip)
 hipError_t launch_series_stats(const double* in, double* out, int64_t S, int64_t T, int64_t ld, hipStream_t st);
 hipError_t launch_nan_instants(const double* in, uint8_t* flags, int64_t S, int64_t T, int64_t ld, hipStream_t st);

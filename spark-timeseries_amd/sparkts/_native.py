@@ -47,6 +47,13 @@ SIGNATURES = {
                                    _c_vp, _c_vp]),
     "sts_ewma_fit": (_c_int, [_c_vp, _c_i64, _c_i64, _c_i64, _c_vp, _c_vp, _c_vp]),
     "sts_ewma_sse_gradient": (_c_int, [_c_vp, _c_i64, _c_i64, _c_i64, _c_vp, _c_vp, _c_vp, _c_vp]),
+    "sts_garch_fit": (_c_int, [_c_vp, _c_i64, _c_i64, _c_i64, _c_vp, _c_vp, _c_vp]),
+    "sts_garch_loglik_gradient": (_c_int, [_c_vp, _c_i64, _c_i64, _c_i64, _c_vp, _c_vp, _c_vp, _c_vp]),
+    "sts_garch_remove": (_c_int, [_c_vp, _c_vp, _c_i64, _c_i64, _c_i64, _c_i64, _c_vp, _c_vp, _c_vp, _c_vp]),
+    "sts_garch_add": (_c_int, [_c_vp, _c_vp, _c_i64, _c_i64, _c_i64, _c_i64, _c_vp, _c_vp, _c_vp, _c_vp]),
+    "sts_argarch_remove": (_c_int, [_c_vp, _c_vp, _c_i64, _c_i64, _c_i64, _c_i64] + [_c_vp] * 6),
+    "sts_argarch_add": (_c_int, [_c_vp, _c_vp, _c_i64, _c_i64, _c_i64, _c_i64] + [_c_vp] * 6),
+    "sts_argarch_fit": (_c_int, [_c_vp, _c_i64, _c_i64, _c_i64, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp]),
     "sts_series_stats": (_c_int, [_c_vp, _c_i64, _c_i64, _c_i64, _c_vp, _c_vp]),
     "sts_nan_instants": (_c_int, [_c_vp, _c_i64, _c_i64, _c_i64, _c_vp, _c_vp]),
     "sts_active_instants": (_c_int, [_c_vp, _c_i64, _c_vp, _c_vp, _c_vp]),
@@ -67,6 +74,8 @@ SIGNATURES = {
     "sts_ewma_add_host": (_c_int, [_c_vp, _c_vp, _c_i64, _c_i64, _c_i64, _c_vp]),
     "sts_ewma_remove_host": (_c_int, [_c_vp, _c_vp, _c_i64, _c_i64, _c_i64, _c_vp]),
     "sts_ewma_fit_host": (_c_int, [_c_vp, _c_i64, _c_i64, _c_i64, _c_vp, _c_vp]),
+    "sts_garch_fit_host": (_c_int, [_c_vp, _c_i64, _c_i64, _c_i64, _c_vp, _c_vp]),
+    "sts_argarch_fit_host": (_c_int, [_c_vp, _c_i64, _c_i64, _c_i64, _c_vp, _c_vp, _c_vp, _c_vp]),
     "sts_ar_fit_host": (_c_int, [_c_vp, _c_i64, _c_i64, _c_i64, _c_int, _c_int, _c_vp, _c_vp, _c_vp]),
     "sts_ar_remove_host": (_c_int, [_c_vp, _c_vp, _c_i64, _c_i64, _c_i64, _c_vp, _c_vp, _c_int]),
     "sts_ar_add_host": (_c_int, [_c_vp, _c_vp, _c_i64, _c_i64, _c_i64, _c_vp, _c_vp, _c_int]),
