@@ -38,6 +38,9 @@ WORKLOADS = {
     "ewma_fit": (1_000_000, 390, 0.0, 6,
                  "EWMA.fitModel (SURVEY.md 8(f) rank 1): commons-math3 NLCG + bracket + Brent per series, "
                  "1,000,000 series x 390 steps (the C2 shape)"),
+    "garch_fit": (100_000, 2_520, 0.0, 11,
+                  "GARCH.fitModel (SURVEY.md 8(f) rank 1): commons-math3 NLCG (3-D, goal-less) + bracket + Brent per "
+                  "series, 100,000 series x 2,520 steps (x - x[:, 0] of the generated panel)"),
     "stats": (1_000_000, 390, 0.0, 7, "TimeSeriesRDD.seriesStats (Spark StatCounter per series), "
               "1,000,000 series x 390 steps (the C2 shape)"),
     "nan_instants": (1_000_000, 390, 0.0, 8,
@@ -113,6 +116,9 @@ def main():
         smooth = torch.empty((S,), dtype=torch.float64, device=dev)
     if args.workload == "stats":
         stats = torch.empty((S, 4), dtype=torch.float64, device=dev)
+    if args.workload == "garch_fit":
+        x -= x[:, :1].clone()                      # return-like rows around 0 (exact, same on the CPU side)
+        gpar = torch.empty((S, 3), dtype=torch.float64, device=dev)
     if args.workload == "nan_instants":
         x[::997, ::10] = float("nan")              # every 10th instant has a NaN somewhere
         flags = torch.zeros(T, dtype=torch.uint8, device=dev)
@@ -164,6 +170,11 @@ def main():
                              "wire_decode")
         elif args.workload == "to_instants":
             raise_for_status(lib.sts_to_instants(x.data_ptr(), inst.data_ptr(), S, T, T, S, sp), "toInstants")
+        elif args.workload == "garch_fit":
+            raise_for_status(lib.sts_garch_fit(x.data_ptr(), S, T, T, gpar.data_ptr(), err.data_ptr(), sp),
+                             "GARCH.fitModel")
+            if world > 1:
+                all_gather_results(gpar)
         elif args.workload == "ewma_fit":
             raise_for_status(lib.sts_ewma_fit(x.data_ptr(), S, T, T, smooth.data_ptr(), err.data_ptr(), sp),
                              "EWMA.fitModel")
@@ -214,6 +225,8 @@ def main():
         bytes_per_step += 8.0 * P * (T - P) * S
     if args.workload == "ewma_fit":      # the series read once + one parameter written (algorithmic)
         bytes_per_step = 8.0 * S * T + 8.0 * S
+    if args.workload == "garch_fit":     # the series read once + three parameters written (algorithmic)
+        bytes_per_step = 8.0 * S * T + 24.0 * S
     if args.workload == "stats":         # read once + 4 doubles per series
         bytes_per_step = 8.0 * S * T + 32.0 * S
     if args.workload == "nan_instants":  # flag pass reads everything; the gather reads + writes kept values
@@ -227,6 +240,8 @@ def main():
               "nan_instants": "sts::nan_instants_kernel + sts::gather_instants_kernel",
               "to_instants": "sts::transpose_kernel (64x64 LDS tiles)",
               "wire_decode": "sts::wire_decode_kernel (big-endian value blocks -> panel)",
+              "garch_fit": "sts::garch_fit_kernel<32,64> (lane-per-series commons-math3 optimizer; one "
+                           "logLikelihood+gradient pass over the wave's series block per optimizer request)",
               "ewma_fit": "sts::ewma_fit_kernel<32,64> (lane-per-series commons-math3 optimizer; one sse+gradient "
                           "pass over the wave's series block per optimizer request)"}[args.workload]
     roofline = None
@@ -242,7 +257,8 @@ def main():
 
     cpu = None
     if rank == 0 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(args, S, T, K, seed, nan_p, out, acf, p_ar, smooth)
+        cpu = cpu_baseline(args, S, T, K, seed, nan_p, out, acf, p_ar, smooth,
+                           gpar if args.workload == "garch_fit" else None)
 
     if rank == 0:
         line = {
@@ -254,7 +270,7 @@ def main():
             "config": {"workload": desc, "series_per_gpu": S, "steps_per_series": T,
                        "numLags": K if args.workload in ("c3", "c1") else None,
                        "fill": {"c3": "linear", "c1": "linear", "c2": "previous", "c4": None, "c5": "nearest",
-                                "ewma_fit": None, "stats": None, "nan_instants": None,
+                                "ewma_fit": None, "garch_fit": None, "stats": None, "nan_instants": None,
                                 "to_instants": None, "wire_decode": None}[args.workload],
                        "parallelism": "dp%d (series sharded by key, one process per GPU)" % world},
             "roofline": roofline,
@@ -280,7 +296,7 @@ def measured_traffic(workload, S, T):
     return rec.get("traffic_bytes_per_launch")
 
 
-def cpu_baseline(args, S, T, K, seed, nan_p, out, acf, p_ar, smooth=None):
+def cpu_baseline(args, S, T, K, seed, nan_p, out, acf, p_ar, smooth=None, gpar_ref=None):
     """The oracle (CPU restatement of the reference loops, oracle/) on a bounded sample of
     the same workload, one series per thread like Spark local[N].  The sample series are
     the rank-0 series 0..n-1, so their GPU results are also checked here."""
@@ -313,6 +329,9 @@ def cpu_baseline(args, S, T, K, seed, nan_p, out, acf, p_ar, smooth=None):
                 oracle.lag(r, 10, False)
         elif args.workload == "ewma_fit":
             rf, _ = oracle.panel_ewma_fit(xs, threads=threads)
+        elif args.workload == "garch_fit":
+            xs = xs - xs[:, :1]
+            rf, _ = oracle.panel_garch_fit(xs, threads=threads)
         elif args.workload in ("stats", "nan_instants", "to_instants", "wire_decode"):
             rf = None
             if args.workload == "stats":
@@ -333,7 +352,7 @@ def cpu_baseline(args, S, T, K, seed, nan_p, out, acf, p_ar, smooth=None):
             rf, _, _ = oracle.panel_ar_fit_remove(xs, p_ar, threads=threads)
         elapsed += time.perf_counter() - t0
         if s_next == 0 and rf is not None:
-            g = (smooth[:n] if args.workload == "ewma_fit" else out[:n]).cpu().numpy()
+            g = {"ewma_fit": smooth, "garch_fit": gpar_ref}.get(args.workload, out)[:n].cpu().numpy()
             if args.workload != "c4":
                 exact = bool(np.array_equal(np.isnan(g), np.isnan(rf)) and
                              np.array_equal(np.nan_to_num(g), np.nan_to_num(rf)))

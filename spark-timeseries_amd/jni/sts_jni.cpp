@@ -137,6 +137,29 @@ JNIEXPORT void JNICALL Java_com_cloudera_sparkts_StsNative_ewmaFit(JNIEnv* env, 
     throw_for(env, st);
 }
 
+// GARCH.fitModel per series (S/models/GARCH.scala:33-53): params = S x (omega, alpha, beta)
+JNIEXPORT void JNICALL Java_com_cloudera_sparkts_StsNative_garchFit(JNIEnv* env, jclass, jdoubleArray in, jlong S,
+                                                                     jlong T, jdoubleArray params) {
+    int st;
+    {
+        Pinned pi(env, in), pp(env, params);
+        st = sts_garch_fit_host(pi.d(), S, T, T, pp.d(), nullptr);
+    }
+    throw_for(env, st);
+}
+
+// ARGARCH.fitModel per series (S/models/GARCH.scala:62-68): c, phi (S) and params (S x 3)
+JNIEXPORT void JNICALL Java_com_cloudera_sparkts_StsNative_argarchFit(JNIEnv* env, jclass, jdoubleArray in, jlong S,
+                                                                       jlong T, jdoubleArray c, jdoubleArray phi,
+                                                                       jdoubleArray params) {
+    int st;
+    {
+        Pinned pi(env, in), pc(env, c), pf(env, phi), pp(env, params);
+        st = sts_argarch_fit_host(pi.d(), S, T, T, pc.d(), pf.d(), pp.d(), nullptr);
+    }
+    throw_for(env, st);
+}
+
 JNIEXPORT void JNICALL Java_com_cloudera_sparkts_StsNative_arFit(JNIEnv* env, jclass, jdoubleArray in, jlong S,
                                                                   jlong T, jint p, jboolean noIntercept,
                                                                   jdoubleArray c, jdoubleArray coef) {

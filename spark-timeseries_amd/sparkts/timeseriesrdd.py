@@ -113,6 +113,10 @@ class TimeSeriesRDD:
         instants are re-partitioned by time with an all-to-all (RCCL over xGMI), so rank r
         returns instants [t0_r, t1_r) (shard_range over T) of ALL series -- Spark's
         toInstants shuffle.  Returns (index slice, (T_r, S_total) tensor)."""
+        index, got, _ = self._instants(group)
+        return index, got
+
+    def _instants(self, group=None):
         import torch
         p = Panel(self.data)
         if not p.device:
@@ -126,7 +130,24 @@ class TimeSeriesRDD:
                 index = index[t0:t1]
             except (TypeError, IndexError, KeyError):
                 index = None
-        return index, got
+        return index, got, t0
+
+    def toRowMatrix(self, group=None):
+        """S/TimeSeriesRDD.scala:410-414: the toInstants rows without their instants (a
+        RowMatrix's row order carries no meaning).  Returns this rank's (T_r, S_total) rows."""
+        return self.toInstants(group)[1]
+
+    def toIndexedRowMatrix(self, group=None):
+        """S/TimeSeriesRDD.scala:385-400: toInstants rows indexed by frequency.difference(
+        first, instant), i.e. the instant's position in a uniform index.  Non-uniform indices
+        raise UnsupportedOperationException("only supported for uniform indices") as the
+        reference does.  Returns (row indices int64 (T_r,), (T_r, S_total) rows)."""
+        from .errors import UnsupportedOperationException
+        if not _is_uniform(self.index):
+            raise UnsupportedOperationException("only supported for uniform indices")
+        import torch
+        _, rows, t0 = self._instants(group)
+        return torch.arange(t0, t0 + rows.shape[0], dtype=torch.int64, device=rows.device), rows
 
     def collectAsTimeSeries(self):
         """(index, keys, (T, S) column-major matrix) like S/TimeSeriesRDD.scala:62-74."""
@@ -230,3 +251,21 @@ def all_gather_results(local, group=None):
     bufs = [torch.empty_like(pad) for _ in range(world)]
     dist.all_gather(bufs, pad, group=group)
     return torch.cat([b[:k] for b, k in zip(bufs, sizes)], dim=0)
+
+
+def _is_uniform(index) -> bool:
+    """A UniformDateTimeIndex analogue: None (positions), a range, or instants with one
+    constant spacing (numpy datetime64 / numbers / ISO date strings)."""
+    import numpy as np
+    if index is None or isinstance(index, range):
+        return True
+    try:
+        a = np.asarray(index)
+        if a.dtype.kind in "US":
+            a = a.astype("datetime64[ns]")
+        if a.size < 3:
+            return True
+        d = np.diff(a)
+        return bool((d == d[0]).all())
+    except (TypeError, ValueError):
+        return False

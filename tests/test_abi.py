@@ -99,3 +99,16 @@ def test_argument_errors_need_no_device(lib):
     from sparkts.errors import IllegalArgumentException
     with pytest.raises(IllegalArgumentException, match="starting index cannot be less than lag"):
         uts.differencesAtLag(np.arange(5.0), 3, startIndex=1)
+
+
+def test_indexed_row_matrix_needs_uniform_index():
+    # S/TimeSeriesRDD.scala:386-388: UnsupportedOperationException for non-uniform indices,
+    # raised before any device work
+    import numpy as np
+    from sparkts.errors import UnsupportedOperationException
+    from sparkts.timeseriesrdd import TimeSeriesRDD, _is_uniform
+    assert _is_uniform(None) and _is_uniform(np.array(["2015-04-09", "2015-04-10", "2015-04-11"]))
+    irregular = np.array(["2015-04-09", "2015-04-10", "2015-04-12"])
+    assert not _is_uniform(irregular)
+    with pytest.raises(UnsupportedOperationException, match="only supported for uniform indices"):
+        TimeSeriesRDD(irregular, None, np.zeros((2, 3))).toIndexedRowMatrix()

@@ -721,6 +721,21 @@ def test_to_instants(torch):
         assert_bits(host(inst), oracle.to_instants(x), "toInstants %dx%d" % (S, T))
 
 
+def test_to_row_matrices(torch):
+    # S/TimeSeriesRDD.scala:385-414: toInstants rows; IndexedRowMatrix row i = instant i
+    from sparkts.errors import UnsupportedOperationException
+    from sparkts.timeseriesrdd import TimeSeriesRDD
+    x = np.random.default_rng(6).standard_normal((9, 33))
+    days = np.datetime64("2015-04-09") + np.arange(33)
+    rdd = TimeSeriesRDD(days.astype(str), None, dev(torch, x))
+    assert_bits(host(rdd.toRowMatrix()), x.T, "toRowMatrix")
+    ri, rows = rdd.toIndexedRowMatrix()
+    assert np.array_equal(host(ri), np.arange(33)) and np.array_equal(host(rows), x.T)
+    days = np.array(["2015-04-09", "2015-04-10", "2015-04-12"])
+    with pytest.raises(UnsupportedOperationException, match="only supported for uniform indices"):
+        TimeSeriesRDD(days, None, dev(torch, x[:, :3])).toIndexedRowMatrix()
+
+
 # ---------------- ingest / egress formats: bit-exact ----------------
 
 def test_wire_decode_encode_round_trip(torch):
