@@ -119,6 +119,14 @@ struct GarchFitArgs {
     int32_t* evals;       // fit: commons-math3 evaluation count (optional)
     double* loglik;       // evaluation: S
     double* grad;         // evaluation: S x 3, the reference's (alpha, beta, omega) order
+    // fit, MaxEval tail (set by launch_garch_fit): a lane still running after pass_budget
+    // passes parks its optimizer state in park[slot] (slot from park_ctr[0], < park_cap)
+    // and garch_tail_kernel finishes it, one wave per series (park_ctr[1]: its work queue)
+    void* park;           // park_cap x GarchOpt
+    int64_t* park_ids;    // series of each slot
+    int32_t* park_ctr;
+    int park_cap;
+    int pass_budget;      // 0: no tail phase
 };
 hipError_t launch_garch_fit(const GarchFitArgs& a, bool fit, hipStream_t st);
 enum GarchOp { kGarchRemove = 0, kGarchAdd = 1, kArgarchRemove = 2, kArgarchRemoveInplace = 3, kArgarchAdd = 4 };
