@@ -29,6 +29,8 @@
 
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 namespace sts {
 namespace {
 
@@ -91,9 +93,10 @@ __global__ __launch_bounds__(64) void garch_fit_kernel(GarchFitArgs a) {
         o.req[1] = a.params[3 * sl + 1];
         o.req[2] = a.params[3 * sl + 2];
     }
-    bool first = true;
+    bool first = true, parked = false;
+    int passes = 0;
     for (;;) {
-        const bool pending = live && o.status < 0;
+        const bool pending = live && o.status < 0 && !parked;
         const unsigned long long want = __ballot(pending);
         if (want == 0) break;
         GarchEval g;
@@ -139,11 +142,20 @@ __global__ __launch_bounds__(64) void garch_fit_kernel(GarchFitArgs a) {
             } else {
                 garch_cache_insert(o);
                 garch_advance(o);
+                // past its pass budget: hand the series to garch_tail_kernel
+                if (a.pass_budget > 0 && o.status < 0 && ++passes == a.pass_budget) {
+                    const int slot = atomicAdd(a.park_ctr, 1);
+                    if (slot < a.park_cap) {
+                        static_cast<GarchOpt*>(a.park)[slot] = o;
+                        a.park_ids[slot] = sl;
+                        parked = true;
+                    }
+                }
             }
         }
         first = false;
     }
-    if (!live) return;
+    if (!live || parked) return;
     if (FIT) {
         const bool ok = o.status == STS_OK;
         for (int j = 0; j < 3; j++) a.params[3 * sl + j] = ok ? o.point[j] : __builtin_nan("");
@@ -153,6 +165,163 @@ __global__ __launch_bounds__(64) void garch_fit_kernel(GarchFitArgs a) {
         if (a.loglik) a.loglik[sl] = o.res_f;
         if (a.grad)
             for (int j = 0; j < 3; j++) a.grad[3 * sl + j] = o.res_g[j];
+    }
+}
+
+// ---- MaxEval tail: one wave per parked series ------------------------------------------
+//
+// A few series need thousands of optimizer passes (up to MaxEval = 10000 evaluations); in
+// garch_fit_kernel each pass is one lane's sequential walk over its series, so those lanes
+// set the launch time.  Here a whole wave evaluates one series.  The pass (GarchEval::run)
+// is a set of first-order recurrences
+//     h_t  = (omega + alpha x_{t-1} x_{t-1}) + beta h_{t-1}
+//     oD_t = 1 + beta oD_{t-1}    aD_t = x_{t-1} x_{t-1} + beta aD_{t-1}    bD_t = h_{t-1} + beta bD_{t-1}
+//     sum += term_t    oG += m_t oD_t    aG += m_t aD_t    bG += m_t bD_t
+// whose costly parts (term_t: fdlibm log + a division, m_t: two divisions) depend only on
+// h_t and x_t.  Every chain has the form y = u_t + b y, with b = beta or, for the sums, b = 1
+// (1 * y is exact and + commutes, so `sum += term` is u + 1 * y bit for bit).  Lanes 0-7 run
+// the eight chains as ONE instruction stream, each from its own u array in LDS, pipelined
+// over C-step chunks: in iteration j lanes 0-2 run h / oD / aD of chunk j, lanes 3-4 bD and
+// sum of chunk j - 1, lanes 5-7 the gradient sums of chunk j - 2.  Before each chain loop
+// all 64 lanes compute the chunk-parallel inputs: u of chunk j, term / m / h_{t-1} of chunk
+// j - 1, the products m oD, m aD, m bD of chunk j - 2.  Same operations, same order as
+// GarchEval, so the pass is bit-identical and the optimizer path unchanged.
+template <int C>
+struct TailLds {
+    static constexpr int kSlots = 3 * C + 2;   // 3 chunk slots; +2 doubles skews the arrays' banks
+    double a[13][kSlots];                       // UH XX ETA H OD AD TERM M UB BD PO PA PB
+    double one[C + 2];                          // u of the oD chain
+    double sink[C];                             // chain outputs nobody reads (the sums)
+};
+
+template <int C>
+__device__ __forceinline__ void garch_tail_pass(const double* __restrict__ x, int64_t T, GarchOpt& o,
+                                                TailLds<C>& L) {
+    enum { UH, XX, ETA, H, OD, AD, TERM, M, UB, BD, PO, PA, PB };
+    const int lane = threadIdx.x;
+    const double omega = o.req[0], alpha = o.req[1], beta = o.req[2];
+    const int64_t nsteps = T > 1 ? T - 1 : 0;      // steps t = 1 .. T-1
+    const int nc = (int)((nsteps + C - 1) / C);
+    const int rem = (int)(nsteps - (int64_t)(nc - 1) * C);   // length of the last chunk
+    const double h0 = omega / (1 - alpha - beta);
+    // chain roles: lane -> (u array, output array, b, chunk lag)
+    const int lag = lane < 3 ? 0 : lane < 5 ? 1 : 2;
+    const double b = lane < 4 ? beta : 1.0;
+    const int u_arr = lane == 0 ? UH : lane == 1 ? -1 : lane == 2 ? XX : lane == 3 ? UB : lane == 4 ? TERM
+                    : lane == 5 ? PO : lane == 6 ? PA : PB;
+    const int w_arr = lane == 0 ? H : lane == 1 ? OD : lane == 2 ? AD : lane == 3 ? BD : -1;
+    double y = lane == 0 ? h0 : 0.0;
+    for (int i = lane; i < C; i += 64) L.one[i] = 1.0;
+    // prefetch of chunk 0's x_{t-1}, x_t
+    constexpr int NP = C / 64;
+    double xp[NP], xe[NP];
+    auto fetch = [&](int j) {
+#pragma unroll
+        for (int k = 0; k < NP; k++) {
+            const int64_t t = 1 + (int64_t)j * C + k * 64 + lane;
+            xp[k] = (j < nc && t < T) ? x[t - 1] : 0.0;
+            xe[k] = (j < nc && t < T) ? x[t] : 0.0;
+        }
+    };
+    fetch(0);
+    for (int j = 0; j < nc + 2; j++) {
+        const int s0 = (j % 3) * C, s1 = ((j + 2) % 3) * C, s2 = ((j + 1) % 3) * C;   // chunks j, j-1, j-2
+        if (j < nc) {   // chunk j: the chain inputs that need only x
+#pragma unroll
+            for (int k = 0; k < NP; k++) {
+                const int i = k * 64 + lane;
+                L.a[UH][s0 + i] = omega + alpha * xp[k] * xp[k];
+                L.a[XX][s0 + i] = xp[k] * xp[k];
+                L.a[ETA][s0 + i] = xe[k];
+            }
+            fetch(j + 1);
+        }
+        if (j >= 1 && j - 1 < nc) {   // chunk j - 1: log-likelihood terms, multipliers, h_{t-1}
+            const double hprev = j == 1 ? h0 : L.a[H][s2 + C - 1];
+            const int len = j - 1 == nc - 1 ? rem : C;
+#pragma unroll
+            for (int k = 0; k < NP; k++) {
+                const int i = k * 64 + lane;
+                if (i < len) {
+                    const double h = L.a[H][s1 + i], eta = L.a[ETA][s1 + i];
+                    L.a[TERM][s1 + i] = -.5 * fdlibm_log(h) - .5 * eta * eta / h;
+                    L.a[M][s1 + i] = (eta * eta / (h * h)) - (1 / h);
+                    L.a[UB][s1 + i] = i > 0 ? L.a[H][s1 + i - 1] : hprev;
+                }
+            }
+        }
+        if (j >= 2) {   // chunk j - 2: gradient products
+            const int len = j - 2 == nc - 1 ? rem : C;
+#pragma unroll
+            for (int k = 0; k < NP; k++) {
+                const int i = k * 64 + lane;
+                if (i < len) {
+                    const double m = L.a[M][s2 + i];
+                    L.a[PO][s2 + i] = m * L.a[OD][s2 + i];
+                    L.a[PA][s2 + i] = m * L.a[AD][s2 + i];
+                    L.a[PB][s2 + i] = m * L.a[BD][s2 + i];
+                }
+            }
+        }
+        __syncthreads();
+        if (lane < 8) {
+            const int cj = j - lag;
+            const bool act = cj >= 0 && cj < nc;
+            const int len = !act ? 0 : cj == nc - 1 ? rem : C;
+            const int s = lag == 0 ? s0 : lag == 1 ? s1 : s2;
+            const double* up = u_arr < 0 ? L.one : &L.a[u_arr][s];
+            double* wp = w_arr < 0 ? L.sink : &L.a[w_arr][s];
+            // steps every active chain takes (lane-uniform), then the partial chunk's rest
+            int full = C;
+            for (int l = 0; l < 3; l++)
+                if (j - l == nc - 1) full = rem < full ? rem : full;
+            const double bf = act ? b : 1.0;     // inactive lanes: y = -0 + 1 * y = y
+            if (!act) up = L.sink;               // (read, then discarded by the select below)
+#pragma unroll 8
+            for (int i = 0; i < full; i++) {
+                const double u = act ? up[i] : -0.0;
+                y = u + bf * y;
+                wp[i] = y;
+            }
+            for (int i = full; i < C; i++) {
+                const bool on = i < len;
+                const double u = on ? up[i] : -0.0;
+                y = u + (on ? b : 1.0) * y;
+                wp[i] = y;
+            }
+        }
+        __syncthreads();
+    }
+    const double sum = __shfl(y, 4), oG = __shfl(y, 5), aG = __shfl(y, 6), bG = __shfl(y, 7);
+    o.res_f = sum + -.5 * fdlibm_log(2 * 3.141592653589793) * (double)(T - 1);
+    o.res_g[0] = aG * .5;   // the reference's order: alpha, beta, omega (:113)
+    o.res_g[1] = bG * .5;
+    o.res_g[2] = oG * .5;
+}
+
+template <int C>
+__global__ __launch_bounds__(64) void garch_tail_kernel(GarchFitArgs a) {
+    __shared__ TailLds<C> L;
+    const int lane = threadIdx.x;
+    const int n_park = a.park_ctr[0] < a.park_cap ? a.park_ctr[0] : a.park_cap;
+    for (;;) {   // work queue over the parked series; every wave leaves when it is empty
+        int idx = 0;
+        if (lane == 0) idx = atomicAdd(a.park_ctr + 1, 1);
+        idx = __shfl(idx, 0);
+        if (idx >= n_park) return;
+        const int64_t sl = a.park_ids[idx];
+        GarchOpt o = static_cast<const GarchOpt*>(a.park)[idx];
+        while (o.status < 0) {
+            garch_tail_pass<C>(a.in + sl * a.ld, a.T, o, L);
+            garch_cache_insert(o);
+            garch_advance(o);
+        }
+        if (lane == 0) {
+            const bool ok = o.status == STS_OK;
+            for (int j = 0; j < 3; j++) a.params[3 * sl + j] = ok ? o.point[j] : __builtin_nan("");
+            if (a.err && !(a.keep_err && a.err[sl] != 0)) a.err[sl] = o.status;
+            if (a.evals) a.evals[sl] = o.evals;
+        }
     }
 }
 
@@ -251,15 +420,54 @@ __global__ __launch_bounds__(64) void garch_effects_kernel(GarchEffectsArgs a) {
 
 constexpr int kGSpw = 32;
 constexpr int kGCh = 64;
+constexpr int kTailC = 128;
+constexpr int64_t kParkCap = 1 << 16;   // parked series per launch (more keep running in phase 1)
+constexpr int kTailGrid = 1024;
+
+// Passes a lane runs in garch_fit_kernel before its series moves to the tail kernel;
+// STS_GARCH_PASS_BUDGET overrides (0 = no tail phase; A/B runs and the tests).
+int garch_pass_budget() {
+    const char* e = std::getenv("STS_GARCH_PASS_BUDGET");
+    return e ? std::atoi(e) : 256;
+}
 
 }  // namespace
 
-hipError_t launch_garch_fit(const GarchFitArgs& a, bool fit, hipStream_t st) {
-    if (a.S <= 0) return hipSuccess;
+hipError_t launch_garch_fit(const GarchFitArgs& a0, bool fit, hipStream_t st) {
+    if (a0.S <= 0) return hipSuccess;
+    GarchFitArgs a = a0;
     dim3 grid((unsigned)((a.S + kGSpw - 1) / kGSpw)), block(64);
-    if (fit) hipLaunchKernelGGL((garch_fit_kernel<kGSpw, kGCh, true>), grid, block, 0, st, a);
-    else hipLaunchKernelGGL((garch_fit_kernel<kGSpw, kGCh, false>), grid, block, 0, st, a);
-    return hipGetLastError();
+    if (!fit) {
+        hipLaunchKernelGGL((garch_fit_kernel<kGSpw, kGCh, false>), grid, block, 0, st, a);
+        return hipGetLastError();
+    }
+    const int budget = garch_pass_budget();
+    void* scratch = nullptr;
+    if (budget > 0) {
+        const int64_t cap = a.S < kParkCap ? a.S : kParkCap;
+        const size_t state = (size_t)cap * sizeof(GarchOpt);
+        hipError_t e = hipMallocAsync(&scratch, state + (size_t)cap * sizeof(int64_t) + 16, st);
+        if (e != hipSuccess) return e;
+        a.park = scratch;
+        a.park_ids = reinterpret_cast<int64_t*>(static_cast<char*>(scratch) + state);
+        a.park_ctr = reinterpret_cast<int32_t*>(a.park_ids + cap);
+        a.park_cap = (int)cap;
+        a.pass_budget = budget;
+        e = hipMemsetAsync(a.park_ctr, 0, 2 * sizeof(int32_t), st);
+        if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL((garch_fit_kernel<kGSpw, kGCh, true>), grid, block, 0, st, a);
+    hipError_t e = hipGetLastError();
+    if (scratch) {
+        if (e == hipSuccess) {
+            const unsigned tg = (unsigned)(a.park_cap < kTailGrid ? a.park_cap : kTailGrid);
+            hipLaunchKernelGGL((garch_tail_kernel<kTailC>), dim3(tg), block, 0, st, a);
+            e = hipGetLastError();
+        }
+        const hipError_t ef = hipFreeAsync(scratch, st);
+        if (e == hipSuccess) e = ef;
+    }
+    return e;
 }
 
 hipError_t launch_garch_effects(int op, const GarchEffectsArgs& a, hipStream_t st) {

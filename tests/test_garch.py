@@ -207,9 +207,19 @@ def test_gpu_loglik_gradient(torch):
     assert bits_equal(g, np.array([oracle.garch_gradient(x[s], om[s], al[s], be[s]) for s in range(40)]))
 
 
+@pytest.fixture(params=["default", "1", "0"])
+def pass_budget(request, monkeypatch):
+    """Passes a series runs in garch_fit_kernel before garch_tail_kernel (one wave per series)
+    takes it over: 1 sends every series past its first pass to the tail kernel, 0 disables
+    the tail phase."""
+    if request.param != "default":
+        monkeypatch.setenv("STS_GARCH_PASS_BUDGET", request.param)
+    return request.param
+
+
 @pytest.mark.gpu
-@pytest.mark.parametrize("S,T", [(1, 10000), (70, 600), (33, 65), (5, 2)])
-def test_gpu_garch_fit(torch, S, T):
+@pytest.mark.parametrize("S,T", [(1, 10000), (70, 600), (33, 65), (5, 2), (3, 1), (40, 129), (40, 257)])
+def test_gpu_garch_fit(torch, S, T, pass_budget):
     from sparkts.models import GARCH
     if S == 1:
         x = argarch_sample(0.0, 0.0, 0.3, 0.5, 0.2, T, MersenneTwister(5))[None, :]   # GARCHSuite "fit model"
@@ -237,7 +247,7 @@ def test_gpu_garch_fit_raises_like_reference(torch):
 
 
 @pytest.mark.gpu
-def test_gpu_argarch_fit(torch):
+def test_gpu_argarch_fit(torch, pass_budget):
     from sparkts.models import ARGARCH
     rows = [argarch_sample(1.0 + 0.1 * s, 0.3 - 0.05 * (s % 5), 0.2, 0.3, 0.4, 1500, MersenneTwister(40 + s))
             for s in range(24)]
