@@ -191,8 +191,44 @@ struct TailLds {
     static constexpr int kSlots = 3 * C + 2;   // 3 chunk slots; +2 doubles skews the arrays' banks
     double a[13][kSlots];                       // UH XX ETA H OD AD TERM M UB BD PO PA PB
     double one[C + 2];                          // u of the oD chain
+    double negz[C + 2];                         // u of an idle chain: -0 + 1 * y == y for every y
     double sink[C];                             // chain outputs nobody reads (the sums)
 };
+
+// LDS hand-offs between lanes of the one wave: the wave's LDS instructions execute in order,
+// so only the compiler must not reorder; an LDS-only fence leaves the x prefetch in flight.
+__device__ __forceinline__ void tail_wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+}
+
+// y = u_i + b y over one C-step chunk, u read 8 steps ahead (unconditionally, so the reads
+// stay ahead of the dependent multiply-add chain).  SEL: steps i >= len are identity steps.
+template <int C, bool SEL>
+__device__ __forceinline__ void tail_chain(const double* up, double* wp, double b, int len, double& y) {
+    double u[8], un[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) u[k] = up[k];
+    for (int i = 0; i < C; i += 8) {
+        if (i + 8 < C) {
+#pragma unroll
+            for (int k = 0; k < 8; k++) un[k] = up[i + 8 + k];
+        }
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            if (SEL) {
+                const bool on = i + k < len;
+                y = (on ? u[k] : -0.0) + (on ? b : 1.0) * y;
+            } else {
+                y = u[k] + b * y;
+            }
+            wp[i + k] = y;
+        }
+#pragma unroll
+        for (int k = 0; k < 8; k++) u[k] = un[k];
+    }
+}
 
 template <int C>
 __device__ __forceinline__ void garch_tail_pass(const double* __restrict__ x, int64_t T, GarchOpt& o,
@@ -211,7 +247,10 @@ __device__ __forceinline__ void garch_tail_pass(const double* __restrict__ x, in
                     : lane == 5 ? PO : lane == 6 ? PA : PB;
     const int w_arr = lane == 0 ? H : lane == 1 ? OD : lane == 2 ? AD : lane == 3 ? BD : -1;
     double y = lane == 0 ? h0 : 0.0;
-    for (int i = lane; i < C; i += 64) L.one[i] = 1.0;
+    for (int i = lane; i < C; i += 64) {
+        L.one[i] = 1.0;
+        L.negz[i] = -0.0;
+    }
     // prefetch of chunk 0's x_{t-1}, x_t
     constexpr int NP = C / 64;
     double xp[NP], xe[NP];
@@ -263,34 +302,23 @@ __device__ __forceinline__ void garch_tail_pass(const double* __restrict__ x, in
                 }
             }
         }
-        __syncthreads();
+        tail_wave_sync();
         if (lane < 8) {
             const int cj = j - lag;
             const bool act = cj >= 0 && cj < nc;
-            const int len = !act ? 0 : cj == nc - 1 ? rem : C;
             const int s = lag == 0 ? s0 : lag == 1 ? s1 : s2;
-            const double* up = u_arr < 0 ? L.one : &L.a[u_arr][s];
-            double* wp = w_arr < 0 ? L.sink : &L.a[w_arr][s];
-            // steps every active chain takes (lane-uniform), then the partial chunk's rest
-            int full = C;
-            for (int l = 0; l < 3; l++)
-                if (j - l == nc - 1) full = rem < full ? rem : full;
-            const double bf = act ? b : 1.0;     // inactive lanes: y = -0 + 1 * y = y
-            if (!act) up = L.sink;               // (read, then discarded by the select below)
-#pragma unroll 8
-            for (int i = 0; i < full; i++) {
-                const double u = act ? up[i] : -0.0;
-                y = u + bf * y;
-                wp[i] = y;
-            }
-            for (int i = full; i < C; i++) {
-                const bool on = i < len;
-                const double u = on ? up[i] : -0.0;
-                y = u + (on ? b : 1.0) * y;
-                wp[i] = y;
-            }
+            // idle chains (chunk out of range) take identity steps from the -0 array
+            const double* up = !act ? L.negz : u_arr < 0 ? L.one : &L.a[u_arr][s];
+            double* wp = (!act || w_arr < 0) ? L.sink : &L.a[w_arr][s];
+            const double bl = act ? b : 1.0;
+            const int len = act && cj == nc - 1 ? rem : C;
+            // does any chain run a partial chunk in this iteration? (lane-uniform)
+            bool partial = false;
+            for (int l = 0; l < 3; l++) partial |= j - l == nc - 1 && rem < C;
+            if (partial) tail_chain<C, true>(up, wp, bl, len, y);
+            else tail_chain<C, false>(up, wp, bl, len, y);
         }
-        __syncthreads();
+        tail_wave_sync();
     }
     const double sum = __shfl(y, 4), oG = __shfl(y, 5), aG = __shfl(y, 6), bG = __shfl(y, 7);
     o.res_f = sum + -.5 * fdlibm_log(2 * 3.141592653589793) * (double)(T - 1);
@@ -421,14 +449,13 @@ __global__ __launch_bounds__(64) void garch_effects_kernel(GarchEffectsArgs a) {
 constexpr int kGSpw = 32;
 constexpr int kGCh = 64;
 constexpr int kTailC = 128;
-constexpr int64_t kParkCap = 1 << 16;   // parked series per launch (more keep running in phase 1)
 constexpr int kTailGrid = 1024;
 
 // Passes a lane runs in garch_fit_kernel before its series moves to the tail kernel;
 // STS_GARCH_PASS_BUDGET overrides (0 = no tail phase; A/B runs and the tests).
 int garch_pass_budget() {
     const char* e = std::getenv("STS_GARCH_PASS_BUDGET");
-    return e ? std::atoi(e) : 256;
+    return e ? std::atoi(e) : 64;
 }
 
 }  // namespace
@@ -444,7 +471,7 @@ hipError_t launch_garch_fit(const GarchFitArgs& a0, bool fit, hipStream_t st) {
     const int budget = garch_pass_budget();
     void* scratch = nullptr;
     if (budget > 0) {
-        const int64_t cap = a.S < kParkCap ? a.S : kParkCap;
+        const int64_t cap = a.S;   // a slot per series (~650 B): every lane past its budget can park
         const size_t state = (size_t)cap * sizeof(GarchOpt);
         hipError_t e = hipMallocAsync(&scratch, state + (size_t)cap * sizeof(int64_t) + 16, st);
         if (e != hipSuccess) return e;
