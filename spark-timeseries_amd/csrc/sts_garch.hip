@@ -448,7 +448,7 @@ __global__ __launch_bounds__(64) void garch_effects_kernel(GarchEffectsArgs a) {
 
 constexpr int kGSpw = 32;
 constexpr int kGCh = 64;
-constexpr int kTailC = 128;
+constexpr int kTailC = 64;
 constexpr int kTailGrid = 1024;
 
 // Passes a lane runs in garch_fit_kernel before its series moves to the tail kernel;
@@ -488,7 +488,13 @@ hipError_t launch_garch_fit(const GarchFitArgs& a0, bool fit, hipStream_t st) {
     if (scratch) {
         if (e == hipSuccess) {
             const unsigned tg = (unsigned)(a.park_cap < kTailGrid ? a.park_cap : kTailGrid);
-            hipLaunchKernelGGL((garch_tail_kernel<kTailC>), dim3(tg), block, 0, st, a);
+            const char* tc = std::getenv("STS_GARCH_TAIL_C");   // A/B: tail chunk length
+            if (tc && std::atoi(tc) == 256)
+                hipLaunchKernelGGL((garch_tail_kernel<256>), dim3(tg), block, 0, st, a);
+            else if (tc && std::atoi(tc) == 128)
+                hipLaunchKernelGGL((garch_tail_kernel<128>), dim3(tg), block, 0, st, a);
+            else
+                hipLaunchKernelGGL((garch_tail_kernel<kTailC>), dim3(tg), block, 0, st, a);
             e = hipGetLastError();
         }
         const hipError_t ef = hipFreeAsync(scratch, st);
