@@ -240,8 +240,9 @@ def main():
               "nan_instants": "sts::nan_instants_kernel + sts::gather_instants_kernel",
               "to_instants": "sts::transpose_kernel (64x64 LDS tiles)",
               "wire_decode": "sts::wire_decode_kernel (big-endian value blocks -> panel)",
-              "garch_fit": "sts::garch_fit_kernel<32,64> (lane-per-series commons-math3 optimizer; one "
-                           "logLikelihood+gradient pass over the wave's series block per optimizer request)",
+              "garch_fit": "sts::garch_fit_kernel<64,64> (lane-per-series commons-math3 optimizer; one "
+                           "logLikelihood+gradient pass over the wave's series block per optimizer request) + "
+                           "sts::garch_tail_kernel<64> (wave per series past 64 passes)",
               "ewma_fit": "sts::ewma_fit_kernel<32,64> (lane-per-series commons-math3 optimizer; one sse+gradient "
                           "pass over the wave's series block per optimizer request)"}[args.workload]
     roofline = None

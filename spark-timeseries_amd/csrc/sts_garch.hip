@@ -30,6 +30,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdlib>
+#include <cstring>
 
 namespace sts {
 namespace {
@@ -446,7 +447,7 @@ __global__ __launch_bounds__(64) void garch_effects_kernel(GarchEffectsArgs a) {
     }
 }
 
-constexpr int kGSpw = 32;
+constexpr int kGSpw = 64;   // A/B 64 x 64 vs 32 x 64: phase 1 178 vs 218 ms (100k x 2520)
 constexpr int kGCh = 64;
 constexpr int kTailC = 64;
 constexpr int kTailGrid = 1024;
@@ -483,7 +484,11 @@ hipError_t launch_garch_fit(const GarchFitArgs& a0, bool fit, hipStream_t st) {
         e = hipMemsetAsync(a.park_ctr, 0, 2 * sizeof(int32_t), st);
         if (e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL((garch_fit_kernel<kGSpw, kGCh, true>), grid, block, 0, st, a);
+    const char* shape = std::getenv("STS_GARCH_SHAPE");   // A/B: series per wave x chunk steps
+    if (shape && !std::strcmp(shape, "32x64"))
+        hipLaunchKernelGGL((garch_fit_kernel<32, 64, true>), dim3((unsigned)((a.S + 31) / 32)), block, 0, st, a);
+    else
+        hipLaunchKernelGGL((garch_fit_kernel<kGSpw, kGCh, true>), grid, block, 0, st, a);
     hipError_t e = hipGetLastError();
     if (scratch) {
         if (e == hipSuccess) {
