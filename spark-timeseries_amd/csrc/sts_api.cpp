@@ -201,7 +201,10 @@ int run_tile(const double* in, double* out, double* lagmat, int64_t S, int64_t T
     a.ld_in = ld_in;
     a.ld_out = ld_out;
     a.tiles_per_series = (T + tw - 1) / tw;
-    const int64_t per_chunk = seg ? sts::kSegTiles : kTilesPerChunk;
+    // STS_SEG_TILES: segment length (tiles) of the seg kernel, for A/B runs only
+    const char* seg_env = seg ? std::getenv("STS_SEG_TILES") : nullptr;
+    const int64_t per_chunk = seg ? (seg_env && std::atoi(seg_env) > 0 ? std::atoi(seg_env) : sts::kSegTiles)
+                                  : kTilesPerChunk;
     a.tiles_per_chunk = a.tiles_per_series < per_chunk ? a.tiles_per_series : per_chunk;
     a.chunks_per_series = (a.tiles_per_series + a.tiles_per_chunk - 1) / a.tiles_per_chunk;
     a.K = K;
