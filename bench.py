@@ -235,7 +235,7 @@ def main():
               "c1": "sts::seg_kernel<2> (wave-private series segments: fill linear + ACF partials, FP64 MFMA)",
               "c5": "sts::tile_kernel<4096,0> (fill nearest + lag-matrix columns)",
               "c2": "sts::recur_kernel<kFillDiffEwma> (fillPrevious -> differencesAtLag(1) -> EWMA add, lane per series)",
-              "c4": "sts::ar_fit_kernel (AR(5) Gram on FP64 MFMA + solve + fused remove)",
+              "c4": "sts::ar_fit_blk_kernel<5,40> (AR(5): lane-blocked register lag products, lane-parallel Gram / Cholesky + refinement, fused remove)",
               "stats": "sts::stats_kernel<64,32> (StatCounter.merge per lane, LDS-staged series block)",
               "nan_instants": "sts::nan_instants_kernel + sts::gather_instants_kernel",
               "to_instants": "sts::transpose_kernel (64x64 LDS tiles)",
@@ -289,7 +289,12 @@ def measured_traffic(workload, S, T):
     import glob
     if workload != "c3" or (S, T) != WORKLOADS["c3"][:2]:
         return None
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_c3_traffic.json")))
+    import re
+
+    def version(path):   # r01_v11 after r01_v7: numeric, not lexical, order
+        return tuple(int(n) for n in re.findall(r"\d+", os.path.basename(path)))
+
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_c3_traffic.json")), key=version)
     if not files:
         return None
     with open(files[-1]) as f:
