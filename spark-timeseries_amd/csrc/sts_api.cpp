@@ -190,7 +190,9 @@ int run_tile(const double* in, double* out, double* lagmat, int64_t S, int64_t T
                         (!out || ((reinterpret_cast<uintptr_t>(out) & 15) == 0 && ld_out % 2 == 0)) &&
                         T < 0x7fff0000LL;
     const bool seg = seg_ok && (force ? !std::strcmp(force, "seg") : T <= 16384);
-    const int tw = seg ? sts::kSegW : (K > 0) ? 4096 : tile_width(T);
+    // STS_TILE_W=2048: 2-wave workgroups on 2048-step tiles for K <= 60 (A/B runs only)
+    const char* tw_env = (!seg && K > 0 && K <= 60 && !lagmat) ? std::getenv("STS_TILE_W") : nullptr;
+    const int tw = seg ? sts::kSegW : (K > 0) ? (tw_env && std::atoi(tw_env) == 2048 ? 2048 : 4096) : tile_width(T);
     sts::TileArgs a{};
     a.in = in;
     a.out = out;

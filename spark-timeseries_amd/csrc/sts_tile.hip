@@ -66,7 +66,6 @@ __device__ __forceinline__ void lds_barrier() {
 typedef double d4 __attribute__((ext_vector_type(4)));
 
 constexpr int kThreads = 256;
-constexpr int kWaves = kThreads / 64;
 constexpr int kBig = 1 << 30;
 
 __device__ __forceinline__ bool isnan_d(double v) { return __builtin_isnan(v); }
@@ -143,8 +142,11 @@ __device__ __forceinline__ int px2_(int q2) { return PAD ? q2 + ((q2 >> 4) << 1)
 // + j%q -- every lag 0 .. 16 NT - q exactly once per step, and the same lag map h(j) - i in
 // every accumulator; TOEPLITZ (K = 61..63) uses NT = floor((K + 15) / 16) + 1 MFMAs with
 // U_t holding lag 16t + j - i.
-template <int TW, int NT, bool SHIFTED>
-__global__ __launch_bounds__(kThreads, 3) void tile_kernel(TileArgs a, int method) {
+template <int TW, int NT, bool SHIFTED, int NTH>
+__global__ __launch_bounds__(NTH, 3) void tile_kernel(TileArgs a, int method) {
+    constexpr int kThreads = NTH;          // 256 (4 waves) or 128 (2 waves, TW = 2048)
+    constexpr int kWaves = NTH / 64;
+    static_assert(TW / 64 % kWaves == 0, "whole 64-step chunks per wave");
     constexpr int EW = kHB + TW + kHA;
     constexpr int NA = SHIFTED ? 2 : (NT > 0 ? NT : 1);      // MFMA accumulators
     constexpr int QS = (SHIFTED && NT > 0) ? 16 / NT : 16;   // window shift step (shifted scheme)
@@ -275,7 +277,7 @@ __global__ __launch_bounds__(kThreads, 3) void tile_kernel(TileArgs a, int metho
     if constexpr (j < RPT) {                                                                \
         const unsigned long long bx_ = __ballot(!isnan_d(R##j.x));                          \
         const unsigned long long by_ = __ballot(!isnan_d(R##j.y));                          \
-        const int w_ = 2 * wave + 8 * j;                                                    \
+        const int w_ = 2 * wave + 2 * kWaves * j;                                                  \
         if (lane == 0) {                                                                    \
             if (w_ < NW) mask[w_] = interleave2((unsigned)bx_, (unsigned)by_);              \
             if (w_ + 1 < NW) mask[w_ + 1] = interleave2((unsigned)(bx_ >> 32), (unsigned)(by_ >> 32)); \
@@ -804,14 +806,17 @@ hipError_t launch_tile(int method, int tw, const TileArgs& a, hipStream_t st) {
     const int64_t nchunk = a.S * a.chunks_per_series;
     if (nchunk <= 0) return hipSuccess;
     if (nchunk > 0x7fffffffLL) return hipErrorInvalidValue;
-    dim3 grid((unsigned)nchunk), block(kThreads);
+    dim3 grid((unsigned)nchunk), block(kThreads), half(kThreads / 2);
     if (tw == 512 && a.K == 0) {
-        hipLaunchKernelGGL((tile_kernel<512, 0, false>), grid, block, 0, st, a, method);
+        hipLaunchKernelGGL((tile_kernel<512, 0, false, kThreads>), grid, block, 0, st, a, method);
+    } else if (tw == 2048 && a.K > 0 && a.K <= 60) {   // 2-wave workgroups (A/B: STS_TILE_W=2048)
+        if (a.K <= 24) hipLaunchKernelGGL((tile_kernel<2048, 2, true, kThreads / 2>), grid, half, 0, st, a, method);
+        else hipLaunchKernelGGL((tile_kernel<2048, 4, true, kThreads / 2>), grid, half, 0, st, a, method);
     } else if (tw == 4096) {
-        if (a.K == 0) hipLaunchKernelGGL((tile_kernel<4096, 0, false>), grid, block, 0, st, a, method);
-        else if (a.K <= 24) hipLaunchKernelGGL((tile_kernel<4096, 2, true>), grid, block, 0, st, a, method);
-        else if (a.K <= 60) hipLaunchKernelGGL((tile_kernel<4096, 4, true>), grid, block, 0, st, a, method);
-        else if (a.K <= 63) hipLaunchKernelGGL((tile_kernel<4096, 5, false>), grid, block, 0, st, a, method);
+        if (a.K == 0) hipLaunchKernelGGL((tile_kernel<4096, 0, false, kThreads>), grid, block, 0, st, a, method);
+        else if (a.K <= 24) hipLaunchKernelGGL((tile_kernel<4096, 2, true, kThreads>), grid, block, 0, st, a, method);
+        else if (a.K <= 60) hipLaunchKernelGGL((tile_kernel<4096, 4, true, kThreads>), grid, block, 0, st, a, method);
+        else if (a.K <= 63) hipLaunchKernelGGL((tile_kernel<4096, 5, false, kThreads>), grid, block, 0, st, a, method);
         else return hipErrorInvalidValue;
     } else {
         return hipErrorInvalidValue;
