@@ -257,7 +257,7 @@ def main():
                     "kernel_launches_timed": int(launches[0])}
 
     cpu = None
-    if rank == 0 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:   # the CPU leg is an N = 1 report
         cpu = cpu_baseline(args, S, T, K, seed, nan_p, out, acf, p_ar, smooth,
                            gpar if args.workload == "garch_fit" else None)
 
