@@ -284,6 +284,14 @@ int sts_fill_method_from_name(const char* name) {
 }
 
 int sts_profile_begin(void) {
+    // create the event pool here, before the caller's timed region: a hipEventCreate inside
+    // it costs CPU time per launch and can starve the queue of short kernels (C1: 0.13 ms)
+    constexpr size_t kPrealloc = 512;
+    while (g_prof.pool.size() < kPrealloc) {
+        hipEvent_t e;
+        HIP_TRY(hipEventCreate(&e), "hipEventCreate");
+        g_prof.pool.push_back(e);
+    }
     g_prof.on = true;
     g_prof.used = 0;
     return STS_OK;
