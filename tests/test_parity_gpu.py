@@ -234,14 +234,25 @@ def test_fill_autocorr_fused(torch, method):
         assert_rel(host(acf), racf, what=method)
 
 
-@pytest.mark.parametrize("kernel", ["tile", "seg", "tile2"])
+# A/B knob settings that change the decomposition: each must stay parity-green
+KNOB_VARIANTS = {
+    "tile2048": ("tile", {"STS_TILE_W": "2048"}),          # 2-wave workgroups, 2048-step tiles
+    "tilec4": ("tile", {"STS_TILES_PER_CHUNK": "4"}),      # 4 tiles per workgroup
+    "seg3": ("seg", {"STS_SEG_TILES": "3"}),               # multi-segment partials + finalize
+}
+
+
+@pytest.mark.parametrize("kernel", ["tile", "seg", "tile2"] + sorted(KNOB_VARIANTS))
 @pytest.mark.parametrize("method", ["linear", "previous", "next", "nearest"])
 def test_fill_autocorr_both_kernels(torch, monkeypatch, kernel, method):
     # both imputation kernels, whatever the length-based dispatch picks: the workgroup
     # tile kernel and the wave-private segment kernel (STS_TILE_KERNEL forces one)
     from sparkts import TimeSeriesRDD
     from sparkts import UnivariateTimeSeries as uts
-    monkeypatch.setenv("STS_TILE_KERNEL", kernel)
+    forced, knobs = KNOB_VARIANTS.get(kernel, (kernel, {}))
+    monkeypatch.setenv("STS_TILE_KERNEL", forced)
+    for k, v in knobs.items():
+        monkeypatch.setenv(k, v)
     rng = np.random.default_rng(zlib.crc32(("both%s%s" % (kernel, method)).encode()))
     for S, T, K in [(7, 600, 20), (5, 2520, 60), (3, 16384 + 77, 24), (2, 70000, 60), (2, 513, 0)]:
         x = random_panel(rng, S, T, 0.07, runs=True)
