@@ -205,10 +205,10 @@ int run_tile(const double* in, double* out, double* lagmat, int64_t S, int64_t T
     a.tiles_per_series = (T + tw - 1) / tw;
     // STS_SEG_TILES: segment length (tiles) of the seg kernel, for A/B runs only
     const char* seg_env = seg ? std::getenv("STS_SEG_TILES") : nullptr;
-    const int64_t per_chunk = seg ? (seg_env && std::atoi(seg_env) > 0 ? std::atoi(seg_env) : sts::kSegTiles)
-                                  : (std::getenv("STS_TILES_PER_CHUNK") && std::atoi(std::getenv("STS_TILES_PER_CHUNK")) > 0
-                                         ? std::atoi(std::getenv("STS_TILES_PER_CHUNK"))   // A/B runs only
-                                         : kTilesPerChunk);
+    // STS_TILES_PER_CHUNK: tiles per tile-kernel workgroup, for A/B runs only
+    const char* tpc_env = seg ? nullptr : std::getenv("STS_TILES_PER_CHUNK");
+    const int seg_knob = seg_env ? std::atoi(seg_env) : 0, tpc_knob = tpc_env ? std::atoi(tpc_env) : 0;
+    const int64_t per_chunk = seg ? (seg_knob > 0 ? seg_knob : sts::kSegTiles) : (tpc_knob > 0 ? tpc_knob : kTilesPerChunk);
     a.tiles_per_chunk = a.tiles_per_series < per_chunk ? a.tiles_per_series : per_chunk;
     a.chunks_per_series = (a.tiles_per_series + a.tiles_per_chunk - 1) / a.tiles_per_chunk;
     a.K = K;
