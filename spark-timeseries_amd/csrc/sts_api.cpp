@@ -182,16 +182,16 @@ int run_tile(const double* in, double* out, double* lagmat, int64_t S, int64_t T
     // short series (T <= 16384: C1, the 10-year daily panels) go to the wave-private
     // segment kernel (2x faster there: one wave per series, no barriers), long ones to the
     // workgroup tile kernel (faster from T = 32768: C3, C5).  The segment kernel needs a
-    // 16-B aligned panel, no lag matrix and K <= 60.  STS_TILE_KERNEL=tile|seg|tile2 forces one
-    // (A/B runs, tools/kbench.py).
-    const char* force = std::getenv("STS_TILE_KERNEL");
+    // 16-B aligned panel, no lag matrix and K <= 60.  In the A/B build STS_TILE_KERNEL=tile|seg
+    // forces one (tools/kbench.py, the knob tests).
+    const char* force = sts::ab_knob("STS_TILE_KERNEL");
     const bool seg_ok = !lagmat && sts::seg_nt(K) >= 0 && (reinterpret_cast<uintptr_t>(in) & 15) == 0 &&
                         (ld_in % 2) == 0 &&
                         (!out || ((reinterpret_cast<uintptr_t>(out) & 15) == 0 && ld_out % 2 == 0)) &&
                         T < 0x7fff0000LL;
     const bool seg = seg_ok && (force ? !std::strcmp(force, "seg") : T <= 16384);
-    // STS_TILE_W=2048: 2-wave workgroups on 2048-step tiles for K <= 60 (A/B runs only)
-    const char* tw_env = (!seg && K > 0 && K <= 60 && !lagmat) ? std::getenv("STS_TILE_W") : nullptr;
+    // STS_TILE_W=2048: 2-wave workgroups on 2048-step tiles for K <= 60 (A/B build only)
+    const char* tw_env = (!seg && K > 0 && K <= 60 && !lagmat) ? sts::ab_knob("STS_TILE_W") : nullptr;
     const int tw = seg ? sts::kSegW : (K > 0) ? (tw_env && std::atoi(tw_env) == 2048 ? 2048 : 4096) : tile_width(T);
     sts::TileArgs a{};
     a.in = in;
@@ -204,9 +204,9 @@ int run_tile(const double* in, double* out, double* lagmat, int64_t S, int64_t T
     a.ld_out = ld_out;
     a.tiles_per_series = (T + tw - 1) / tw;
     // STS_SEG_TILES: segment length (tiles) of the seg kernel, for A/B runs only
-    const char* seg_env = seg ? std::getenv("STS_SEG_TILES") : nullptr;
+    const char* seg_env = seg ? sts::ab_knob("STS_SEG_TILES") : nullptr;
     // STS_TILES_PER_CHUNK: tiles per tile-kernel workgroup, for A/B runs only
-    const char* tpc_env = seg ? nullptr : std::getenv("STS_TILES_PER_CHUNK");
+    const char* tpc_env = seg ? nullptr : sts::ab_knob("STS_TILES_PER_CHUNK");
     const int seg_knob = seg_env ? std::atoi(seg_env) : 0, tpc_knob = tpc_env ? std::atoi(tpc_env) : 0;
     const int64_t per_chunk = seg ? (seg_knob > 0 ? seg_knob : sts::kSegTiles) : (tpc_knob > 0 ? tpc_knob : kTilesPerChunk);
     a.tiles_per_chunk = a.tiles_per_series < per_chunk ? a.tiles_per_series : per_chunk;
@@ -220,7 +220,8 @@ int run_tile(const double* in, double* out, double* lagmat, int64_t S, int64_t T
     // final ACF itself (no partials, no second launch)
     const bool one_seg = seg && a.chunks_per_series == 1;
     const int64_t last_len = T - (a.tiles_per_series - 1) * tw;
-    const bool fuse = one_seg && K > 0 && T > 2 * (int64_t)K && last_len >= 64 && !std::getenv("STS_NO_FUSED_ACF");
+    const bool fuse = one_seg && K > 0 && T > 2 * (int64_t)K && T >= 2 * sts::kAcfEdge && last_len >= 64 &&
+                      !sts::ab_knob("STS_NO_FUSED_ACF");
     a.err_all = one_seg ? 1 : 0;
     a.acf_fused = fuse ? acf : nullptr;
     if (err && !one_seg) HIP_TRY(hipMemsetAsync(err, 0, (size_t)S * sizeof(int32_t), st), "hipMemsetAsync(err)");
@@ -231,9 +232,7 @@ int run_tile(const double* in, double* out, double* lagmat, int64_t S, int64_t T
         a.partials = static_cast<double*>(part.p);
     }
     prof_mark(st);
-    const bool t2 = !seg && tw == 4096 && sts::tile2_supported(K, a) && force && !std::strcmp(force, "tile2");
-    hipError_t e = seg ? sts::launch_segment(method, a, st)
-                       : (t2 ? sts::launch_tile2(method, a, st) : sts::launch_tile(method, tw, a, st));
+    hipError_t e = seg ? sts::launch_segment(method, a, st) : sts::launch_tile(method, tw, a, st);
     prof_mark(st);
     if (e != hipSuccess) return hip_fail(e, name);
     if (K > 0 && !fuse) {
@@ -309,6 +308,8 @@ int sts_profile_end(double* kernel_ms, int64_t* launches) {
         n++;
     }
     g_prof.used = 0;
+    for (hipEvent_t e : g_prof.pool) (void)hipEventDestroy(e);   // recreated by the next begin
+    g_prof.pool.clear();
     if (kernel_ms) *kernel_ms = total;
     if (launches) *launches = n;
     return STS_OK;

@@ -590,7 +590,7 @@ hipError_t launch_ar_fit(const ArArgs& a, hipStream_t st) {
     if (a.S <= 0) return hipSuccess;
     if (a.p < 1 || a.p > kPMax) return hipErrorInvalidValue;
     // register path: p <= 8, T <= 64 * 40 (lane blocks of B steps, B in {8, 16, 24, 32, 40})
-    if (a.p <= kRegPB && a.T <= 64 * 40 && !std::getenv("STS_AR_STAGED")) {
+    if (a.p <= kRegPB && a.T <= 64 * 40 && !ab_knob("STS_AR_STAGED")) {
         dim3 g((unsigned)((a.S + kRegWaves - 1) / kRegWaves)), b(64 * kRegWaves);
         const int64_t need = (a.T + 63) / 64;
         const int B = need <= 8 ? 8 : need <= 16 ? 16 : need <= 24 ? 24 : need <= 32 ? 32 : 40;

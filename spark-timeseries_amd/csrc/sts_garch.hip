@@ -453,9 +453,10 @@ constexpr int kTailC = 64;
 constexpr int kTailGrid = 1024;
 
 // Passes a lane runs in garch_fit_kernel before its series moves to the tail kernel;
-// STS_GARCH_PASS_BUDGET overrides (0 = no tail phase; A/B runs and the tests).
+// STS_GARCH_PASS_BUDGET overrides it in the A/B build (0 = no tail phase; A/B runs and the
+// tests).
 int garch_pass_budget() {
-    const char* e = std::getenv("STS_GARCH_PASS_BUDGET");
+    const char* e = ab_knob("STS_GARCH_PASS_BUDGET");
     return e ? std::atoi(e) : 64;
 }
 
@@ -484,7 +485,7 @@ hipError_t launch_garch_fit(const GarchFitArgs& a0, bool fit, hipStream_t st) {
         e = hipMemsetAsync(a.park_ctr, 0, 2 * sizeof(int32_t), st);
         if (e != hipSuccess) return e;
     }
-    const char* shape = std::getenv("STS_GARCH_SHAPE");   // A/B: series per wave x chunk steps
+    const char* shape = ab_knob("STS_GARCH_SHAPE");   // A/B: series per wave x chunk steps
     if (shape && !std::strcmp(shape, "32x64"))
         hipLaunchKernelGGL((garch_fit_kernel<32, 64, true>), dim3((unsigned)((a.S + 31) / 32)), block, 0, st, a);
     else
@@ -493,7 +494,7 @@ hipError_t launch_garch_fit(const GarchFitArgs& a0, bool fit, hipStream_t st) {
     if (scratch) {
         if (e == hipSuccess) {
             const unsigned tg = (unsigned)(a.park_cap < kTailGrid ? a.park_cap : kTailGrid);
-            const char* tc = std::getenv("STS_GARCH_TAIL_C");   // A/B: tail chunk length
+            const char* tc = ab_knob("STS_GARCH_TAIL_C");   // A/B: tail chunk length
             if (tc && std::atoi(tc) == 256)
                 hipLaunchKernelGGL((garch_tail_kernel<256>), dim3(tg), block, 0, st, a);
             else if (tc && std::atoi(tc) == 128)

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdlib>
 
 #include "sts.h"
 
@@ -14,7 +15,13 @@ namespace sts {
 // steps of look-ahead (ACF pairs reach 16*NT-1 <= 79 steps past the tile).
 constexpr int kHB = 64;
 constexpr int kHA = 128;
-constexpr int kPartStride = 66;  // per-tile partials: lags 0..63, sum(y), pad
+// per-chunk ACF partials: [0, 64) lag products, [64] sum y and [65] sum y^2 over the
+// series' middle (sts_acf.hpp), [66] the shift c, [67] pad
+constexpr int kPartStride = 68;
+constexpr int kPartSum = 64, kPartSq = 65, kPartShift = 66;
+// autocorr head / tail length handled per lag by the finalize (sts_acf.hpp); K <= kAcfEdge
+// on the fused paths, and series shorter than 2 kAcfEdge take the direct two-pass finalize
+constexpr int kAcfEdge = 64;
 
 struct TileArgs {
     const double* in;
@@ -41,11 +48,17 @@ struct FinalizeArgs {
     int K;
 };
 
+// A/B experiment knobs (environment variables) exist only in the -DSTS_AB build
+// (build/libsts_hip_ab.so, tools/ and the knob tests); the product libsts_hip.so never reads
+// its environment, so a Spark executor's environment cannot change which kernels run.
+#ifdef STS_AB
+inline const char* ab_knob(const char* name) { return std::getenv(name); }
+#else
+inline const char* ab_knob(const char*) { return nullptr; }
+#endif
+
 // launchers (return hipError_t of the launch)
 hipError_t launch_tile(int method, int tw, const TileArgs& a, hipStream_t st);
-// role-split variant (sts_tile2.hip): fill waves and MFMA waves on different tiles
-bool tile2_supported(int K, const TileArgs& a);
-hipError_t launch_tile2(int method, const TileArgs& a, hipStream_t st);
 hipError_t launch_acf_finalize(const FinalizeArgs& a, hipStream_t st);
 
 // Wave-private segment kernel (sts_seg.hip): tiles of kSegW steps, kSegTiles tiles per

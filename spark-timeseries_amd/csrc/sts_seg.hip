@@ -22,7 +22,9 @@
 //   * the NaN positions are compacted and imputed with every lane busy; linear replays
 //     the reference's sequential accumulation r = r + inc (t - L adds) -- bit-exact, the
 //     library is built with -ffp-contract=off;
-//   * the filled tile goes out with 16-B stores and y = F - F(0) replaces it in the ring;
+//   * the filled tile goes out with 16-B stores and y = F - c replaces it in the ring (c =
+//     the robust shift of sts_acf.hpp; sum y and sum y^2 over the series' middle are
+//     accumulated here);
 //   * the PREVIOUS tile's lag products run on MFMA (its ring slot plus this tile's head).
 //
 // Lag products with 4 MFMAs per 64 steps for K <= 60 (2 for K <= 24).  With
@@ -37,6 +39,7 @@
 // for 61 needed (the plain Toeplitz blocking needs 5 MFMAs = 80).  The lag map is the
 // same for every t, so the NT accumulators are summed before the diagonal extraction.
 #include "sts_internal.hpp"
+#include "sts_acf.hpp"
 
 #include <hip/hip_runtime.h>
 
@@ -153,8 +156,8 @@ struct Mfma {
     }
     // lag products of the chunks [c_lo, 8) of the tile in ring slot SLOT
     template <int SLOT>
-    __device__ static __forceinline__ void tile(const double* ring, int c_lo, d4 (&U)[Mfma<NT>::NA], double& sy,
-                                                int lane, int offb) {
+    __device__ static __forceinline__ void tile(const double* ring, int c_lo, d4 (&U)[Mfma<NT>::NA], int lane,
+                                                int offb) {
         const double* pa = ring + SLOT * kW + lane;
         const double* pb = ring + SLOT * kW + offb;
         // software pipeline, one chunk deep: chunk c + 1's operands load while chunk c's
@@ -179,7 +182,6 @@ struct Mfma {
             }
 #pragma unroll
             for (int t = 0; t < NT; t++) U[t % NA] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[t], b[t], U[t % NA], 0, 0, 0);
-            sy += a[0];
             __builtin_amdgcn_sched_barrier(0);
             if (c + 1 < kWords) {
 #pragma unroll
@@ -195,7 +197,8 @@ struct Mfma {
 struct SegState {
     int Lc;          // last valid index before the tile being imputed (-1: none)
     double Lv;       // its value
-    double c0;       // ACF shift F(0)
+    double c0;       // ACF shift (sts_acf.hpp robust_shift)
+    double sm, qm;   // this lane's sum y / sum y^2 over the series' middle (sts_acf.hpp)
     bool err;        // nearest: "Input is all NaNs!"
 };
 
@@ -230,8 +233,8 @@ __device__ __forceinline__ int masks_to_lds(const v2d (&R)[4], unsigned long lon
 // global memory from scan_from); lookv its value.
 template <int NT, int SLOT>
 __device__ __forceinline__ void impute_tile(WaveLds& w, const double* src, double* dst, int kb, int T, int method,
-                                            int look, double lookv, int scan_from, bool store, SegState& st,
-                                            int lane, v2d& head) {
+                                            int look, double lookv, int scan_from, bool store, bool own,
+                                            SegState& st, int lane, v2d& head) {
     double* ring = w.ring + SLOT * kW;
     const bool needL = (method == STS_FILL_LINEAR || method == STS_FILL_PREVIOUS || method == STS_FILL_NEAREST);
     const bool needN = (method == STS_FILL_LINEAR || method == STS_FILL_NEXT || method == STS_FILL_NEAREST);
@@ -353,7 +356,8 @@ __device__ __forceinline__ void impute_tile(WaveLds& w, const double* src, doubl
         wave_sync();
     }
 
-    // ---- filled output (16-B stores), then y = F - c0 (0 past the series end) ----
+    // ---- filled output (16-B stores), then y = F - c0 (0 past the series end); a tile of
+    //      this segment (own) adds its middle positions to the lane's sums ----
     v2d* r2 = reinterpret_cast<v2d*>(ring) + lane;
     const bool full = (kb + kW <= T);
 #pragma unroll
@@ -373,6 +377,16 @@ __device__ __forceinline__ void impute_tile(WaveLds& w, const double* src, doubl
             y.x = (full || t < T) ? f.x - st.c0 : 0.0;
             y.y = (full || t + 1 < T) ? f.y - st.c0 : 0.0;
             r2[64 * u] = y;
+            if (own) {
+                if (acf_mid(t, T)) {
+                    st.sm += y.x;
+                    st.qm = __builtin_fma(y.x, y.x, st.qm);
+                }
+                if (acf_mid(t + 1, T)) {
+                    st.sm += y.y;
+                    st.qm = __builtin_fma(y.y, y.y, st.qm);
+                }
+            }
             if (SLOT == 0 && u == 0) reinterpret_cast<v2d*>(w.ring + 2 * kW)[lane] = y;
             if (u == 0 && kb == 0) head = y;          // y(2 lane), y(2 lane + 1): fused ACF finalize
         }
@@ -410,8 +424,7 @@ enum { kMmNone = 0, kMmPre = 1, kMmFull = 2 };
 // Rn = tile k + 1 (in flight), Rnn = free (receives tile k + 2).
 template <int NT, int SLOT, int MM>
 __device__ __forceinline__ void seg_step(WaveLds& w, const SegCtx& cx, int k, v2d (&Rnn)[4], v2d (&Rn)[4],
-                                         SegState& st, d4 (&U)[Mfma<NT>::NA], double& sy, int lane, int offb,
-                                         v2d& head) {
+                                         SegState& st, d4 (&U)[Mfma<NT>::NA], int lane, int offb, v2d& head) {
     if (k + 2 <= cx.kLast) load_tile(Rnn, cx.src, (k + 2) * kW, cx.T, lane);
     const bool have_next = (k + 1 <= cx.kLast);
     int look = kBig, scan_from = (k + 1) * kW;
@@ -429,12 +442,12 @@ __device__ __forceinline__ void seg_step(WaveLds& w, const SegCtx& cx, int k, v2
     }
     if (k < cx.ntiles) {
         impute_tile<NT, SLOT>(w, cx.src, cx.dst, k * kW, cx.T, cx.method, look, lookv, scan_from,
-                              cx.dst != nullptr && k < cx.k1, st, lane, head);
+                              cx.dst != nullptr && k < cx.k1, k < cx.k1, st, lane, head);
     } else if constexpr (NT > 0) {
         zero_slot<SLOT>(w, lane);
     }
     if constexpr (NT > 0 && MM != kMmNone)
-        Mfma<NT>::template tile<SLOT ^ 1>(w.ring, MM == kMmPre ? kWords - 1 : 0, U, sy, lane, offb);
+        Mfma<NT>::template tile<SLOT ^ 1>(w.ring, MM == kMmPre ? kWords - 1 : 0, U, lane, offb);
     if (have_next) {
         wave_sync();
         raw_to_slot(w.ring + (SLOT ^ 1) * kW, Rn, lane);
@@ -467,16 +480,11 @@ __global__ __launch_bounds__(256, 4) void seg_kernel(TileArgs a, int method) {
     SegState st;
     st.err = false;
     st.c0 = 0.0;
+    st.sm = 0.0;
+    st.qm = 0.0;
     st.Lc = -1;
     st.Lv = 0.0;
-    if (NT > 0) {
-        double x0 = cx.src[0];
-        if (method == STS_FILL_NEXT && isnan_d(x0)) {
-            const int f = scan_fwd(cx.src, 0, cx.T, lane);
-            x0 = (f < cx.T) ? cx.src[f] : __builtin_nan("");
-        }
-        st.c0 = x0;
-    }
+    if (NT > 0) st.c0 = robust_shift(cx.src, cx.T, lane);   // the same value in every segment
     if (needL && cx.k0 > 0) {
         st.Lc = scan_back(cx.src, cx.k0 * kW, lane);
         st.Lv = (st.Lc >= 0) ? cx.src[st.Lc] : 0.0;
@@ -486,7 +494,6 @@ __global__ __launch_bounds__(256, 4) void seg_kernel(TileArgs a, int method) {
     d4 U[Mfma<NT>::NA];
 #pragma unroll
     for (int t = 0; t < Mfma<NT>::NA; t++) U[t] = d4{0.0, 0.0, 0.0, 0.0};
-    double sy = 0.0;
 
     v2d RA[4], RB[4];
     load_tile(RA, cx.src, cx.k0 * kW, cx.T, lane);
@@ -498,12 +505,12 @@ __global__ __launch_bounds__(256, 4) void seg_kernel(TileArgs a, int method) {
 
     // first step peeled: its MFMA work is the pre-chunk (segment 0) or nothing
     v2d head = {0.0, 0.0};
-    if (NT > 0 && g == 0) seg_step<NT, 0, kMmPre>(w, cx, cx.k0, RA, RB, st, U, sy, lane, offb, head);
-    else seg_step<NT, 0, kMmNone>(w, cx, cx.k0, RA, RB, st, U, sy, lane, offb, head);
+    if (NT > 0 && g == 0) seg_step<NT, 0, kMmPre>(w, cx, cx.k0, RA, RB, st, U, lane, offb, head);
+    else seg_step<NT, 0, kMmNone>(w, cx, cx.k0, RA, RB, st, U, lane, offb, head);
     for (int k = cx.k0 + 1; k <= cx.kEnd; k += 2) {
-        seg_step<NT, 1, kMmFull>(w, cx, k, RB, RA, st, U, sy, lane, offb, head);
+        seg_step<NT, 1, kMmFull>(w, cx, k, RB, RA, st, U, lane, offb, head);
         if (k + 1 > cx.kEnd) break;
-        seg_step<NT, 0, kMmFull>(w, cx, k + 1, RA, RB, st, U, sy, lane, offb, head);
+        seg_step<NT, 0, kMmFull>(w, cx, k + 1, RA, RB, st, U, lane, offb, head);
     }
     const int klast_slot = (cx.ntiles - 1 - cx.k0) & 1;   // ring slot of the series' last tile
     // st.err is per lane (the lane that imputed the failing NaN): one wave-wide answer
@@ -539,40 +546,37 @@ __global__ __launch_bounds__(256, 4) void seg_kernel(TileArgs a, int method) {
             const int i = 16 * (j / Q) + (16 - Q) + (j % Q) - lane;
             if (i >= 0 && i < 16) lagacc += scr[i * 16 + j];
         }
+        double sm = st.sm, qm = st.qm;
 #pragma unroll
-        for (int d = 32; d >= 1; d >>= 1) sy += __shfl_xor(sy, d);
+        for (int d = 32; d >= 1; d >>= 1) {
+            sm += __shfl_xor(sm, d);
+            qm += __shfl_xor(qm, d);
+        }
         if (a.acf_fused == nullptr) {
             double* part = a.partials + unit * kPartStride;
             part[lane] = lagacc;
-            if (lane == 0) part[64] = sy;
+            if (lane == 0) {
+                part[kPartSum] = sm;
+                part[kPartSq] = qm;
+                part[kPartShift] = st.c0;
+            }
         } else {
-            // ---- one segment per series: acf_finalize_kernel's general path (T > 2K) right
-            //      here, with the head y(0..K) from tile 0 (registers) and the tail
-            //      y(T-K..T) from the last tile's ring slot (host guarantees it holds >= 64
-            //      steps).  Same operations in the same order -> the same bits. ----
+            // ---- one segment per series: acf_finalize_kernel's general path (T >= 2 kAcfEdge,
+            //      T > 2K) right here, with the head y(0..63) from tile 0 (registers) and the
+            //      tail y(T-64..T) from the last tile's ring slot (host guarantees it holds
+            //      >= 64 steps).  Same operations in the same order -> the same bits. ----
             const int K = a.K, T = cx.T;
             const int i = lane + 1;
-            const double Pi = 0.0 + __shfl(lagacc, (lane + 1) & 63), P0 = 0.0 + __shfl(lagacc, 0), Sy = 0.0 + sy;
+            const double Pi = 0.0 + __shfl(lagacc, (lane + 1) & 63), Sm = 0.0 + sm, Qm = 0.0 + qm;
             const double* tail = tail_base;   // y of the last tile, indexed by series position - kb_last
-            double pre_s = 0.0, pre_q = 0.0, suf_s = 0.0, suf_q = 0.0;
-            for (int j = 0; j < K; j++) {
-                const double hx = __shfl(head.x, j >> 1), hy = __shfl(head.y, j >> 1);
-                const double y = (j & 1) ? hy : hx;
-                const double z = tail[T - 1 - j - kb_last];
-                if (j < i) {
-                    pre_s += y;
-                    pre_q += y * y;
-                    suf_s += z;
-                    suf_q += z * z;
-                }
-            }
-            const double N = (double)(T - i);
-            const double sum1 = Sy - pre_s, sum2 = Sy - suf_s;
-            const double sq1 = P0 - pre_q, sq2 = P0 - suf_q;
-            const double v1 = sq1 - sum1 * sum1 / N;
-            const double v2 = sq2 - sum2 * sum2 / N;
-            const double cv = Pi - sum1 * sum2 / N;
-            if (lane < K) a.acf_fused[s * K + lane] = cv / (__builtin_sqrt(v1) * __builtin_sqrt(v2));
+            const double r = acf_combine(
+                Pi, Sm, Qm, i, T,
+                [&](int j) {
+                    const double hx = __shfl(head.x, j >> 1), hy = __shfl(head.y, j >> 1);
+                    return (j & 1) ? hy : hx;
+                },
+                [&](int j) { return tail[T - 1 - j - kb_last]; });
+            if (lane < K) a.acf_fused[s * K + lane] = r;
         }
     }
 }

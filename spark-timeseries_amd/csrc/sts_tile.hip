@@ -19,15 +19,17 @@
 // reference bit for bit (no FMA: the library is built with -ffp-contract=off).
 // Runs longer than the halos fall back to a wave-wide scan of global memory.
 //
-// Autocorrelation: with y = F - F(0) (a shift; exact algebra for a correlation),
-// the kernel accumulates per tile P_i = sum_j y_j * y_{j+i} (i = 0..63) and
-// sum_j y_j for j in the tile, with y = 0 past the series end.  The lag products are
+// Autocorrelation: with y = F - c (c = the robust shift of sts_acf.hpp: the median of 64
+// samples of the series; exact algebra for a correlation), the kernel accumulates per
+// chunk P_i = sum_j y_j * y_{j+i} (i = 0..63) with y = 0 past the series end, and sum y /
+// sum y^2 over the series' middle [64, T - 64) in the store pass.  The lag products are
 // FP64 MFMA rank-4 updates: viewing the series as rows of 16, U_t = sum_a A_a^T A_{a+t}
 // (A_a = 16 consecutive steps) holds every pair at lag 16t + c - b; lane l of a wave
 // feeds element j0 + l as the A operand and j0 + 16t + l as the B operand of
 // v_mfma_f64_16x16x4_f64, so both operands are contiguous LDS reads.  A finalize
 // kernel (sts_acf_finalize) combines the tiles in a fixed order (deterministic).
 #include "sts_internal.hpp"
+#include "sts_acf.hpp"
 
 #include <hip/hip_runtime.h>
 
@@ -200,21 +202,19 @@ __global__ __launch_bounds__(NTH, 3) void tile_kernel(TileArgs a, int method) {
     const int ncols = a.max_lag + (a.include_original ? 1 : 0);
     const int init = a.include_original ? 0 : 1;
 
-    // ACF shift c0 = F(0), once per workgroup (before any prefetch is in flight)
+    // ACF shift c0 (sts_acf.hpp: median of 64 raw samples; identical in every workgroup of
+    // the series), once per workgroup before any prefetch is in flight
     double c0 = 0.0;
     if (NT > 0) {
         if (wave == 0) {
-            double x0 = src[0];
-            if (method == STS_FILL_NEXT && isnan_d(x0)) {
-                const int64_t f = scan_fwd(src, 0, T, lane);
-                x0 = (f < T) ? src[f] : __builtin_nan("");
-            }
-            if (lane == 0) sh_d_[0][0] = x0;
+            const double c = robust_shift(src, T, lane);
+            if (lane == 0) sh_d_[0][0] = c;
         }
         lds_barrier();
         c0 = sh_d_[0][0];
         lds_barrier();
     }
+    double acc_s = 0.0, acc_q = 0.0;   // sum y, sum y^2 over this thread's middle positions
 
     // register prefetch of one INTERIOR extended tile [e0, e0 + EW); the first and last tile
     // of a series (which touch its ends) are loaded synchronously with bounds checks
@@ -251,7 +251,6 @@ __global__ __launch_bounds__(NTH, 3) void tile_kernel(TileArgs a, int method) {
     d4 U[NA];
 #pragma unroll
     for (int t = 0; t < NA; t++) U[t] = d4{0.0, 0.0, 0.0, 0.0};
-    double sy = 0.0;
     bool series_err = false;
 
 #ifdef STS_STAMPS
@@ -513,6 +512,14 @@ __global__ __launch_bounds__(NTH, 3) void tile_kernel(TileArgs a, int method) {
                             y.x = fv[j].x - c0;
                             y.y = fv[j].y - c0;
                             v2[px2(vq + jj * kThreads)] = y;
+                            // middle sums: a fast tile ends >= REACH steps before T, so only
+                            // the series head (tile 0, positions < kAcfEdge) is excluded
+                            if (jj < FS && (t0 > 0 || tid + jj * kThreads >= kAcfEdge / 2)) {
+                                acc_s += y.x;
+                                acc_s += y.y;
+                                acc_q = __builtin_fma(y.x, y.x, acc_q);
+                                acc_q = __builtin_fma(y.y, y.y, acc_q);
+                            }
                         }
                     }
                 }
@@ -544,6 +551,17 @@ __global__ __launch_bounds__(NTH, 3) void tile_kernel(TileArgs a, int method) {
                     f.x = (q < qB) ? f.x - c0 : 0.0;
                     f.y = (q + 1 < qB) ? f.y - c0 : 0.0;
                     v2[px2(q2)] = f;
+                    if (q < qW) {
+                        const int64_t t = (int64_t)e0 + q;
+                        if (acf_mid(t, T)) {
+                            acc_s += f.x;
+                            acc_q = __builtin_fma(f.x, f.x, acc_q);
+                        }
+                        if (q + 1 < qW && acf_mid(t + 1, T)) {
+                            acc_s += f.y;
+                            acc_q = __builtin_fma(f.y, f.y, acc_q);
+                        }
+                    }
                 }
             }
             // shifted scheme, first tile: the pre-chunk (positions [0, 4t) of the series) reads
@@ -588,7 +606,6 @@ __global__ __launch_bounds__(NTH, 3) void tile_kernel(TileArgs a, int method) {
 #pragma unroll
                     for (int t = 0; t < NT; t++)
                         U[t % NA] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[t], bv[t], U[t % NA], 0, 0, 0);
-                    sy += av[0];
                 };
                 // wave 0 of the first tile also runs chunk -1 (the look-back, y = 0), whose
                 // shifted windows hold the series' first QS t steps
@@ -618,7 +635,6 @@ __global__ __launch_bounds__(NTH, 3) void tile_kernel(TileArgs a, int method) {
 #pragma unroll
                         for (int t = 0; t < NT; t++)
                             U[t % NA] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[t], bv[t], U[t % NA], 0, 0, 0);
-                        sy += av[0];
                         __builtin_amdgcn_sched_barrier(0);   // one chunk's operands live at a time
                     }
                     c = cend;
@@ -645,7 +661,6 @@ __global__ __launch_bounds__(NTH, 3) void tile_kernel(TileArgs a, int method) {
 #pragma unroll
                         for (int t = 0; t < NT; t++)
                             U[t % NA] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[t], bv[t], U[t % NA], 0, 0, 0);
-                        sy += av[0];
 #pragma unroll
                         for (int t = 0; t < NT; t++) {
                             av[t] = an[t];
@@ -666,7 +681,6 @@ __global__ __launch_bounds__(NTH, 3) void tile_kernel(TileArgs a, int method) {
                     const double av = (jrel < tlen) ? bv[0] : 0.0;   // A only inside the tile
 #pragma unroll
                     for (int t = 0; t < NT; t++) U[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv[t], U[t], 0, 0, 0);
-                    sy += av;
                 }
             }
         }
@@ -718,10 +732,16 @@ __global__ __launch_bounds__(NTH, 3) void tile_kernel(TileArgs a, int method) {
             }
         }
 #pragma unroll
-        for (int d = 32; d >= 1; d >>= 1) sy += __shfl_xor(sy, d);
+        for (int d = 32; d >= 1; d >>= 1) {
+            acc_s += __shfl_xor(acc_s, d);
+            acc_q += __shfl_xor(acc_q, d);
+        }
         double* wsum = vals + kWaves * 256;
         wsum[wave * kPartStride + lane] = lagacc;
-        if (lane == 0) wsum[wave * kPartStride + 64] = sy;
+        if (lane == 0) {
+            wsum[wave * kPartStride + kPartSum] = acc_s;
+            wsum[wave * kPartStride + kPartSq] = acc_q;
+        }
         lds_barrier();
         if (wave == 0) {
             double* part = a.partials + ch * kPartStride;
@@ -730,21 +750,26 @@ __global__ __launch_bounds__(NTH, 3) void tile_kernel(TileArgs a, int method) {
             for (int w = 0; w < kWaves; w++) tot += wsum[w * kPartStride + lane];
             part[lane] = tot;
             if (lane == 0) {
-                double ts = 0.0;
+                double ts = 0.0, tq = 0.0;
 #pragma unroll
-                for (int w = 0; w < kWaves; w++) ts += wsum[w * kPartStride + 64];
-                part[64] = ts;
+                for (int w = 0; w < kWaves; w++) {
+                    ts += wsum[w * kPartStride + kPartSum];
+                    tq += wsum[w * kPartStride + kPartSq];
+                }
+                part[kPartSum] = ts;
+                part[kPartSq] = tq;
+                part[kPartShift] = c0;
             }
         }
     }
 }
 
-// One wave per series: combine tile partials in tile order (deterministic), apply the
-// head/tail corrections, and form the reference's correlation
-//   cov / (sqrt(var1) * sqrt(var2))            (S/UnivariateTimeSeries.scala:80-89)
-// from shifted moments.  Lane l computes lag i = l + 1.  Series with T <= 2K run the
-// reference's two-pass loop directly (reproduces its NaN pattern exactly when a NaN sits
-// in the middle of a short series).
+// One wave per series: combine the chunk partials in chunk order (deterministic) and form
+// the reference's correlation cov / (sqrt(var1) * sqrt(var2)) (S/UnivariateTimeSeries.scala:
+// 80-89) with the robust head / tail handling of sts_acf.hpp.  Lane l computes lag i = l + 1.
+// Series with T <= 2K (or shorter than the two edges) run the reference's two-pass loop
+// directly (reproduces its NaN pattern exactly when a NaN sits in the middle of a short
+// series).
 __global__ __launch_bounds__(256) void acf_finalize_kernel(FinalizeArgs a) {
     const int lane = threadIdx.x & 63;
     const int64_t s = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -757,7 +782,7 @@ __global__ __launch_bounds__(256) void acf_finalize_kernel(FinalizeArgs a) {
     double out;
     if (i >= T) {
         out = __builtin_nan("");
-    } else if (T <= 2 * (int64_t)K) {
+    } else if (T <= 2 * (int64_t)K || T < 2 * kAcfEdge) {
         const int64_t len = T - i;
         double s1 = 0.0, s2 = 0.0;
         for (int64_t j = 0; j < len; j++) s1 += F[i + j];
@@ -772,30 +797,16 @@ __global__ __launch_bounds__(256) void acf_finalize_kernel(FinalizeArgs a) {
         }
         out = cv / (__builtin_sqrt(v1) * __builtin_sqrt(v2));
     } else {
-        double Pi = 0.0, P0 = 0.0, Sy = 0.0;
+        double Pi = 0.0, Sm = 0.0, Qm = 0.0;
         const double* pp = a.partials + s * a.parts_per_series * kPartStride;
+        const double c = pp[kPartShift];
         for (int64_t k = 0; k < a.parts_per_series; k++, pp += kPartStride) {
             Pi += pp[i];
-            P0 += pp[0];
-            Sy += pp[64];
+            Sm += pp[kPartSum];
+            Qm += pp[kPartSq];
         }
-        const double c0 = F[0];
-        double pre_s = 0.0, pre_q = 0.0, suf_s = 0.0, suf_q = 0.0;
-        for (int j = 0; j < i; j++) {
-            double y = F[j] - c0;
-            pre_s += y;
-            pre_q += y * y;
-            double z = F[T - 1 - j] - c0;
-            suf_s += z;
-            suf_q += z * z;
-        }
-        const double N = (double)(T - i);
-        const double sum1 = Sy - pre_s, sum2 = Sy - suf_s;
-        const double sq1 = P0 - pre_q, sq2 = P0 - suf_q;
-        const double v1 = sq1 - sum1 * sum1 / N;
-        const double v2 = sq2 - sum2 * sum2 / N;
-        const double cv = Pi - sum1 * sum2 / N;
-        out = cv / (__builtin_sqrt(v1) * __builtin_sqrt(v2));
+        out = acf_combine(Pi, Sm, Qm, i, T, [&](int j) { return F[j] - c; },
+                          [&](int j) { return F[T - 1 - j] - c; });
     }
     a.acf[s * K + lane] = out;
 }
@@ -806,12 +817,14 @@ hipError_t launch_tile(int method, int tw, const TileArgs& a, hipStream_t st) {
     const int64_t nchunk = a.S * a.chunks_per_series;
     if (nchunk <= 0) return hipSuccess;
     if (nchunk > 0x7fffffffLL) return hipErrorInvalidValue;
-    dim3 grid((unsigned)nchunk), block(kThreads), half(kThreads / 2);
+    dim3 grid((unsigned)nchunk), block(kThreads);
     if (tw == 512 && a.K == 0) {
         hipLaunchKernelGGL((tile_kernel<512, 0, false, kThreads>), grid, block, 0, st, a, method);
-    } else if (tw == 2048 && a.K > 0 && a.K <= 60) {   // 2-wave workgroups (A/B: STS_TILE_W=2048)
-        if (a.K <= 24) hipLaunchKernelGGL((tile_kernel<2048, 2, true, kThreads / 2>), grid, half, 0, st, a, method);
-        else hipLaunchKernelGGL((tile_kernel<2048, 4, true, kThreads / 2>), grid, half, 0, st, a, method);
+#ifdef STS_AB
+    } else if (tw == 2048 && a.K > 0 && a.K <= 60) {   // 2-wave workgroups (A/B build: STS_TILE_W=2048)
+        if (a.K <= 24) hipLaunchKernelGGL((tile_kernel<2048, 2, true, kThreads / 2>), grid, dim3(kThreads / 2), 0, st, a, method);
+        else hipLaunchKernelGGL((tile_kernel<2048, 4, true, kThreads / 2>), grid, dim3(kThreads / 2), 0, st, a, method);
+#endif
     } else if (tw == 4096) {
         if (a.K == 0) hipLaunchKernelGGL((tile_kernel<4096, 0, false, kThreads>), grid, block, 0, st, a, method);
         else if (a.K <= 24) hipLaunchKernelGGL((tile_kernel<4096, 2, true, kThreads>), grid, block, 0, st, a, method);

@@ -112,6 +112,29 @@ def lib():
     return load_library()
 
 
+_variants = {}
+
+
+def load_variant(path: str):
+    """Bind ANOTHER build of the library (same C ABI) without touching the product handle:
+    build/libsts_hip_ab.so (A/B experiment knobs, -DSTS_AB) for the knob parity tests and
+    tools/.  The product library never reads its environment."""
+    with _lock:
+        if path not in _variants:
+            if not os.path.exists(path):
+                raise NativeLibraryError("library variant not found at %s" % path)
+            v = ctypes.CDLL(path)
+            for name, (res, args) in SIGNATURES.items():
+                fn = getattr(v, name)
+                fn.restype = res
+                fn.argtypes = args
+            _variants[path] = v
+    return _variants[path]
+
+
+AB_LIB_PATH = os.path.join(PKG_ROOT, "build", "libsts_hip_ab.so")
+
+
 def ensure_device(device: int) -> None:
     """sts_init(device) once per (thread, device): selects the HIP device and checks gfx950."""
     key = (threading.get_ident(), device)

@@ -16,3 +16,20 @@ for p in (ROOT, os.path.join(ROOT, "oracle"), os.path.join(ROOT, "spark-timeseri
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (HIP device) and libsts_hip.so")
+
+
+import pytest  # noqa: E402
+
+
+@pytest.fixture
+def ab_lib(monkeypatch):
+    """Route the sparkts mirror through build/libsts_hip_ab.so (the -DSTS_AB build that reads
+    the A/B experiment knobs) for one test; the product libsts_hip.so ignores the
+    environment.  Yields a setter: ab_lib(NAME=value, ...) sets knobs for this test."""
+    from sparkts import _native
+    monkeypatch.setattr(_native, "_lib", _native.load_variant(_native.AB_LIB_PATH))
+
+    def knobs(**kv):
+        for k, v in kv.items():
+            monkeypatch.setenv(k, str(v))
+    return knobs

@@ -211,9 +211,11 @@ def test_gpu_loglik_gradient(torch):
 def pass_budget(request, monkeypatch):
     """Passes a series runs in garch_fit_kernel before garch_tail_kernel (one wave per series)
     takes it over: 1 sends every series past its first pass to the tail kernel, 0 disables
-    the tail phase."""
+    the tail phase.  The overrides run on the A/B build (libsts_hip_ab.so); "default" is the
+    product library."""
     if request.param != "default":
-        monkeypatch.setenv("STS_GARCH_PASS_BUDGET", request.param)
+        ab = request.getfixturevalue("ab_lib")
+        ab(STS_GARCH_PASS_BUDGET=request.param)
     return request.param
 
 

@@ -234,25 +234,24 @@ def test_fill_autocorr_fused(torch, method):
         assert_rel(host(acf), racf, what=method)
 
 
-# A/B knob settings that change the decomposition: each must stay parity-green
+# Both imputation kernels on every length, whatever the product dispatch picks, and the A/B
+# knob settings that change the decomposition -- all through the A/B build
+# (libsts_hip_ab.so); each must stay parity-green.
 KNOB_VARIANTS = {
-    "tile2048": ("tile", {"STS_TILE_W": "2048"}),          # 2-wave workgroups, 2048-step tiles
-    "tilec4": ("tile", {"STS_TILES_PER_CHUNK": "4"}),      # 4 tiles per workgroup
-    "seg3": ("seg", {"STS_SEG_TILES": "3"}),               # multi-segment partials + finalize
+    "tile": {"STS_TILE_KERNEL": "tile"},
+    "seg": {"STS_TILE_KERNEL": "seg"},
+    "tile2048": {"STS_TILE_KERNEL": "tile", "STS_TILE_W": "2048"},    # 2-wave workgroups, 2048-step tiles
+    "tilec4": {"STS_TILE_KERNEL": "tile", "STS_TILES_PER_CHUNK": "4"},  # 4 tiles per workgroup
+    "seg3": {"STS_TILE_KERNEL": "seg", "STS_SEG_TILES": "3"},          # multi-segment partials + finalize
 }
 
 
-@pytest.mark.parametrize("kernel", ["tile", "seg", "tile2"] + sorted(KNOB_VARIANTS))
+@pytest.mark.parametrize("kernel", sorted(KNOB_VARIANTS))
 @pytest.mark.parametrize("method", ["linear", "previous", "next", "nearest"])
-def test_fill_autocorr_both_kernels(torch, monkeypatch, kernel, method):
-    # both imputation kernels, whatever the length-based dispatch picks: the workgroup
-    # tile kernel and the wave-private segment kernel (STS_TILE_KERNEL forces one)
+def test_fill_autocorr_both_kernels(torch, ab_lib, kernel, method):
     from sparkts import TimeSeriesRDD
     from sparkts import UnivariateTimeSeries as uts
-    forced, knobs = KNOB_VARIANTS.get(kernel, (kernel, {}))
-    monkeypatch.setenv("STS_TILE_KERNEL", forced)
-    for k, v in knobs.items():
-        monkeypatch.setenv(k, v)
+    ab_lib(**KNOB_VARIANTS[kernel])
     rng = np.random.default_rng(zlib.crc32(("both%s%s" % (kernel, method)).encode()))
     for S, T, K in [(7, 600, 20), (5, 2520, 60), (3, 16384 + 77, 24), (2, 70000, 60), (2, 513, 0)]:
         x = random_panel(rng, S, T, 0.07, runs=True)
@@ -270,37 +269,42 @@ def test_fill_autocorr_both_kernels(torch, monkeypatch, kernel, method):
             assert_bits(got, ref, "%s %s T=%d" % (kernel, method, T))
 
 
-@pytest.mark.parametrize("T", [121, 512, 575, 576, 1000, 1024, 2520, 4097, 16384])
+@pytest.mark.parametrize("T", [121, 128, 512, 575, 576, 1000, 1024, 2520, 4097, 16384])
 def test_fused_acf_finalize_matches_two_kernel_path(torch, monkeypatch, T):
     # one segment per series: the segment kernel finalizes the ACF itself (no partials, no
-    # second launch) when T > 2K and its last tile holds >= 64 steps; bit-identical to the
-    # separate acf_finalize_kernel, and err is written for every series without a memset
+    # second launch) when T > 2K, T >= 128 and its last tile holds >= 64 steps; bit-identical
+    # to the separate acf_finalize_kernel (forced with STS_NO_FUSED_ACF on the A/B build), and
+    # err is written for every series without a memset
     from sparkts import TimeSeriesRDD
+    from sparkts import _native
     rng = np.random.default_rng(T)
     x = random_panel(rng, 9, T, 0.05, runs=True)
     x[4] = 7.0                                            # constant: 0/0 = NaN
     x[5, 0] = NaN                                         # head NaN -> all-NaN ACF
+    prod = _native.lib()
+    ab = _native.load_variant(_native.AB_LIB_PATH)
     for K in (1, 20, 60):
         if T <= 2 * K:
             continue
         f1, a1 = TimeSeriesRDD(None, None, dev(torch, x)).fillAndAutocorr("linear", K)
+        monkeypatch.setattr(_native, "_lib", ab)
         monkeypatch.setenv("STS_NO_FUSED_ACF", "1")
         f2, a2 = TimeSeriesRDD(None, None, dev(torch, x)).fillAndAutocorr("linear", K)
         monkeypatch.delenv("STS_NO_FUSED_ACF")
+        monkeypatch.setattr(_native, "_lib", prod)
         assert_bits(host(a1), host(a2), "fused vs separate finalize T=%d K=%d" % (T, K))
         assert_bits(host(f1.data), host(f2.data), "filled")
         _, racf, _ = oracle.panel_fill_autocorr(x, "linear", K)
         assert_rel(host(a1), racf, what="fused T=%d K=%d" % (T, K))
     # err written for every series (stale values in the caller's array are overwritten)
-    from sparkts import _native
     xn = x.copy()
     xn[2, 1:] = NaN
     xd = dev(torch, xn)
     out = torch.empty_like(xd)
     acf = torch.empty((9, 20), dtype=torch.float64, device="cuda:0")
     err = torch.full((9,), 99, dtype=torch.int32, device="cuda:0")
-    st = _native.lib().sts_fill_autocorr(xd.data_ptr(), out.data_ptr(), 9, T, T, T, 1, 20, acf.data_ptr(),
-                                         err.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    st = prod.sts_fill_autocorr(xd.data_ptr(), out.data_ptr(), 9, T, T, T, 1, 20, acf.data_ptr(),
+                                err.data_ptr(), torch.cuda.current_stream().cuda_stream)
     assert st == 0
     want = np.zeros(9, np.int32)
     want[2] = 2                                            # nearest on [x0, NaN, ...]: "Input is all NaNs!"
@@ -554,11 +558,13 @@ def test_ar_fit_register_path_shapes(torch, p):
 
 
 def test_ar_fit_register_path_matches_staged_on_nan(torch, monkeypatch):
-    # NaN anywhere -> NaN model, same as the LDS-staged kernel
+    # NaN anywhere -> NaN model, same as the LDS-staged kernel (forced on the A/B build)
+    from sparkts import _native
     from sparkts.models import Autoregression
     x = oracle.gen_ar_panel(8, 4, 2520, 5)
     x[1, 700] = NaN
     got = Autoregression.fitModel(dev(torch, x), 5)
+    monkeypatch.setattr(_native, "_lib", _native.load_variant(_native.AB_LIB_PATH))
     monkeypatch.setenv("STS_AR_STAGED", "1")
     ref = Autoregression.fitModel(dev(torch, x), 5)
     assert np.isnan(host(got.c)[1]) and np.isnan(host(ref.c)[1])
