@@ -11,11 +11,13 @@
 // about eps * N * (sigma^2 + (mean - c)^2), so (mean - c)^2 / sigma^2 is the number of
 // bits lost.  Two rules keep that ratio O(1):
 //
-//  1. c is the MEDIAN of the valid values among 64 samples spread evenly over the series
-//     (robust_shift below; an outlier at x[0] or a level far from x[0] cannot move it;
-//     |median - mean| <= sigma for the sampled population).  Every workgroup of a series
-//     computes it from the same raw samples in the same order, so all of them agree bit
-//     for bit and the partials combine.
+//  1. c is the MEDIAN of the valid values among 64 samples of the series (an outlier at
+//     x[0] or a level far from x[0] cannot move it; |median - mean| <= sigma for the sampled
+//     population): spread evenly over the whole series in the tile kernel (robust_shift),
+//     and over its first 512-step tile in the segment kernel (T <= 16384 there, so a first
+//     tile at another level is >= 1/32 of the series and bounds (mean - c)^2 / sigma^2 by
+//     ~32).  Every workgroup / segment of a series computes it from the same raw samples the
+//     same way, so all of them agree bit for bit and the partials combine.
 //  2. sum y and sum y^2 are accumulated only over the MIDDLE [kAcfEdge, T - kAcfEdge) of
 //     the series; the head and tail (the only positions that differ between the lag
 //     slices, since K <= kAcfEdge) are added explicitly per lag (acf_combine).  The lag
@@ -39,27 +41,48 @@ __device__ __forceinline__ double acf_readlane(double v, int l) {
     return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
 }
 
+// The lower median of the valid per-lane samples v (ok: valid) of one wave, in the total
+// order (value, lane): a ballot quickselect -- each round takes the middle remaining
+// candidate as the pivot, counts the candidates below it with one ballot and keeps the side
+// that holds the wanted rank (a few scalar rounds; a sorted sample needs one).  0.0 when no
+// sample is valid.  Wave-uniform, deterministic (a pure function of the samples).
+__device__ __forceinline__ double median_of_lanes(double v, bool ok, int lane) {
+    unsigned long long cand = __ballot(ok);
+    int n = __popcll(cand);
+    if (n == 0) return 0.0;
+    int k = (n - 1) >> 1;                          // rank wanted among the candidates
+    for (;;) {
+        // pivot lane: the (n / 2)-th set bit of cand (popcount bisection, scalar)
+        unsigned long long m = cand;
+        int want = n >> 1, pl = 0;
+#pragma unroll
+        for (int width = 32; width >= 1; width >>= 1) {
+            const int c = __popcll(m & ((1ull << width) - 1ull));
+            if (want >= c) { want -= c; m >>= width; pl += width; }
+        }
+        const double pv = acf_readlane(v, pl);
+        const bool in = (cand >> lane) & 1ull;
+        const unsigned long long lt = __ballot(in && (v < pv || (v == pv && lane < pl)));
+        const int cnt = __popcll(lt);
+        if (cnt == k) return pv;
+        if (cnt > k) {
+            cand = lt;
+        } else {
+            cand &= ~lt & ~(1ull << pl);
+            k -= cnt + 1;
+        }
+        n = __popcll(cand);
+    }
+}
+
 // Robust shift of series `src` (length T >= 1), computed by one whole wave: lane l samples
-// x[t_l] (or x[t_l + 1] when x[t_l] is NaN), t_l = l * T / 64; the result is the lower
-// median of the valid samples (ranks by value, ties by lane).  0.0 when every sample is
-// NaN (the series is then almost all NaN; any constant is exact algebra).  Wave-uniform.
+// x[t_l] (or x[t_l + 1] when x[t_l] is NaN), t_l = l * T / 64, spread over the whole series;
+// the result is the lower median of the valid samples.
 __device__ __forceinline__ double robust_shift(const double* src, int64_t T, int lane) {
     const int64_t t = (int64_t)lane * T / 64;
     double v = src[t];
     if (__builtin_isnan(v) && t + 1 < T) v = src[t + 1];
-    const bool ok = !__builtin_isnan(v);
-    const unsigned long long m = __ballot(ok);
-    const int n = __popcll(m);
-    if (n == 0) return 0.0;
-    int rank = 0;
-#pragma unroll 8
-    for (int j = 0; j < 64; j++) {
-        const double vj = acf_readlane(v, j);
-        const bool vj_ok = (m >> j) & 1ull;
-        rank += (vj_ok && (vj < v || (vj == v && j < lane))) ? 1 : 0;
-    }
-    const unsigned long long sel = __ballot(ok && rank == ((n - 1) >> 1));
-    return acf_readlane(v, __ffsll((long long)sel) - 1);
+    return median_of_lanes(v, !__builtin_isnan(v), lane);
 }
 
 // True when series position t contributes to the middle sums (rule 2).

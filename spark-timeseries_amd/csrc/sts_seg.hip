@@ -40,6 +40,7 @@
 // same for every t, so the NT accumulators are summed before the diagonal extraction.
 #include "sts_internal.hpp"
 #include "sts_acf.hpp"
+#include "sts_scan.hpp"
 
 #include <hip/hip_runtime.h>
 
@@ -56,6 +57,8 @@ constexpr int kRing = 2 * kW + 128;   // two slots + a mirror of slot 0's head
 constexpr int kWaves = 4;             // waves per workgroup (independent)
 constexpr int kBig = 0x7fffffff;
 
+constexpr int kMaxRuns = kW / (kLongRun + 2) + 2;   // runs with chain-pass steps in one tile
+
 struct WaveLds {
     double ring[kRing];
     unsigned long long m2[2][kWords]; // validity masks of the tiles in ring slots 0 / 1
@@ -63,6 +66,14 @@ struct WaveLds {
     int lastUp[kWords];               // last valid global index in words <= w (carry: < tile)
     int firstFrom[kWords];            // first valid global index in words >= w (look-ahead)
     int wbase[kWords + 1];            // exclusive prefix count of need bits
+    // linear fill, chain pass (as in sts_tile.hip): runs with steps more than kLongRun past
+    // L, and the chain value at the last step of the previous tile (by tile parity)
+    int nlong;
+    int run_q[kMaxRuns], run_L[kMaxRuns], run_N[kMaxRuns];
+    double run_Lv[kMaxRuns], run_Nv[kMaxRuns];
+    int carry_L[2], carry_t[2];
+    double carry_r[2];
+    int cN_pos, cN;                   // cache of the global look-ahead scan: first valid >= cN_pos is cN
 };
 
 __device__ __forceinline__ bool isnan_d(double v) { return __builtin_isnan(v); }
@@ -92,28 +103,6 @@ __device__ __forceinline__ double readlane_d(double v, int l) {
     const unsigned lo = __builtin_amdgcn_readlane((unsigned)u, l);
     const unsigned hi = __builtin_amdgcn_readlane((unsigned)(u >> 32), l);
     return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
-}
-
-// Wave-wide search of global memory for the last valid index < from (-1: none).
-__device__ int scan_back(const double* src, int from, int lane) {
-    for (int base = from - 64;; base -= 64) {
-        const int t = base + lane;
-        const bool v = (t >= 0 && t < from) ? !isnan_d(src[t]) : false;
-        const unsigned long long m = __ballot(v);
-        if (m) return base + 63 - __clzll(m);
-        if (base <= 0) return -1;
-    }
-}
-
-// Wave-wide search for the first valid index >= from (T: none).
-__device__ int scan_fwd(const double* src, int from, int T, int lane) {
-    for (int base = from;; base += 64) {
-        if (base >= T) return T;
-        const int t = base + lane;
-        const bool v = (t < T) ? !isnan_d(src[t]) : false;
-        const unsigned long long m = __ballot(v);
-        if (m) return base + __ffsll(m) - 1;
-    }
 }
 
 // One tile into registers: lane l, register u holds steps kb + 128u + 2l (+1).
@@ -228,6 +217,42 @@ __device__ __forceinline__ int masks_to_lds(const v2d (&R)[4], unsigned long lon
     return f;
 }
 
+// Linear fill, chain pass: one lane per long run walks r = r + inc through the run's steps in
+// tile [kb, tend), starting from the previous tile's carried value when the run continues from
+// it, else replaying from L.
+__device__ __forceinline__ void chain_pass(WaveLds& w, double* ring, int kb, int tend, int lane) {
+    const int nl = __builtin_amdgcn_readfirstlane(w.nlong);
+    const int rd = ((kb / kW) + 1) & 1, wr = (kb / kW) & 1;
+    for (int r = lane; r < nl; r += 64) {
+        const int q0 = w.run_q[r], L = w.run_L[r], N = w.run_N[r];
+        const double Lv = w.run_Lv[r];
+        const double inc = (w.run_Nv[r] - Lv) / (double)(N - L);
+        const int tstart = kb + q0;
+        double v;
+        if (w.carry_L[rd] == L && w.carry_t[rd] == tstart - 1) {
+            v = w.carry_r[rd];
+        } else {
+            v = Lv;
+            int j = tstart - 1 - L;   // replay from L, 8 dependent adds per trip
+            for (; j >= 8; j -= 8) {
+                v = v + inc; v = v + inc; v = v + inc; v = v + inc;
+                v = v + inc; v = v + inc; v = v + inc; v = v + inc;
+            }
+            for (; j > 0; j--) v = v + inc;
+        }
+        for (int q = q0; kb + q < tend && kb + q < N; q++) {
+            v = v + inc;
+            ring[q] = v;
+            if (q == kW - 1) {
+                w.carry_L[wr] = L;
+                w.carry_t[wr] = kb + kW - 1;
+                w.carry_r[wr] = v;
+            }
+        }
+    }
+    wave_sync();
+}
+
 // Impute tile k (ring slot SLOT, raw; masks in w.m2[SLOT]) and turn it into y; optionally
 // store it.  look: first valid index >= kb + kW when known (kBig: unknown, then scan
 // global memory from scan_from); lookv its value.
@@ -272,8 +297,13 @@ __device__ __forceinline__ void impute_tile(WaveLds& w, const double* src, doubl
                 f = look;
                 fv = lookv;
                 if (look == kBig) {
-                    if (lastneed > lastv) {
-                        f = scan_fwd(src, scan_from, T, lane);
+                    if (lastneed > lastv) {   // a long gap is scanned once, not once per tile
+                        const int cp = w.cN_pos, cn = w.cN;
+                        f = (cp >= 0 && cp <= scan_from && cn >= scan_from) ? cn : (int)scan_fwd(src, scan_from, T, lane);
+                        if (lane == 0) {
+                            w.cN_pos = scan_from;
+                            w.cN = f;
+                        }
                         fv = (f < T) ? src[f] : 0.0;
                     } else {
                         f = T;
@@ -287,6 +317,7 @@ __device__ __forceinline__ void impute_tile(WaveLds& w, const double* src, doubl
                     if (lane == 0) w.firstFrom[i] = ff;
                 }
             }
+            if (lane == 0) w.nlong = 0;
             wave_sync();
             // ---- impute the compacted NaN positions; F goes into the ring in place
             //      (every (L, N) source is a valid position, never rewritten) ----
@@ -335,6 +366,17 @@ __device__ __forceinline__ void impute_tile(WaveLds& w, const double* src, doubl
                 }
                 case STS_FILL_LINEAR: {
                     if (Lt < 0 || Nt >= T) break;             // runs touching index 0 or n-1 stay NaN
+                    if (t - Lt > kLongRun) {                  // the chain pass produces this step
+                        if (t - Lt == kLongRun + 1 || q == 0) {
+                            const int rr = atomicAdd(&w.nlong, 1);
+                            w.run_q[rr] = q;
+                            w.run_L[rr] = Lt;
+                            w.run_N[rr] = Nt;
+                            w.run_Lv[rr] = Lv;
+                            w.run_Nv[rr] = Nv;
+                        }
+                        continue;
+                    }
                     const double inc = (Nv - Lv) / (double)(Nt - Lt);
                     double acc = Lv;
                     for (int j = t - Lt; j > 0; j--) acc = acc + inc;   // sequential, as :259-261
@@ -348,6 +390,9 @@ __device__ __forceinline__ void impute_tile(WaveLds& w, const double* src, doubl
             }
         }
         wave_sync();
+        // ---- linear fill, chain pass (rare: a run with steps more than kLongRun past L) ----
+        if (method == STS_FILL_LINEAR && nnan > 0 && __builtin_amdgcn_readfirstlane(w.nlong) > 0)
+            chain_pass(w, ring, kb, tend, lane);
         if (lastv >= 0) {
             st.Lc = lastv;
             st.Lv = ring[lastv - kb];
@@ -377,15 +422,12 @@ __device__ __forceinline__ void impute_tile(WaveLds& w, const double* src, doubl
             y.x = (full || t < T) ? f.x - st.c0 : 0.0;
             y.y = (full || t + 1 < T) ? f.y - st.c0 : 0.0;
             r2[64 * u] = y;
-            if (own) {
-                if (acf_mid(t, T)) {
-                    st.sm += y.x;
-                    st.qm = __builtin_fma(y.x, y.x, st.qm);
-                }
-                if (acf_mid(t + 1, T)) {
-                    st.sm += y.y;
-                    st.qm = __builtin_fma(y.y, y.y, st.qm);
-                }
+            if (own) {   // sum y / sum y^2 over the series' middle (sts_acf.hpp rule 2)
+                const double zx = acf_mid(t, T) ? y.x : 0.0, zy = acf_mid(t + 1, T) ? y.y : 0.0;
+                st.sm += zx;
+                st.sm += zy;
+                st.qm = __builtin_fma(zx, zx, st.qm);
+                st.qm = __builtin_fma(zy, zy, st.qm);
             }
             if (SLOT == 0 && u == 0) reinterpret_cast<v2d*>(w.ring + 2 * kW)[lane] = y;
             if (u == 0 && kb == 0) head = y;          // y(2 lane), y(2 lane + 1): fused ACF finalize
@@ -482,11 +524,15 @@ __global__ __launch_bounds__(256, 4) void seg_kernel(TileArgs a, int method) {
     st.c0 = 0.0;
     st.sm = 0.0;
     st.qm = 0.0;
+    if (lane == 0) w.cN_pos = -1;
+    if (lane < 2) {
+        w.carry_L[lane] = -1;
+        w.carry_t[lane] = -kBig;   // matches no tile start
+    }
     st.Lc = -1;
     st.Lv = 0.0;
-    if (NT > 0) st.c0 = robust_shift(cx.src, cx.T, lane);   // the same value in every segment
     if (needL && cx.k0 > 0) {
-        st.Lc = scan_back(cx.src, cx.k0 * kW, lane);
+        st.Lc = (int)scan_back(cx.src, cx.k0 * kW, lane);
         st.Lv = (st.Lc >= 0) ? cx.src[st.Lc] : 0.0;
     }
 
@@ -498,6 +544,22 @@ __global__ __launch_bounds__(256, 4) void seg_kernel(TileArgs a, int method) {
     v2d RA[4], RB[4];
     load_tile(RA, cx.src, cx.k0 * kW, cx.T, lane);
     if (cx.k0 + 1 <= cx.kLast) load_tile(RB, cx.src, (cx.k0 + 1) * kW, cx.T, lane);
+    if (NT > 0) {
+        // ACF shift (sts_acf.hpp): median of 64 samples of the series' first tile, lane l taking
+        // step 128 (l & 3) + 2 l (or the step after it when NaN) from the registers -- no
+        // extra load for segment 0; later segments (A/B build only) load tile 0 themselves
+        v2d R0[4];
+        if (g == 0) {
+#pragma unroll
+            for (int u = 0; u < 4; u++) R0[u] = RA[u];
+        } else {
+            load_tile(R0, cx.src, 0, cx.T, lane);
+        }
+        const int u = lane & 3;
+        const v2d r = (u == 0) ? R0[0] : (u == 1) ? R0[1] : (u == 2) ? R0[2] : R0[3];
+        const double v = __builtin_isnan(r.x) ? r.y : r.x;
+        st.c0 = median_of_lanes(v, !__builtin_isnan(v), lane);
+    }
     masks_to_lds(RA, w.m2[0], lane);
     raw_to_slot(w.ring, RA, lane);
     if (NT > 0 && g == 0) zero_slot<1>(w, lane);     // "tile -1": y = 0 before the series

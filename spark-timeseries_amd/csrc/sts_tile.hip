@@ -16,8 +16,11 @@
 // the first valid index N(t) >= t.  From (L, N) every method is a copy except linear,
 // whose reference loop accumulates r[j] = r[j-1] + inc SEQUENTIALLY from the run
 // start: each NaN step replays that chain from L (t - L adds), which reproduces the
-// reference bit for bit (no FMA: the library is built with -ffp-contract=off).
-// Runs longer than the halos fall back to a wave-wide scan of global memory.
+// reference bit for bit (no FMA: the library is built with -ffp-contract=off).  Steps more
+// than kLongRun past L are instead produced by a per-run CHAIN pass (one lane walks the run
+// once, carrying its value across the workgroup's tiles), so a gap of G steps costs O(G),
+// not O(G^2).  Runs longer than the halos find L / N with a 512-step-wide scan of global
+// memory whose answer is cached for the workgroup's next tiles.
 //
 // Autocorrelation: with y = F - c (c = the robust shift of sts_acf.hpp: the median of 64
 // samples of the series; exact algebra for a correlation), the kernel accumulates per
@@ -30,6 +33,7 @@
 // kernel (sts_acf_finalize) combines the tiles in a fixed order (deterministic).
 #include "sts_internal.hpp"
 #include "sts_acf.hpp"
+#include "sts_scan.hpp"
 
 #include <hip/hip_runtime.h>
 
@@ -45,9 +49,6 @@
 #define STS_LDS_BARRIER 1
 #endif
 
-#ifndef STS_WAVE_SCAN
-#define STS_WAVE_SCAN 0        // every wave runs the word scan into its own LDS copy (no barrier)
-#endif
 
 namespace sts {
 namespace {
@@ -109,28 +110,6 @@ __device__ __forceinline__ unsigned long long interleave2(unsigned ev, unsigned 
     return (bitrep(ev) & 0x5555555555555555ull) | (bitrep(od) & 0xAAAAAAAAAAAAAAAAull);
 }
 
-// Wave-wide search of global memory for the last valid index < from (stop at 0).
-__device__ int64_t scan_back(const double* src, int64_t from, int lane) {
-    for (int64_t base = from - 64;; base -= 64) {
-        int64_t t = base + lane;
-        bool v = (t >= 0 && t < from) ? !isnan_d(src[t]) : false;
-        unsigned long long m = __ballot(v);
-        if (m) return base + 63 - __clzll(m);
-        if (base <= 0) return -1;
-    }
-}
-
-// Wave-wide search for the first valid index >= from (stop at T).
-__device__ int64_t scan_fwd(const double* src, int64_t from, int64_t T, int lane) {
-    for (int64_t base = from;; base += 64) {
-        int64_t t = base + lane;
-        bool v = (t < T) ? !isnan_d(src[t]) : false;
-        unsigned long long m = __ballot(v);
-        if (m) return base + __ffsll(m) - 1;
-        if (base + 64 >= T) return T;
-    }
-}
-
 // Padded LDS index of extended-tile position q: 4 doubles of padding per 32.  Keeps the
 // lag-product B-operand gathers (16-step-spaced groups, see below) conflict-free across the
 // 64 LDS banks; 16-B pairs (even q) never straddle a pad.
@@ -166,24 +145,28 @@ __global__ __launch_bounds__(NTH, 3) void tile_kernel(TileArgs a, int method) {
     static_assert(NW <= 128, "word scan handles at most 128 words");
     __shared__ __attribute__((aligned(16))) double vals[EWP];   // padded (px) for the shifted scheme
     __shared__ unsigned long long mask[NW];
-    constexpr int NSC = STS_WAVE_SCAN ? kWaves : 1;   // copies of the scan results
-    __shared__ int lastUpTo_[NSC][NW];     // last valid E-position in words <= w (-1: none)
-    __shared__ int firstFrom_[NSC][NW];    // first valid E-position in words >= w (kBig: none)
-    __shared__ int wbase_[NSC][NW + 1];    // NaN-list offset of each word (exclusive prefix count)
-    __shared__ unsigned long long wneed_[NSC][NW];   // NaN positions to impute, per word
-    __shared__ int sh_i_[NSC][3];          // lext, next (series positions), NaN count
-    __shared__ double sh_d_[NSC][3];       // c0, value at lext, value at next
+    __shared__ int lastUpTo[NW];           // last valid E-position in words <= w (-1: none)
+    __shared__ int firstFrom[NW];          // first valid E-position in words >= w (kBig: none)
+    __shared__ int wbase[NW + 1];          // NaN-list offset of each word (exclusive prefix count)
+    __shared__ unsigned long long wneed[NW];   // NaN positions to impute, per word
+    __shared__ int sh_i[4];                // lext, next (series positions), NaN count, long runs
+    __shared__ double sh_d[3];             // c0, value at lext, value at next
+    // linear fill, chain pass: runs with steps more than kLongRun past L (registered by their
+    // first such step in the tile), and the chain value at the last step of the previous
+    // tile (double-buffered by tile parity: read [(k + 1) & 1], write [k & 1])
+    constexpr int kMaxRuns = EW / (kLongRun + 2) + 2;
+    __shared__ int run_q[kMaxRuns], run_L[kMaxRuns], run_N[kMaxRuns];
+    __shared__ double run_Lv[kMaxRuns], run_Nv[kMaxRuns];
+    __shared__ int carry_L[2], carry_t[2];
+    __shared__ double carry_r[2];
+    // wave 0's caches of the global scans (series positions; LDS, not registers: nothing is
+    // live across tiles for them): the last valid index before sh_c[0] is sh_c[1]; the first
+    // valid index at or after sh_c[2] is sh_c[3]
+    __shared__ int sh_c[4];
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform: scalar loop control
-    const int wsc = STS_WAVE_SCAN ? wave : 0;
-    int* lastUpTo = lastUpTo_[wsc];
-    int* firstFrom = firstFrom_[wsc];
-    int* wbase = wbase_[wsc];
-    unsigned long long* wneed = wneed_[wsc];
-    int* sh_i = sh_i_[wsc];
-    double* sh_d = sh_d_[wsc];
     // one workgroup = one CHUNK of tiles_per_chunk consecutive tiles of one series
     const int64_t nchunk = a.S * a.chunks_per_series;
     const int64_t ch = xcd_remap(blockIdx.x, nchunk);
@@ -202,17 +185,13 @@ __global__ __launch_bounds__(NTH, 3) void tile_kernel(TileArgs a, int method) {
     const int ncols = a.max_lag + (a.include_original ? 1 : 0);
     const int init = a.include_original ? 0 : 1;
 
-    // ACF shift c0 (sts_acf.hpp: median of 64 raw samples; identical in every workgroup of
-    // the series), once per workgroup before any prefetch is in flight
-    double c0 = 0.0;
-    if (NT > 0) {
-        if (wave == 0) {
-            const double c = robust_shift(src, T, lane);
-            if (lane == 0) sh_d_[0][0] = c;
-        }
-        lds_barrier();
-        c0 = sh_d_[0][0];
-        lds_barrier();
+    if (tid < 2) {
+        carry_L[tid] = -1;
+        carry_t[tid] = -kBig;   // matches no tile start
+    }
+    if (tid == 0) {
+        sh_c[0] = -kBig;
+        sh_c[2] = -1;
     }
     double acc_s = 0.0, acc_q = 0.0;   // sum y, sum y^2 over this thread's middle positions
 
@@ -260,6 +239,13 @@ __global__ __launch_bounds__(NTH, 3) void tile_kernel(TileArgs a, int method) {
     bool have = interior(k_begin);
     if (have) STS_ISSUE(k_begin);
     else STS_CLEAR();
+    // ACF shift (sts_acf.hpp: median of 64 raw samples; identical in every workgroup of the
+    // series): wave 0 computes it while its first tile's loads are in flight and leaves it in
+    // sh_d[0]; every wave reads it after the tile loop's first barrier (no extra barrier)
+    if (NT > 0 && wave == 0) {
+        const double c = robust_shift(src, T, lane);
+        if (lane == 0) sh_d[0] = c;
+    }
     for (int64_t k = k_begin; k < k_end; k++) {
         const int t0 = (int)(k * TW);
         const int t1 = (t0 + TW < T) ? t0 + TW : (int)T;
@@ -317,11 +303,15 @@ __global__ __launch_bounds__(NTH, 3) void tile_kernel(TileArgs a, int method) {
         }
         STAMP(3);
 
-        // ---- 3. word scans (wave 0, or every wave into its own copy; lane l: words 2l, 2l+1):
-        //      last valid position up to each word, first valid from each word, and the
-        //      NaN-list offset of each word ----
-        if (STS_WAVE_SCAN || wave == 0) {
-            const int w0 = 2 * lane, w1 = 2 * lane + 1;
+        // ---- 3. word scans (wave 0; lane l: words 2l, 2l+1): last valid position up to each
+        //      word, first valid from each word, and the NaN-list offset of each word ----
+        if (wave == 0) {
+            // opaque: recomputed per tile (two VALU ops) instead of hoisted out of the tile loop,
+            // where the derived LDS addresses were spilled to scratch and reloaded behind a
+            // vmcnt(0) on wave 0's critical path
+            int w0 = 2 * lane;
+            asm volatile("" : "+v"(w0));
+            const int w1 = w0 + 1;
             const unsigned long long m0 = (w0 < NW) ? mask[w0] : ~0ull;
             const unsigned long long m1 = (w1 < NW) ? mask[w1] : ~0ull;
             const int l0 = (w0 < NW && m0) ? w0 * 64 + 63 - __clzll(m0) : -1;
@@ -372,28 +362,41 @@ __global__ __launch_bounds__(NTH, 3) void tile_kernel(TileArgs a, int method) {
                 wbase[w1] = exc + __popcll(n0);
                 wneed[w1] = n1;
             }
-            // slow paths: a NaN run longer than the halos (rare)
+            // slow paths: a NaN run longer than the halos (rare); the answers are cached for
+            // the next tiles of this workgroup, so a long gap is scanned once per workgroup
             int lext = -1, next = (int)T;
-            if (needL && e0 > 0 && firstValidE > qA && nnan > 0) lext = (int)scan_back(src, e0, lane);
-            if (needN && e0 + EW < T && qB > qA && lastValidE < qB - 1 && nnan > 0)
-                next = (int)scan_fwd(src, e0 + EW, T, lane);
+            if (needL && e0 > 0 && firstValidE > qA && nnan > 0)
+                lext = (sh_c[0] == e0) ? sh_c[1] : (int)scan_back(src, e0, lane);
+            if (needN && e0 + EW < T && qB > qA && lastValidE < qB - 1 && nnan > 0) {
+                const int from = e0 + EW;
+                const int cN_pos = sh_c[2], cN = sh_c[3];
+                next = (cN_pos >= 0 && cN_pos <= from && cN >= from) ? cN : (int)scan_fwd(src, from, T, lane);
+                if (lane == 0) {
+                    sh_c[2] = from;
+                    sh_c[3] = next;
+                }
+            }
+            // the last valid index before the next tile's e0 = e0 + TW: in this tile's words
+            // [0, TW / 64) (lane TW / 128 - 1's inclusive prefix max), else lext
+            if (needL) {
+                const int lq = __shfl(pm, TW / 128 - 1);
+                if (lane == 0) {
+                    sh_c[0] = e0 + TW;
+                    sh_c[1] = (lq >= 0) ? e0 + lq : lext;
+                }
+            }
             if (lane == 0) {
                 wbase[NW] = nnan;
                 sh_i[0] = lext;
                 sh_i[1] = next;
                 sh_i[2] = nnan;
+                sh_i[3] = 0;
                 sh_d[1] = (lext >= 0) ? src[lext] : 0.0;
                 sh_d[2] = (next < T) ? src[next] : 0.0;
             }
         }
         STAMP(4);
-#if STS_WAVE_SCAN
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");   // own copy: wave-local order
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
-#else
         lds_barrier();
-#endif
         STAMP(5);
 
         // ---- 4. impute the compacted NaN positions, all lanes busy; F goes back into
@@ -453,6 +456,17 @@ __global__ __launch_bounds__(NTH, 3) void tile_kernel(TileArgs a, int method) {
                 }
                 case STS_FILL_LINEAR: {
                     if (Lt < 0 || Nt >= T) break;             // runs touching index 0 or n-1 stay NaN
+                    if (t - Lt > kLongRun) {                  // the chain pass produces this step
+                        if (t - Lt == kLongRun + 1 || q == qA) {
+                            const int r = atomicAdd(&sh_i[3], 1);
+                            run_q[r] = q;
+                            run_L[r] = Lt;
+                            run_N[r] = Nt;
+                            run_Lv[r] = Lv;
+                            run_Nv[r] = Nv;
+                        }
+                        continue;
+                    }
                     const double inc = (Nv - Lv) / (double)(Nt - Lt);
                     double r = Lv;
                     for (int j = t - Lt; j > 0; j--) r = r + inc;   // sequential, as :259-261
@@ -467,11 +481,47 @@ __global__ __launch_bounds__(NTH, 3) void tile_kernel(TileArgs a, int method) {
         }
         STAMP(6);
         lds_barrier();
+        // ---- 4b. linear fill, chain pass: one lane per long run walks r = r + inc through
+        //      the run's steps in [qA, qB), starting from the previous tile's carried value when
+        //      the run continues from it, else replaying from L ----
+        if (method == STS_FILL_LINEAR && sh_i[3] > 0) {
+            const int nl = sh_i[3];
+            const int rd = (int)((k + 1) & 1), wr = (int)(k & 1);
+            for (int r = tid; r < nl; r += kThreads) {
+                const int q0 = run_q[r], L = run_L[r], N = run_N[r];
+                const double Lv = run_Lv[r];
+                const double inc = (run_Nv[r] - Lv) / (double)(N - L);
+                const int tstart = e0 + q0;
+                double v;
+                if (carry_L[rd] == L && carry_t[rd] == tstart - 1) {
+                    v = carry_r[rd];
+                } else {
+                    v = Lv;
+                    int j = tstart - 1 - L;   // replay from L, 8 dependent adds per trip
+                    for (; j >= 8; j -= 8) {
+                        v = v + inc; v = v + inc; v = v + inc; v = v + inc;
+                        v = v + inc; v = v + inc; v = v + inc; v = v + inc;
+                    }
+                    for (; j > 0; j--) v = v + inc;
+                }
+                for (int q = q0; q < qB && e0 + q < N; q++) {
+                    v = v + inc;
+                    vals[px(q)] = v;
+                    if (e0 + q == t1 - 1) {
+                        carry_L[wr] = L;
+                        carry_t[wr] = t1 - 1;
+                        carry_r[wr] = v;
+                    }
+                }
+            }
+            lds_barrier();
+        }
         STAMP(7);
 
         // ---- 5. filled output + lag matrix (16-B stores), then y = F - F(0) in place
         //      (0 past the series end) for the MFMA phase; start the next tile's loads ----
         {
+            const double c0 = sh_d[0];
             const bool al = dst && ((reinterpret_cast<uintptr_t>(dst) & 15) == 0);
             double2* v2 = reinterpret_cast<double2*>(vals);
             const int qBfull = (NT > 0) ? ((SHIFTED || qW + 64 + 16 * NT >= EW) ? EW : qW + 64 + 16 * NT) : 0;
@@ -512,14 +562,6 @@ __global__ __launch_bounds__(NTH, 3) void tile_kernel(TileArgs a, int method) {
                             y.x = fv[j].x - c0;
                             y.y = fv[j].y - c0;
                             v2[px2(vq + jj * kThreads)] = y;
-                            // middle sums: a fast tile ends >= REACH steps before T, so only
-                            // the series head (tile 0, positions < kAcfEdge) is excluded
-                            if (jj < FS && (t0 > 0 || tid + jj * kThreads >= kAcfEdge / 2)) {
-                                acc_s += y.x;
-                                acc_s += y.y;
-                                acc_q = __builtin_fma(y.x, y.x, acc_q);
-                                acc_q = __builtin_fma(y.y, y.y, acc_q);
-                            }
                         }
                     }
                 }
@@ -551,17 +593,6 @@ __global__ __launch_bounds__(NTH, 3) void tile_kernel(TileArgs a, int method) {
                     f.x = (q < qB) ? f.x - c0 : 0.0;
                     f.y = (q + 1 < qB) ? f.y - c0 : 0.0;
                     v2[px2(q2)] = f;
-                    if (q < qW) {
-                        const int64_t t = (int64_t)e0 + q;
-                        if (acf_mid(t, T)) {
-                            acc_s += f.x;
-                            acc_q = __builtin_fma(f.x, f.x, acc_q);
-                        }
-                        if (q + 1 < qW && acf_mid(t + 1, T)) {
-                            acc_s += f.y;
-                            acc_q = __builtin_fma(f.y, f.y, acc_q);
-                        }
-                    }
                 }
             }
             // shifted scheme, first tile: the pre-chunk (positions [0, 4t) of the series) reads
@@ -577,6 +608,16 @@ __global__ __launch_bounds__(NTH, 3) void tile_kernel(TileArgs a, int method) {
             STAMP(9);
             // ---- 6. lag products on MFMA ----
             constexpr int CPW = TW / 64 / kWaves;   // 64-step chunks per wave
+            // sum y / sum y^2 over the series' middle (sts_acf.hpp rule 2): lane l of the chunk
+            // at series position p holds y(p + l)
+            auto mid_sums = [&](int p, double y) {
+                const double z = acf_mid(p + lane, T) ? y : 0.0;
+                acc_s += z;
+                acc_q = __builtin_fma(z, z, acc_q);
+            };
+            // a tile wholly inside the middle takes the unrolled loop with plain sums; the
+            // series' first and last tiles take the per-chunk loop with the per-lane test
+            const bool tile_mid = t0 >= kAcfEdge && t1 + kAcfEdge <= T;
             const int tlen = t1 - t0;
             const int nch = (tlen + 63) / 64;
             int c = wave * CPW;
@@ -606,12 +647,13 @@ __global__ __launch_bounds__(NTH, 3) void tile_kernel(TileArgs a, int method) {
 #pragma unroll
                     for (int t = 0; t < NT; t++)
                         U[t % NA] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[t], bv[t], U[t % NA], 0, 0, 0);
+                    return av[0];   // y at chunk position lane
                 };
                 // wave 0 of the first tile also runs chunk -1 (the look-back, y = 0), whose
                 // shifted windows hold the series' first QS t steps
-                if (k == 0 && wave == 0) chunk_mfma(vals);
+                if (k == 0 && wave == 0) chunk_mfma(vals);   // y = 0 there: no middle-sum term
 #if STS_MFMA_UNROLL
-                if (cend - c == CPW) {
+                if (cend - c == CPW && tile_mid) {
                     // full chunk range, unrolled: per-lane LDS indices made opaque once per
                     // tile (else LICM hoists all 16 x 2NT of them out of the tile loop and
                     // spills), chunk offsets (72 doubles per padded chunk) fold into the
@@ -635,6 +677,8 @@ __global__ __launch_bounds__(NTH, 3) void tile_kernel(TileArgs a, int method) {
 #pragma unroll
                         for (int t = 0; t < NT; t++)
                             U[t % NA] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[t], bv[t], U[t % NA], 0, 0, 0);
+                        acc_s += av[0];   // middle sums: VALU under the MFMA pipe
+                        acc_q = __builtin_fma(av[0], av[0], acc_q);
                         __builtin_amdgcn_sched_barrier(0);   // one chunk's operands live at a time
                     }
                     c = cend;
@@ -669,7 +713,7 @@ __global__ __launch_bounds__(NTH, 3) void tile_kernel(TileArgs a, int method) {
                     }
                 }
 #else
-                for (; c < cend; c++) chunk_mfma(vals + px(qA + 64 * c));   // chunk start: a multiple of 32
+                for (; c < cend; c++) mid_sums(t0 + 64 * c, chunk_mfma(vals + px(qA + 64 * c)));   // chunk start: a multiple of 32
 #endif
             } else {
                 // U_t += y(j0 + l) x y(j0 + 16t + l)
@@ -681,6 +725,7 @@ __global__ __launch_bounds__(NTH, 3) void tile_kernel(TileArgs a, int method) {
                     const double av = (jrel < tlen) ? bv[0] : 0.0;   // A only inside the tile
 #pragma unroll
                     for (int t = 0; t < NT; t++) U[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv[t], U[t], 0, 0, 0);
+                    mid_sums(t0 + 64 * c, av);
                 }
             }
         }
@@ -758,7 +803,7 @@ __global__ __launch_bounds__(NTH, 3) void tile_kernel(TileArgs a, int method) {
                 }
                 part[kPartSum] = ts;
                 part[kPartSq] = tq;
-                part[kPartShift] = c0;
+                part[kPartShift] = sh_d[0];
             }
         }
     }

@@ -147,6 +147,85 @@ def test_fill_long_runs_and_edges(torch, method):
     assert_bits(host(out)[ok], ref[ok], method)
 
 
+def _gap_rows(T, gaps, seed):
+    rng = np.random.default_rng(seed)
+    rows = []
+    for a, b in gaps:
+        x = 1e4 + np.cumsum(rng.standard_normal(T) * 0.01)
+        x[rng.random(T) < 0.05] = NaN
+        x[0] = x[-1] = 1e4                                    # interior gaps only: linear fills them
+        x[a:b] = NaN
+        rows.append(x)
+    return np.array(rows)
+
+
+@pytest.mark.parametrize("method", ["linear", "previous", "next", "nearest"])
+def test_fill_long_gaps_bit_exact(torch, method):
+    # NaN runs around the chain-pass threshold (kLongRun = 32), across tile (4096) and
+    # workgroup (16 tiles) boundaries, starting / ending at tile edges, and longer than a
+    # workgroup: the chain pass (carried across tiles) and the cached global scans
+    from sparkts import _native
+    from sparkts import UnivariateTimeSeries as uts
+    T = 200_000
+    gaps = [(100, 133), (100, 134), (4063, 4097), (4096, 4096 + 33), (4000, 12300), (8192, 8192 + 4096),
+            (60000, 70000), (65536 - 7, 65536 + 40), (30000, 190000), (4096 * 5 - 1, 4096 * 21 + 1),
+            (2, T - 2), (17, 99)]
+    x = _gap_rows(T, gaps, 7)
+    ref, err = oracle.panel_fill(x, method, threads=4)
+    xd = dev(torch, x)
+    out = torch.empty_like(xd)
+    e = torch.zeros(x.shape[0], dtype=torch.int32, device="cuda:0")
+    assert _native.lib().sts_fill(xd.data_ptr(), out.data_ptr(), x.shape[0], T, T, T, uts.fill_method_code(method),
+                                  e.data_ptr(), None) == 0
+    torch.cuda.synchronize()
+    assert np.array_equal(host(e), err)
+    assert_bits(host(out), ref, method)
+    # the same through the fused fill + ACF path (tile kernel with MFMA) and the segment kernel
+    K = 60
+    filled, acf = __import__("sparkts").TimeSeriesRDD(None, None, xd).fillAndAutocorr(method, K)
+    assert_bits(host(filled.data), ref, method + " fused")
+    xs = _gap_rows(16000, [(40, 15950), (100, 133), (511, 545), (1000, 9000)], 8)
+    rs, es = oracle.panel_fill(xs, method)
+    assert_bits(host(uts.fillts(dev(torch, xs), method)), rs, method + " segment kernel")
+
+
+@pytest.mark.parametrize("T,gap", [(982_800, (200_000, 700_000)), (16_384, (30, 16_300))])
+def test_fill_linear_long_gap_is_linear_time(torch, T, gap):
+    # a G-step interior gap used to cost O(G^2) sequential adds (each NaN
+    # replayed its whole chain from L); the chain pass makes it O(G).  Bit-exact, and the
+    # gap panel must fill in about the time of a gap-free one.
+    from sparkts import _native
+    S = 4
+    x = _gap_rows(T, [gap] * S, 9)
+    xd = dev(torch, x)
+    out = torch.empty_like(xd)
+    acf = torch.empty((S, 60), dtype=torch.float64, device="cuda:0")
+    lib = _native.lib()
+
+    def run(src):
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        ev0.record()
+        assert lib.sts_fill_autocorr(src.data_ptr(), out.data_ptr(), S, T, T, T, 0, 60, acf.data_ptr(), None,
+                                     torch.cuda.current_stream().cuda_stream) == 0
+        ev1.record()
+        torch.cuda.synchronize()
+        return ev0.elapsed_time(ev1)
+
+    run(xd)
+    t_gap = min(run(xd) for _ in range(3))
+    ref, racf, _ = oracle.panel_fill_autocorr(x, "linear", 60, threads=4)
+    assert_bits(host(out), ref, "linear gap")
+    assert_rel(host(acf), racf, what="acf after a long gap")
+    base = dev(torch, _gap_rows(T, [(10, 11)] * S, 9))
+    run(base)
+    t_base = min(run(base) for _ in range(3))
+    print("T=%d gap=%d: %.3f ms with the gap, %.3f ms without" % (T, gap[1] - gap[0], t_gap, t_base))
+    # the floor is the reference's own serial chain (bit-exactness forbids reassociating the
+    # G additions): ~G dependent FP64 adds in the workgroup deepest in the gap.  The O(G^2)
+    # replay took on the order of a second for G = 500k.
+    assert t_gap < t_base + 50.0, (t_gap, t_base)
+
+
 def test_fill_nearest_raises(torch):
     from sparkts import UnivariateTimeSeries as uts
     from sparkts.errors import IllegalArgumentException
