@@ -52,14 +52,11 @@ __device__ __forceinline__ double median_of_lanes(double v, bool ok, int lane) {
     if (n == 0) return 0.0;
     int k = (n - 1) >> 1;                          // rank wanted among the candidates
     for (;;) {
-        // pivot lane: the (n / 2)-th set bit of cand (popcount bisection, scalar)
-        unsigned long long m = cand;
-        int want = n >> 1, pl = 0;
-#pragma unroll
-        for (int width = 32; width >= 1; width >>= 1) {
-            const int c = __popcll(m & ((1ull << width) - 1ull));
-            if (want >= c) { want -= c; m >>= width; pl += width; }
-        }
+        // pivot lane: the first candidate at or after the middle of the candidates' lane range
+        // (scalar; for a monotone sample that is its median)
+        const int lo = __ffsll((long long)cand) - 1, hi = 63 - __clzll(cand);
+        const int mid = (lo + hi) >> 1;
+        const int pl = mid + __ffsll((long long)(cand >> mid)) - 1;
         const double pv = acf_readlane(v, pl);
         const bool in = (cand >> lane) & 1ull;
         const unsigned long long lt = __ballot(in && (v < pv || (v == pv && lane < pl)));

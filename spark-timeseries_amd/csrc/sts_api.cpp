@@ -227,9 +227,17 @@ int run_tile(const double* in, double* out, double* lagmat, int64_t S, int64_t T
     if (err && !one_seg) HIP_TRY(hipMemsetAsync(err, 0, (size_t)S * sizeof(int32_t), st), "hipMemsetAsync(err)");
     Scratch part(st);
     if (K > 0 && !fuse) {
-        hipError_t e = part.alloc((size_t)(S * a.chunks_per_series) * sts::kPartStride * sizeof(double));
+        // chunk partials, then (tile kernel) the per-series shifts
+        const size_t np = (size_t)(S * a.chunks_per_series) * sts::kPartStride;
+        hipError_t e = part.alloc((np + (seg ? 0 : (size_t)S)) * sizeof(double));
         if (e != hipSuccess) return hip_fail(e, "hipMallocAsync(partials)");
         a.partials = static_cast<double*>(part.p);
+        if (!seg) {
+            double* sh = a.partials + np;
+            e = sts::launch_acf_shift(in, S, T, ld_in, sh, st);
+            if (e != hipSuccess) return hip_fail(e, "acf shift");
+            a.shift = sh;
+        }
     }
     prof_mark(st);
     hipError_t e = seg ? sts::launch_segment(method, a, st) : sts::launch_tile(method, tw, a, st);

@@ -37,6 +37,7 @@ struct TileArgs {
     int max_lag;          // lag matrix p
     int include_original; // lag matrix inc
     double* acf_fused;    // seg kernel, one segment per series: final ACF written directly (S x K)
+    const double* shift;  // tile kernel with K > 0: per-series ACF shift (launch_acf_shift)
     int err_all;          // seg kernel, one segment per series: err[s] written for every series
 };
 
@@ -60,6 +61,8 @@ inline const char* ab_knob(const char*) { return nullptr; }
 // launchers (return hipError_t of the launch)
 hipError_t launch_tile(int method, int tw, const TileArgs& a, hipStream_t st);
 hipError_t launch_acf_finalize(const FinalizeArgs& a, hipStream_t st);
+// per-series robust ACF shift (sts_acf.hpp) for the tile kernel
+hipError_t launch_acf_shift(const double* in, int64_t S, int64_t T, int64_t ld, double* shift, hipStream_t st);
 
 // Wave-private segment kernel (sts_seg.hip): tiles of kSegW steps, kSegTiles tiles per
 // wave.  TileArgs.tiles_per_series = ceil(T / kSegW), tiles_per_chunk = tiles per

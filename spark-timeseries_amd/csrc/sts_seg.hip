@@ -44,6 +44,8 @@
 
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 namespace sts {
 namespace {
 
@@ -57,8 +59,6 @@ constexpr int kRing = 2 * kW + 128;   // two slots + a mirror of slot 0's head
 constexpr int kWaves = 4;             // waves per workgroup (independent)
 constexpr int kBig = 0x7fffffff;
 
-constexpr int kMaxRuns = kW / (kLongRun + 2) + 2;   // runs with chain-pass steps in one tile
-
 struct WaveLds {
     double ring[kRing];
     unsigned long long m2[2][kWords]; // validity masks of the tiles in ring slots 0 / 1
@@ -66,11 +66,8 @@ struct WaveLds {
     int lastUp[kWords];               // last valid global index in words <= w (carry: < tile)
     int firstFrom[kWords];            // first valid global index in words >= w (look-ahead)
     int wbase[kWords + 1];            // exclusive prefix count of need bits
-    // linear fill, chain pass (as in sts_tile.hip): runs with steps more than kLongRun past
-    // L, and the chain value at the last step of the previous tile (by tile parity)
-    int nlong;
-    int run_q[kMaxRuns], run_L[kMaxRuns], run_N[kMaxRuns];
-    double run_Lv[kMaxRuns], run_Nv[kMaxRuns];
+    // linear fill, long runs (as in sts_tile.hip): the chain value at the last step of the
+    // previous tile (by tile parity)
     int carry_L[2], carry_t[2];
     double carry_r[2];
     int cN_pos, cN;                   // cache of the global look-ahead scan: first valid >= cN_pos is cN
@@ -217,42 +214,6 @@ __device__ __forceinline__ int masks_to_lds(const v2d (&R)[4], unsigned long lon
     return f;
 }
 
-// Linear fill, chain pass: one lane per long run walks r = r + inc through the run's steps in
-// tile [kb, tend), starting from the previous tile's carried value when the run continues from
-// it, else replaying from L.
-__device__ __forceinline__ void chain_pass(WaveLds& w, double* ring, int kb, int tend, int lane) {
-    const int nl = __builtin_amdgcn_readfirstlane(w.nlong);
-    const int rd = ((kb / kW) + 1) & 1, wr = (kb / kW) & 1;
-    for (int r = lane; r < nl; r += 64) {
-        const int q0 = w.run_q[r], L = w.run_L[r], N = w.run_N[r];
-        const double Lv = w.run_Lv[r];
-        const double inc = (w.run_Nv[r] - Lv) / (double)(N - L);
-        const int tstart = kb + q0;
-        double v;
-        if (w.carry_L[rd] == L && w.carry_t[rd] == tstart - 1) {
-            v = w.carry_r[rd];
-        } else {
-            v = Lv;
-            int j = tstart - 1 - L;   // replay from L, 8 dependent adds per trip
-            for (; j >= 8; j -= 8) {
-                v = v + inc; v = v + inc; v = v + inc; v = v + inc;
-                v = v + inc; v = v + inc; v = v + inc; v = v + inc;
-            }
-            for (; j > 0; j--) v = v + inc;
-        }
-        for (int q = q0; kb + q < tend && kb + q < N; q++) {
-            v = v + inc;
-            ring[q] = v;
-            if (q == kW - 1) {
-                w.carry_L[wr] = L;
-                w.carry_t[wr] = kb + kW - 1;
-                w.carry_r[wr] = v;
-            }
-        }
-    }
-    wave_sync();
-}
-
 // Impute tile k (ring slot SLOT, raw; masks in w.m2[SLOT]) and turn it into y; optionally
 // store it.  look: first valid index >= kb + kW when known (kBig: unknown, then scan
 // global memory from scan_from); lookv its value.
@@ -268,10 +229,17 @@ __device__ __forceinline__ void impute_tile(WaveLds& w, const double* src, doubl
         // ---- word tables (wave-uniform scalars, short-lived) ----
         int wb[kWords + 1];
         int run = st.Lc, lastneed = -1;
+        bool lg = false;   // linear: can a step lie more than kLongRun past its last valid index?
         wb[0] = 0;
 #pragma unroll
         for (int i = 0; i < kWords; i++) {
             const unsigned long long m = uni64(w.m2[SLOT][i]);
+            if (method == STS_FILL_LINEAR) {   // (conservative, as in sts_tile.hip: a long run
+                // puts > kLongRun / 2 NaNs into one word, or reaches into the tile's first word
+                // from more than kLongRun before it)
+                const int tz = m ? __ffsll(m) - 1 : 64;
+                lg = lg || __popcll(~m) > kLongRun / 2 || (i == 0 && tz > 0 && kb + tz - 1 - run > kLongRun);
+            }
             if (m) run = kb + 64 * i + 63 - __clzll(m);
             const int hi = tend - (kb + 64 * i);               // real steps of word i: bits [0, hi)
             unsigned long long r = 0ull;
@@ -317,12 +285,14 @@ __device__ __forceinline__ void impute_tile(WaveLds& w, const double* src, doubl
                     if (lane == 0) w.firstFrom[i] = ff;
                 }
             }
-            if (lane == 0) w.nlong = 0;
             wave_sync();
             // ---- impute the compacted NaN positions; F goes into the ring in place
             //      (every (L, N) source is a valid position, never rewritten) ----
             const int Lc = st.Lc;
             const double Lcv = st.Lv;
+            // two versions of the loop: only a flagged tile carries the long-run chain code
+            auto impute = [&](auto long_tag) {
+            constexpr bool LONG = decltype(long_tag)::value;
             for (int idx = lane; idx < nnan; idx += 64) {
                 int wd = 0;
 #pragma unroll
@@ -366,14 +336,35 @@ __device__ __forceinline__ void impute_tile(WaveLds& w, const double* src, doubl
                 }
                 case STS_FILL_LINEAR: {
                     if (Lt < 0 || Nt >= T) break;             // runs touching index 0 or n-1 stay NaN
-                    if (t - Lt > kLongRun) {                  // the chain pass produces this step
+                    if (LONG && t - Lt > kLongRun) {
+                        // a step more than kLongRun past L: the lane holding the run's first
+                        // such step in this tile walks the chain through all of them (O(run)),
+                        // from the previous tile's carried value when the run continues from
+                        // it, else replaying from L; the other lanes skip theirs
                         if (t - Lt == kLongRun + 1 || q == 0) {
-                            const int rr = atomicAdd(&w.nlong, 1);
-                            w.run_q[rr] = q;
-                            w.run_L[rr] = Lt;
-                            w.run_N[rr] = Nt;
-                            w.run_Lv[rr] = Lv;
-                            w.run_Nv[rr] = Nv;
+                            const double inc = (Nv - Lv) / (double)(Nt - Lt);
+                            const int rd = ((kb / kW) + 1) & 1, wr = (kb / kW) & 1;
+                            double v;
+                            if (w.carry_L[rd] == Lt && w.carry_t[rd] == t - 1) {
+                                v = w.carry_r[rd];
+                            } else {
+                                v = Lv;
+                                int j = t - 1 - Lt;   // replay from L, 8 dependent adds per trip
+                                for (; j >= 8; j -= 8) {
+                                    v = v + inc; v = v + inc; v = v + inc; v = v + inc;
+                                    v = v + inc; v = v + inc; v = v + inc; v = v + inc;
+                                }
+                                for (; j > 0; j--) v = v + inc;
+                            }
+                            for (int qq = q; kb + qq < tend && kb + qq < Nt; qq++) {
+                                v = v + inc;
+                                ring[qq] = v;
+                                if (qq == kW - 1) {
+                                    w.carry_L[wr] = Lt;
+                                    w.carry_t[wr] = kb + kW - 1;
+                                    w.carry_r[wr] = v;
+                                }
+                            }
                         }
                         continue;
                     }
@@ -388,11 +379,11 @@ __device__ __forceinline__ void impute_tile(WaveLds& w, const double* src, doubl
                 }
                 ring[q] = r;
             }
+            };
+            if (lg) impute(std::true_type{});
+            else impute(std::false_type{});
         }
         wave_sync();
-        // ---- linear fill, chain pass (rare: a run with steps more than kLongRun past L) ----
-        if (method == STS_FILL_LINEAR && nnan > 0 && __builtin_amdgcn_readfirstlane(w.nlong) > 0)
-            chain_pass(w, ring, kb, tend, lane);
         if (lastv >= 0) {
             st.Lc = lastv;
             st.Lv = ring[lastv - kb];
@@ -423,7 +414,9 @@ __device__ __forceinline__ void impute_tile(WaveLds& w, const double* src, doubl
             y.y = (full || t + 1 < T) ? f.y - st.c0 : 0.0;
             r2[64 * u] = y;
             if (own) {   // sum y / sum y^2 over the series' middle (sts_acf.hpp rule 2)
-                const double zx = acf_mid(t, T) ? y.x : 0.0, zy = acf_mid(t + 1, T) ? y.y : 0.0;
+                const bool mid_tile = kb >= kAcfEdge && kb + kW + kAcfEdge <= T;   // wave-uniform
+                const double zx = (mid_tile || acf_mid(t, T)) ? y.x : 0.0;
+                const double zy = (mid_tile || acf_mid(t + 1, T)) ? y.y : 0.0;
                 st.sm += zx;
                 st.sm += zy;
                 st.qm = __builtin_fma(zx, zx, st.qm);

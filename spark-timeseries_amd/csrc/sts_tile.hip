@@ -17,9 +17,9 @@
 // whose reference loop accumulates r[j] = r[j-1] + inc SEQUENTIALLY from the run
 // start: each NaN step replays that chain from L (t - L adds), which reproduces the
 // reference bit for bit (no FMA: the library is built with -ffp-contract=off).  Steps more
-// than kLongRun past L are instead produced by a per-run CHAIN pass (one lane walks the run
-// once, carrying its value across the workgroup's tiles), so a gap of G steps costs O(G),
-// not O(G^2).  Runs longer than the halos find L / N with a 512-step-wide scan of global
+// than kLongRun past L are instead produced by one lane walking the run's chain once,
+// carrying its value across the workgroup's tiles), so a gap of G steps costs O(G), not
+// O(G^2).  Runs longer than the halos find L / N with a 512-step-wide scan of global
 // memory whose answer is cached for the workgroup's next tiles.
 //
 // Autocorrelation: with y = F - c (c = the robust shift of sts_acf.hpp: the median of 64
@@ -36,6 +36,8 @@
 #include "sts_scan.hpp"
 
 #include <hip/hip_runtime.h>
+
+#include <type_traits>
 
 #ifndef STS_MFMA_PIPE
 #define STS_MFMA_PIPE 0   // experiment knob: software-pipelined MFMA operand loads
@@ -110,6 +112,51 @@ __device__ __forceinline__ unsigned long long interleave2(unsigned ev, unsigned 
     return (bitrep(ev) & 0x5555555555555555ull) | (bitrep(od) & 0xAAAAAAAAAAAAAAAAull);
 }
 
+// Wave-wide scans of one int per lane for wave 0's word scan: DPP within rows of 16 lanes
+// (row_shr / row_shl 1, 2, 4, 8; lanes without a source keep the identity) and readlane
+// carries across the four rows -- VALU-latency steps instead of one ds_bpermute round trip
+// per step.  dpp controls: row_shl:n = 0x100 + n, row_shr:n = 0x110 + n, wave_shl:1 = 0x130,
+// wave_shr:1 = 0x138.
+template <int CTRL>
+__device__ __forceinline__ int dpp(int old, int v) {
+    return __builtin_amdgcn_update_dpp(old, v, CTRL, 0xf, 0xf, false);
+}
+__device__ __forceinline__ int rl(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
+__device__ __forceinline__ int imax(int a, int b) { return a > b ? a : b; }
+__device__ __forceinline__ int imin(int a, int b) { return a < b ? a : b; }
+// inclusive prefix max over lanes 0..lane
+__device__ __forceinline__ int wave_prefix_max(int v, int lane) {
+    constexpr int I = -0x7fffffff - 1;
+    v = imax(v, dpp<0x111>(I, v));
+    v = imax(v, dpp<0x112>(I, v));
+    v = imax(v, dpp<0x114>(I, v));
+    v = imax(v, dpp<0x118>(I, v));
+    const int p1 = rl(v, 15), p2 = imax(p1, rl(v, 31)), p3 = imax(p2, rl(v, 47));
+    const int r = lane >> 4;
+    return imax(v, r == 0 ? I : r == 1 ? p1 : r == 2 ? p2 : p3);
+}
+// inclusive prefix sum over lanes 0..lane
+__device__ __forceinline__ int wave_prefix_sum(int v, int lane) {
+    v += dpp<0x111>(0, v);
+    v += dpp<0x112>(0, v);
+    v += dpp<0x114>(0, v);
+    v += dpp<0x118>(0, v);
+    const int p1 = rl(v, 15), p2 = p1 + rl(v, 31), p3 = p2 + rl(v, 47);
+    const int r = lane >> 4;
+    return v + (r == 0 ? 0 : r == 1 ? p1 : r == 2 ? p2 : p3);
+}
+// inclusive suffix min over lanes lane..63
+__device__ __forceinline__ int wave_suffix_min(int v, int lane) {
+    constexpr int I = 0x7fffffff;
+    v = imin(v, dpp<0x101>(I, v));
+    v = imin(v, dpp<0x102>(I, v));
+    v = imin(v, dpp<0x104>(I, v));
+    v = imin(v, dpp<0x108>(I, v));
+    const int s3 = rl(v, 48), s2 = imin(s3, rl(v, 32)), s1 = imin(s2, rl(v, 16));
+    const int r = lane >> 4;
+    return imin(v, r == 0 ? s1 : r == 1 ? s2 : r == 2 ? s3 : I);
+}
+
 // Padded LDS index of extended-tile position q: 4 doubles of padding per 32.  Keeps the
 // lag-product B-operand gathers (16-step-spaced groups, see below) conflict-free across the
 // 64 LDS banks; 16-B pairs (even q) never straddle a pad.
@@ -149,14 +196,10 @@ __global__ __launch_bounds__(NTH, 3) void tile_kernel(TileArgs a, int method) {
     __shared__ int firstFrom[NW];          // first valid E-position in words >= w (kBig: none)
     __shared__ int wbase[NW + 1];          // NaN-list offset of each word (exclusive prefix count)
     __shared__ unsigned long long wneed[NW];   // NaN positions to impute, per word
-    __shared__ int sh_i[4];                // lext, next (series positions), NaN count, long runs
-    __shared__ double sh_d[3];             // c0, value at lext, value at next
-    // linear fill, chain pass: runs with steps more than kLongRun past L (registered by their
-    // first such step in the tile), and the chain value at the last step of the previous
-    // tile (double-buffered by tile parity: read [(k + 1) & 1], write [k & 1])
-    constexpr int kMaxRuns = EW / (kLongRun + 2) + 2;
-    __shared__ int run_q[kMaxRuns], run_L[kMaxRuns], run_N[kMaxRuns];
-    __shared__ double run_Lv[kMaxRuns], run_Nv[kMaxRuns];
+    __shared__ int sh_i[4];                // lext, next (series positions), NaN count, long-run flag
+    __shared__ double sh_d[3];             // (unused), value at lext, value at next
+    // linear fill, long runs: the chain value at the last step of the previous tile
+    // (double-buffered by tile parity: read [(k + 1) & 1], write [k & 1])
     __shared__ int carry_L[2], carry_t[2];
     __shared__ double carry_r[2];
     // wave 0's caches of the global scans (series positions; LDS, not registers: nothing is
@@ -239,13 +282,9 @@ __global__ __launch_bounds__(NTH, 3) void tile_kernel(TileArgs a, int method) {
     bool have = interior(k_begin);
     if (have) STS_ISSUE(k_begin);
     else STS_CLEAR();
-    // ACF shift (sts_acf.hpp: median of 64 raw samples; identical in every workgroup of the
-    // series): wave 0 computes it while its first tile's loads are in flight and leaves it in
-    // sh_d[0]; every wave reads it after the tile loop's first barrier (no extra barrier)
-    if (NT > 0 && wave == 0) {
-        const double c = robust_shift(src, T, lane);
-        if (lane == 0) sh_d[0] = c;
-    }
+    // ACF shift (sts_acf.hpp: median of 64 raw samples of the series), computed once per
+    // series by acf_shift_kernel before this launch: a scalar load
+    const double c0 = (NT > 0) ? a.shift[s] : 0.0;
     for (int64_t k = k_begin; k < k_end; k++) {
         const int t0 = (int)(k * TW);
         const int t1 = (t0 + TW < T) ? t0 + TW : (int)T;
@@ -329,25 +368,24 @@ __global__ __launch_bounds__(NTH, 3) void tile_kernel(TileArgs a, int method) {
             };
             const unsigned long long n0 = (w0 < NW) ? need(w0, m0) : 0ull;
             const unsigned long long n1 = (w1 < NW) ? need(w1, m1) : 0ull;
-            int pm = l1 > l0 ? l1 : l0;                           // inclusive prefix max
-            int sm = f0 < f1 ? f0 : f1;                           // inclusive suffix min
-            int pc = __popcll(n0) + __popcll(n1);                 // inclusive prefix count
-#pragma unroll
-            for (int d = 1; d < 64; d <<= 1) {
-                const int o = __shfl_up(pm, d);
-                const int c = __shfl_up(pc, d);
-                const int u = __shfl_down(sm, d);
-                if (lane >= d) { pm = o > pm ? o : pm; pc += c; }
-                if (lane + d < 64) sm = u < sm ? u : sm;
-            }
-            int ex = __shfl_up(pm, 1);
-            int exc = __shfl_up(pc, 1);
-            int exs = __shfl_down(sm, 1);
-            if (lane == 0) { ex = -1; exc = 0; }
-            if (lane == 63) exs = kBig;
-            const int nnan = __shfl(pc, 63);
-            const int firstValidE = __shfl(sm, 0);
-            const int lastValidE = __shfl(pm, 63);
+            const int pm = wave_prefix_max(l1 > l0 ? l1 : l0, lane);           // inclusive prefix max
+            const int sm = wave_suffix_min(f0 < f1 ? f0 : f1, lane);           // inclusive suffix min
+            const int pc = wave_prefix_sum(__popcll(n0) + __popcll(n1), lane); // inclusive prefix count
+            const int ex = dpp<0x138>(-1, pm);       // exclusive: lane - 1's value (wave_shr:1)
+            const int exc = dpp<0x138>(0, pc);
+            const int exs = dpp<0x130>(kBig, sm);    // lane + 1's value (wave_shl:1)
+            const int nnan = rl(pc, 63);
+            const int firstValidE = rl(sm, 0);
+            const int lastValidE = rl(pm, 63);
+            // linear fill: can a step of this tile lie more than kLongRun past its last valid
+            // index?  Such a step ends a run of > kLongRun NaNs, which puts more than half of
+            // that many NaNs into one word of the extended tile (a run reaching in from before
+            // the tile fills the whole look-back word).  Conservative: a false alarm only
+            // selects the loop that carries the long-run code, and the per-step replay is exact
+            // for any run length.
+            const bool lg = method == STS_FILL_LINEAR &&
+                            __ballot((w0 < NW && __popcll(~m0) > kLongRun / 2) ||
+                                     (w1 < NW && __popcll(~m1) > kLongRun / 2)) != 0ull;
             if (w0 < NW) {
                 lastUpTo[w0] = ex > l0 ? ex : l0;
                 const int a0 = f1 < exs ? f1 : exs;
@@ -379,7 +417,7 @@ __global__ __launch_bounds__(NTH, 3) void tile_kernel(TileArgs a, int method) {
             // the last valid index before the next tile's e0 = e0 + TW: in this tile's words
             // [0, TW / 64) (lane TW / 128 - 1's inclusive prefix max), else lext
             if (needL) {
-                const int lq = __shfl(pm, TW / 128 - 1);
+                const int lq = rl(pm, TW / 128 - 1);
                 if (lane == 0) {
                     sh_c[0] = e0 + TW;
                     sh_c[1] = (lq >= 0) ? e0 + lq : lext;
@@ -390,7 +428,7 @@ __global__ __launch_bounds__(NTH, 3) void tile_kernel(TileArgs a, int method) {
                 sh_i[0] = lext;
                 sh_i[1] = next;
                 sh_i[2] = nnan;
-                sh_i[3] = 0;
+                sh_i[3] = lg ? 1 : 0;
                 sh_d[1] = (lext >= 0) ? src[lext] : 0.0;
                 sh_d[2] = (next < T) ? src[next] : 0.0;
             }
@@ -405,6 +443,10 @@ __global__ __launch_bounds__(NTH, 3) void tile_kernel(TileArgs a, int method) {
             const int nnan = sh_i[2];
             const int lext = sh_i[0], next = sh_i[1];
             const double lextv = sh_d[1], nextv = sh_d[2];
+            // two versions of the loop: only a tile flagged by the word scan carries the
+            // long-run chain code
+            auto impute = [&](auto long_tag) {
+            constexpr bool LONG = decltype(long_tag)::value;
             for (int idx = tid; idx < nnan; idx += kThreads) {
                 // the word holding NaN #idx: last w with wbase[w] <= idx (binary search) ...
                 int lo = 0, hi = NW;
@@ -456,14 +498,37 @@ __global__ __launch_bounds__(NTH, 3) void tile_kernel(TileArgs a, int method) {
                 }
                 case STS_FILL_LINEAR: {
                     if (Lt < 0 || Nt >= T) break;             // runs touching index 0 or n-1 stay NaN
-                    if (t - Lt > kLongRun) {                  // the chain pass produces this step
+                    if (LONG && t - Lt > kLongRun) {
+                        // a step more than kLongRun past L: the lane holding the run's first
+                        // such step in this tile walks the chain r = r + inc through all of
+                        // them (O(run), not O(run^2)), starting from the previous tile's
+                        // carried value when the run continues from it, else replaying from L;
+                        // the other lanes skip theirs
                         if (t - Lt == kLongRun + 1 || q == qA) {
-                            const int r = atomicAdd(&sh_i[3], 1);
-                            run_q[r] = q;
-                            run_L[r] = Lt;
-                            run_N[r] = Nt;
-                            run_Lv[r] = Lv;
-                            run_Nv[r] = Nv;
+                            const double inc = (Nv - Lv) / (double)(Nt - Lt);
+                            const int rd = (int)((k + 1) & 1), wr = (int)(k & 1);
+                            double v;
+                            if (carry_L[rd] == Lt && carry_t[rd] == t - 1) {
+                                v = carry_r[rd];
+                            } else {
+                                v = Lv;
+                                int j = t - 1 - Lt;   // replay from L, 8 dependent adds per trip
+                                for (; j >= 8; j -= 8) {
+                                    v = v + inc; v = v + inc; v = v + inc; v = v + inc;
+                                    v = v + inc; v = v + inc; v = v + inc; v = v + inc;
+                                }
+                                for (; j > 0; j--) v = v + inc;
+                            }
+                            const int qend = (Nt - e0 < qB) ? Nt - e0 : qB;
+                            for (int qq = q; qq < qend; qq++) {
+                                v = v + inc;
+                                vals[px(qq)] = v;
+                                if (e0 + qq == t1 - 1) {
+                                    carry_L[wr] = Lt;
+                                    carry_t[wr] = t1 - 1;
+                                    carry_r[wr] = v;
+                                }
+                            }
                         }
                         continue;
                     }
@@ -478,50 +543,17 @@ __global__ __launch_bounds__(NTH, 3) void tile_kernel(TileArgs a, int method) {
                 }
                 vals[px(q)] = f;
             }
+        };
+            if (sh_i[3]) impute(std::true_type{});
+            else impute(std::false_type{});
         }
         STAMP(6);
         lds_barrier();
-        // ---- 4b. linear fill, chain pass: one lane per long run walks r = r + inc through
-        //      the run's steps in [qA, qB), starting from the previous tile's carried value when
-        //      the run continues from it, else replaying from L ----
-        if (method == STS_FILL_LINEAR && sh_i[3] > 0) {
-            const int nl = sh_i[3];
-            const int rd = (int)((k + 1) & 1), wr = (int)(k & 1);
-            for (int r = tid; r < nl; r += kThreads) {
-                const int q0 = run_q[r], L = run_L[r], N = run_N[r];
-                const double Lv = run_Lv[r];
-                const double inc = (run_Nv[r] - Lv) / (double)(N - L);
-                const int tstart = e0 + q0;
-                double v;
-                if (carry_L[rd] == L && carry_t[rd] == tstart - 1) {
-                    v = carry_r[rd];
-                } else {
-                    v = Lv;
-                    int j = tstart - 1 - L;   // replay from L, 8 dependent adds per trip
-                    for (; j >= 8; j -= 8) {
-                        v = v + inc; v = v + inc; v = v + inc; v = v + inc;
-                        v = v + inc; v = v + inc; v = v + inc; v = v + inc;
-                    }
-                    for (; j > 0; j--) v = v + inc;
-                }
-                for (int q = q0; q < qB && e0 + q < N; q++) {
-                    v = v + inc;
-                    vals[px(q)] = v;
-                    if (e0 + q == t1 - 1) {
-                        carry_L[wr] = L;
-                        carry_t[wr] = t1 - 1;
-                        carry_r[wr] = v;
-                    }
-                }
-            }
-            lds_barrier();
-        }
         STAMP(7);
 
         // ---- 5. filled output + lag matrix (16-B stores), then y = F - F(0) in place
         //      (0 past the series end) for the MFMA phase; start the next tile's loads ----
         {
-            const double c0 = sh_d[0];
             const bool al = dst && ((reinterpret_cast<uintptr_t>(dst) & 15) == 0);
             double2* v2 = reinterpret_cast<double2*>(vals);
             const int qBfull = (NT > 0) ? ((SHIFTED || qW + 64 + 16 * NT >= EW) ? EW : qW + 64 + 16 * NT) : 0;
@@ -803,7 +835,7 @@ __global__ __launch_bounds__(NTH, 3) void tile_kernel(TileArgs a, int method) {
                 }
                 part[kPartSum] = ts;
                 part[kPartSq] = tq;
-                part[kPartShift] = sh_d[0];
+                part[kPartShift] = c0;
             }
         }
     }
@@ -856,7 +888,26 @@ __global__ __launch_bounds__(256) void acf_finalize_kernel(FinalizeArgs a) {
     a.acf[s * K + lane] = out;
 }
 
+// One wave per series: the robust ACF shift (sts_acf.hpp) of every series, once per call,
+// for the tile kernel's workgroups to load (instead of each of a series' ~15 workgroups
+// sampling and ranking it again).
+__global__ __launch_bounds__(256) void acf_shift_kernel(const double* in, int64_t S, int64_t T, int64_t ld,
+                                                        double* shift) {
+    const int lane = threadIdx.x & 63;
+    const int64_t s = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (s >= S) return;
+    const double c = robust_shift(in + s * ld, T, lane);
+    if (lane == 0) shift[s] = c;
+}
+
 }  // namespace
+
+hipError_t launch_acf_shift(const double* in, int64_t S, int64_t T, int64_t ld, double* shift, hipStream_t st) {
+    if (S <= 0 || T <= 0) return hipSuccess;
+    dim3 grid((unsigned)((S + 3) / 4)), block(256);
+    hipLaunchKernelGGL(acf_shift_kernel, grid, block, 0, st, in, S, T, ld, shift);
+    return hipGetLastError();
+}
 
 hipError_t launch_tile(int method, int tw, const TileArgs& a, hipStream_t st) {
     const int64_t nchunk = a.S * a.chunks_per_series;

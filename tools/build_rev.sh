@@ -3,12 +3,12 @@
 #   tools/build_rev.sh REV NAME -> spark-timeseries_amd/build/var_NAME/libsts_hip.so
 set -e
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
-REV=$1; NAME=$2
+REV=$1; NAME=$2; XFLAGS=$3
 W=/tmp/rev_$NAME; rm -rf $W; mkdir -p $W
 git -C $ROOT archive $REV spark-timeseries_amd/csrc include | tar -x -C $W
 cd $W/spark-timeseries_amd/csrc
 for f in *.hip *.cpp; do
-  /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off -I$W/include -I. -c $f -o $W/$f.o &
+  /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off $XFLAGS -I$W/include -I. -c $f -o $W/$f.o &
 done
 wait
 mkdir -p $ROOT/spark-timeseries_amd/build/var_$NAME
