@@ -35,6 +35,10 @@ WORKLOADS = {
     "c2": (1_000_000, 390, 0.05, 2,
            "C2: fillPrevious -> differencesAtLag(1) -> EWMA(0.2).add, 1,000,000 series x 390 steps"),
     "c4": (500_000, 2_520, 0.0, 4, "C4: AR(5) fit + removeTimeDependentEffects, 500,000 series x 2,520 steps"),
+    "stage_c2": (1_000_000, 390, 0.05, 2,
+                 "C2 (fillPrevious -> differencesAtLag(1) -> EWMA(0.2).add, 1,000,000 series x 390 steps) from "
+                 "HOST-resident panels through the _host entry points' pinned staging pipeline; value = the "
+                 "HBM-resident rate, the host-resident rates are in 'staging'"),
     "ewma_fit": (1_000_000, 390, 0.0, 6,
                  "EWMA.fitModel (SURVEY.md 8(f) rank 1): commons-math3 NLCG + bracket + Brent per series, "
                  "1,000,000 series x 390 steps (the C2 shape)"),
@@ -102,6 +106,8 @@ def main():
     out = torch.empty_like(x)
     acf = torch.empty((S, K), dtype=torch.float64, device=dev)
     err = torch.zeros(S, dtype=torch.int32, device=dev)
+    if args.workload in ("stage_c2",):
+        pass
     if args.workload == "c4":
         cgen = torch.empty(S, dtype=torch.float64, device=dev)
         pgen = torch.empty((S, p_ar), dtype=torch.float64, device=dev)
@@ -144,7 +150,7 @@ def main():
                                                    err.data_ptr(), sp), "fill_autocorr")
             if world > 1:
                 all_gather_results(acf)
-        elif args.workload == "c2":
+        elif args.workload in ("c2", "stage_c2"):
             raise_for_status(lib.sts_fill_diff_ewma(x.data_ptr(), out.data_ptr(), S, T, T, T, 3, 1, smooth.data_ptr(),
                                                     err.data_ptr(), sp), "fill_diff_ewma")
         elif args.workload == "c5":
@@ -235,6 +241,7 @@ def main():
               "c1": "sts::seg_kernel<2> (wave-private series segments: fill linear + ACF partials, FP64 MFMA)",
               "c5": "sts::tile_kernel<4096,0> (fill nearest + lag-matrix columns)",
               "c2": "sts::recur_kernel<kFillDiffEwma> (fillPrevious -> differencesAtLag(1) -> EWMA add, lane per series)",
+              "stage_c2": "sts::recur_kernel<kFillDiffEwma> (fillPrevious -> differencesAtLag(1) -> EWMA add, lane per series)",
               "c4": "sts::ar_fit_blk_kernel<5,40> (AR(5): lane-blocked register lag products, lane-parallel Gram / Cholesky + refinement, fused remove)",
               "stats": "sts::stats_kernel<64,32> (StatCounter.merge per lane, LDS-staged series block)",
               "nan_instants": "sts::nan_instants_kernel + sts::gather_instants_kernel",
@@ -245,6 +252,7 @@ def main():
                            "sts::garch_tail_kernel<64> (wave per series past 64 passes)",
               "ewma_fit": "sts::ewma_fit_kernel<32,64> (lane-per-series commons-math3 optimizer; one sse+gradient "
                           "pass over the wave's series block per optimizer request)"}[args.workload]
+    staging = staging_leg(args, lib, x, out, smooth, S, T) if args.workload == "stage_c2" and rank == 0 else None
     roofline = None
     if launches[0] > 0:
         avg_ms = kern_ms[0] / launches[0]
@@ -257,7 +265,7 @@ def main():
                     "kernel_launches_timed": int(launches[0])}
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:   # the CPU leg is an N = 1 report
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.workload != "stage_c2":   # the CPU leg is an N = 1 report
         cpu = cpu_baseline(args, S, T, K, seed, nan_p, out, acf, p_ar, smooth,
                            gpar if args.workload == "garch_fit" else None)
 
@@ -270,16 +278,76 @@ def main():
             "data": "synthetic: Philox4x32-10 counter-based panel generated in HBM (SURVEY.md 8(d)), %g NaN" % nan_p,
             "config": {"workload": desc, "series_per_gpu": S, "steps_per_series": T,
                        "numLags": K if args.workload in ("c3", "c1") else None,
-                       "fill": {"c3": "linear", "c1": "linear", "c2": "previous", "c4": None, "c5": "nearest",
+                       "fill": {"c3": "linear", "c1": "linear", "c2": "previous", "stage_c2": "previous", "c4": None,
+                                "c5": "nearest",
                                 "ewma_fit": None, "garch_fit": None, "stats": None, "nan_instants": None,
                                 "to_instants": None, "wire_decode": None}[args.workload],
                        "parallelism": "dp%d (series sharded by key, one process per GPU)" % world},
             "roofline": roofline,
             "cpu_baseline": cpu,
         }
+        if staging is not None:
+            line["staging"] = staging
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def staging_leg(args, lib, x, out, smooth, S, T):
+    """Host-resident C2 through sts_fill_diff_ewma_host (csrc/sts_host.cpp): the panel and the
+    result live in host memory -- pageable numpy arrays, and pinned buffers from
+    sts_host_alloc -- and every call stages them through HBM in ~64 MB chunks on three
+    overlapped streams.  Reports the end-to-end series-elements/s (wall time of the whole
+    host-to-host call) and the PCIe transfer rates of the staging streams."""
+    import ctypes
+    import numpy as np
+    import torch
+    from sparkts.errors import raise_for_status
+    torch.cuda.synchronize()
+    host_x = x.cpu().numpy()
+    want = out.cpu().numpy().view(np.uint64)      # the HBM-resident path's result
+    sm = smooth.cpu().numpy()
+    n = S * T * 8
+    res = {}
+    for kind in ("pageable", "pinned"):
+        if kind == "pageable":
+            hin, hout, keep = host_x, np.empty_like(host_x), None
+        else:
+            pin, pout = ctypes.c_void_p(), ctypes.c_void_p()
+            raise_for_status(lib.sts_host_alloc(n, ctypes.byref(pin)), "sts_host_alloc")
+            raise_for_status(lib.sts_host_alloc(n, ctypes.byref(pout)), "sts_host_alloc")
+            hin = np.frombuffer((ctypes.c_char * n).from_address(pin.value), dtype=np.float64).reshape(S, T)
+            hout = np.frombuffer((ctypes.c_char * n).from_address(pout.value), dtype=np.float64).reshape(S, T)
+            hin[:] = host_x
+            keep = (pin, pout)
+        stats = np.zeros(8)
+        walls = []
+        for it in range(1 + max(1, min(args.steps, 3))):   # first call warms the staging buffers
+            t0 = time.perf_counter()
+            raise_for_status(lib.sts_fill_diff_ewma_host(hin.ctypes.data, hout.ctypes.data, S, T, T, 3, 1,
+                                                         sm.ctypes.data, None), "fill_diff_ewma_host")
+            if it:
+                walls.append(time.perf_counter() - t0)
+                lib.sts_staging_stats(stats.ctypes.data)
+        wall = min(walls)
+        wall_ms, h2d_ms, k_ms, d2h_ms, b_in, b_out, chunks, direct = stats
+        res[kind] = {"series_elements_per_s": S * T / wall, "wall_ms": round(wall * 1e3, 2),
+                     "h2d_GBps": round(b_in / (h2d_ms * 1e-3) / 1e9, 2) if h2d_ms > 0 else None,
+                     "d2h_GBps": round(b_out / (d2h_ms * 1e-3) / 1e9, 2) if d2h_ms > 0 else None,
+                     "pcie_both_ways_GBps": round((b_in + b_out) / wall / 1e9, 2),
+                     "kernel_ms_sum": round(k_ms, 2), "chunks": int(chunks),
+                     "direct_dma_fraction": round(direct, 4),
+                     "bytes_h2d": b_in, "bytes_d2h": b_out}
+        res[kind]["bit_exact_vs_hbm_path"] = bool(np.array_equal(hout.view(np.uint64), want))
+        if kind == "pinned":
+            del hin, hout
+            for p in keep:
+                lib.sts_host_free(p)
+    lib.sts_staging_release()
+    res["note"] = ("end-to-end = host panel in -> host panel out for one sts_fill_diff_ewma_host call; GB/s = "
+                   "bytes / summed per-chunk DMA event time on the staging streams (transfers overlap the kernels "
+                   "and each other, so they do not add up to the wall time)")
+    return res
 
 
 def measured_traffic(workload, S, T):
@@ -302,6 +370,17 @@ def measured_traffic(workload, S, T):
     return rec.get("traffic_bytes_per_launch")
 
 
+def cpu_threads():
+    """Spark local[N] with N = the host cores this process may use: the CPU affinity set,
+    capped by OMP_NUM_THREADS when the environment sets it (the GPU box grants each
+    single-GPU job 16 of its cores and says so there, while nproc reports the whole machine)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+    return max(1, n)
+
+
 def cpu_baseline(args, S, T, K, seed, nan_p, out, acf, p_ar, smooth=None, gpar_ref=None):
     """The oracle (CPU restatement of the reference loops, oracle/) on a bounded sample of
     the same workload, one series per thread like Spark local[N].  The sample series are
@@ -309,7 +388,7 @@ def cpu_baseline(args, S, T, K, seed, nan_p, out, acf, p_ar, smooth=None, gpar_r
     import numpy as np
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
-    threads = max(1, min(16, os.cpu_count() or 1))
+    threads = cpu_threads()
     per_round = threads
     if args.workload in ("stats", "nan_instants", "to_instants", "wire_decode"):
         threads, per_round = 1, 4096     # single-threaded restatements (one partition)

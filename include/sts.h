@@ -37,6 +37,7 @@
 #ifndef STS_H
 #define STS_H
 
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -301,9 +302,34 @@ int sts_gen_panel(double* out, int64_t s0, int64_t S, int64_t T, int64_t ld, uin
 int sts_gen_ar_panel(double* out, double* c, double* phi, int64_t s0, int64_t S, int64_t T,
                      int64_t ld, uint64_t seed, int p, void* stream);
 
-/* ---- host-buffer variants (JNI path): stage host arrays through HBM on the calling
- * thread's stream; err_per_series, c, coef, acf are host arrays.  Return after the
- * results are back on the host. ---- */
+/* ---- host-buffer variants (JNI path).  Each call runs a per-thread PINNED STAGING
+ * PIPELINE: the panel is split by series into chunks of ~64 MB of device traffic, and each
+ * chunk's H2D copy, kernel(s) and D2H copy run on one of three per-thread HIP streams, so
+ * uploads, compute and downloads of consecutive chunks overlap.  Host arrays that are
+ * already pinned (sts_host_alloc) move by DMA directly; pageable arrays go through the
+ * thread's reused pinned bounce buffers.  err_per_series, c, coef, acf, ... are host arrays;
+ * with err_per_series NULL the first failing series becomes the return status (the
+ * reference's exception), decided after every chunk is back.  Return after the results are
+ * on the host.  Reference operators as for the device entry points above. ---- */
+
+/* Pinned host memory for callers that fill it themselves (the JNI shim copies Java arrays
+ * into it with GetDoubleArrayRegion, then calls a _host entry point on it: no JVM array is
+ * held across device work). */
+int sts_host_alloc(size_t bytes, void** out);
+int sts_host_free(void* p);
+/* Free the calling thread's staging streams and buffers (they are otherwise reused). */
+int sts_staging_release(void);
+/* Statistics of the calling thread's last _host call: out8 = {wall ms, H2D ms, kernel ms,
+ * D2H ms (summed per-chunk event times on the staging streams; they overlap each other),
+ * H2D bytes, D2H bytes, chunks, fraction of the bytes moved by direct DMA from / to pinned
+ * caller memory}. */
+int sts_staging_stats(double* out8);
+int sts_fill_autocorr_host(const double* in, double* filled, int64_t S, int64_t T, int64_t ld,
+                           int method, int K, double* acf, int32_t* err_per_series);
+int sts_fill_diff_ewma_host(const double* in, double* out, int64_t S, int64_t T, int64_t ld,
+                            int method, int lag, const double* smoothing, int32_t* err_per_series);
+int sts_ar_fit_remove_host(const double* in, double* out, int64_t S, int64_t T, int64_t ld, int p,
+                           int no_intercept, double* c, double* coef, int32_t* err_per_series);
 int sts_fill_host(const double* in, double* out, int64_t S, int64_t T, int64_t ld, int method,
                   int32_t* err_per_series);
 int sts_autocorr_host(const double* in, int64_t S, int64_t T, int64_t ld, int K, double* acf);

@@ -118,14 +118,7 @@ struct ErrSink {
         hipError_t e = hipMemcpyAsync(h.data(), dev, (size_t)S * sizeof(int32_t), hipMemcpyDeviceToHost, scratch.st);
         if (e == hipSuccess) e = hipStreamSynchronize(scratch.st);
         if (e != hipSuccess) return hip_fail(e, what);
-        for (int64_t s = 0; s < S; s++) {
-            if (h[(size_t)s] == STS_ERR_ALL_NAN) return fail(STS_ERR_ALL_NAN, "Input is all NaNs! (series %lld)", (long long)s);
-            if (h[(size_t)s] == STS_ERR_SINGULAR) return fail(STS_ERR_SINGULAR, "singular AR design matrix (series %lld)", (long long)s);
-            if (h[(size_t)s] == STS_ERR_TOO_MANY_EVALUATIONS)
-                return fail(STS_ERR_TOO_MANY_EVALUATIONS, "TooManyEvaluationsException: illegal state: maximal count (10000) exceeded: evaluations (series %lld)", (long long)s);
-            if (h[(size_t)s] != 0) return fail(h[(size_t)s], "%s failed for series %lld", what, (long long)s);
-        }
-        return STS_OK;
+        return sts::series_status(h.data(), S, what);
     }
 };
 
@@ -260,6 +253,27 @@ int run_tile(const double* in, double* out, double* lagmat, int64_t S, int64_t T
 }
 
 }  // namespace
+
+namespace sts {
+
+// The first failing series of a host copy of err_per_series -> the reference's exception
+// (status + thread-local message); STS_OK when none failed.
+int series_status(const int32_t* h, int64_t S, const char* what) {
+    for (int64_t s = 0; s < S; s++) {
+        if (h[s] == STS_ERR_ALL_NAN) return fail(STS_ERR_ALL_NAN, "Input is all NaNs! (series %lld)", (long long)s);
+        if (h[s] == STS_ERR_SINGULAR) return fail(STS_ERR_SINGULAR, "singular AR design matrix (series %lld)", (long long)s);
+        if (h[s] == STS_ERR_TOO_MANY_EVALUATIONS)
+            return fail(STS_ERR_TOO_MANY_EVALUATIONS,
+                        "TooManyEvaluationsException: illegal state: maximal count (10000) exceeded: evaluations (series %lld)",
+                        (long long)s);
+        if (h[s] != 0) return fail(h[s], "%s failed for series %lld", what, (long long)s);
+    }
+    return STS_OK;
+}
+
+int set_error(int status, const char* msg) { return fail(status, "%s", msg); }
+
+}  // namespace sts
 
 extern "C" {
 

@@ -1,111 +1,418 @@
-// sts_host.cpp -- host-buffer entry points (the JNI path): stage the
-// caller's arrays into HBM on the calling thread's stream (hipStreamPerThread), run the
-// device entry point, copy the results back and wait.  Scratch is stream-ordered, so
-// concurrent executor threads never share buffers.
+// sts_host.cpp -- host-buffer entry points (the JNI path): a per-thread
+// PINNED STAGING PIPELINE in front of the device entry points.
+//
+// A `_host` call is split by series into chunks of ~kChunkBytes of device traffic.  Each
+// chunk runs H2D -> kernel(s) -> D2H on one of kSlots slots, each slot owning a HIP stream,
+// a device buffer and pinned bounce buffers, all reused across calls.  While chunk i's
+// kernel runs, chunk i+1 uploads and chunk i-1 downloads (three streams), and the calling
+// thread fills the next slot's bounce buffer: copy, compute and the CPU side overlap.
+//
+// Host memory that is already pinned (hipHostMalloc'd, e.g. by sts_host_alloc -- the JNI
+// shim copies a Java array straight into such a buffer with GetDoubleArrayRegion) is moved
+// by DMA directly, with no bounce copy; pageable memory goes through the slot's pinned
+// buffer (one CPU copy, the same one hipMemcpy would make internally, but overlapped).
+//
+// Every device entry point runs on the slot's stream; per-series statuses always go to a
+// device array and come back with the chunk, so a NULL err_per_series keeps the reference's
+// exception semantics (the first failing series becomes the return status after all
+// chunks) without a synchronisation per chunk.  Staging state is per calling thread, so
+// Spark's N executor threads never share buffers or streams; sts_staging_release frees it.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <cstring>
+#include <functional>
+#include <vector>
 
-#include "sts.h"
+#include "sts_internal.hpp"
 
 namespace {
 
-hipStream_t kStream = hipStreamPerThread;
+constexpr int kSlots = 3;
+constexpr size_t kChunkBytes = size_t(64) << 20;   // device bytes (in + out) per chunk
+constexpr size_t kAlign = 256;
 
-struct Dev {
-    void* p = nullptr;
-    ~Dev() {
-        if (p) (void)hipFreeAsync(p, kStream);
-    }
-    template <class T>
-    T* as() { return static_cast<T*>(p); }
+size_t align_up(size_t b) { return (b + kAlign - 1) / kAlign * kAlign; }
+
+struct Slot {
+    hipStream_t st = nullptr;
+    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};   // before H2D, after H2D, after kernel, after D2H
+    void* dev = nullptr;
+    size_t dev_cap = 0;
+    void* pin = nullptr;
+    size_t pin_cap = 0;
+    bool busy = false;
+    int64_t s0 = 0, ns = 0;
 };
 
-int up(Dev& d, const void* h, size_t bytes) {
-    if (hipMallocAsync(&d.p, bytes ? bytes : 16, kStream) != hipSuccess) return STS_ERR_HIP;
-    if (h && bytes && hipMemcpyAsync(d.p, h, bytes, hipMemcpyHostToDevice, kStream) != hipSuccess) return STS_ERR_HIP;
+struct Stager {
+    int device = -1;
+    Slot slot[kSlots];
+    // statistics of this thread's last _host call (sts_staging_stats)
+    double st_h2d_ms = 0, st_kernel_ms = 0, st_d2h_ms = 0, st_wall_ms = 0;
+    double st_bytes_h2d = 0, st_bytes_d2h = 0, st_chunks = 0, st_direct = 0;   // bytes moved by direct DMA
+};
+thread_local Stager g_stager;
+
+void release(Stager& g) {
+    for (Slot& s : g.slot) {
+        if (s.st) (void)hipStreamSynchronize(s.st);
+        if (s.dev) (void)hipFree(s.dev);
+        if (s.pin) (void)hipHostFree(s.pin);
+        for (hipEvent_t& e : s.ev)
+            if (e) (void)hipEventDestroy(e);
+        if (s.st) (void)hipStreamDestroy(s.st);
+        s = Slot();
+    }
+    g.device = -1;
+}
+
+int hip_status(hipError_t e, const char* where) {
+    char buf[256];
+    snprintf(buf, sizeof buf, "%s: %s", where, hipGetErrorString(e));
+    return sts::set_error(STS_ERR_HIP, buf);
+}
+
+int ensure_stager(Stager& g) {
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return hip_status(e, "hipGetDevice");
+    if (g.device == dev) return STS_OK;
+    release(g);
+    for (Slot& s : g.slot) {
+        if ((e = hipStreamCreateWithFlags(&s.st, hipStreamNonBlocking)) != hipSuccess) return hip_status(e, "hipStreamCreate");
+        for (hipEvent_t& ev : s.ev)
+            if ((e = hipEventCreate(&ev)) != hipSuccess) return hip_status(e, "hipEventCreate");
+    }
+    g.device = dev;
     return STS_OK;
 }
 
-int down(void* h, const Dev& d, size_t bytes) {
-    if (h && bytes && hipMemcpyAsync(h, d.p, bytes, hipMemcpyDeviceToHost, kStream) != hipSuccess) return STS_ERR_HIP;
+bool is_pinned(const void* p) {
+    if (!p) return false;
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();   // pageable memory: clear the sticky lookup error
+        return false;
+    }
+    return a.type == hipMemoryTypeHost;
+}
+
+// One per-series array of a _host call.  On the device, chunk rows are contiguous (`row`
+// bytes per series); on the host, series s starts at s * hstride.
+struct Arg {
+    const void* src = nullptr;   // host input (copied in), or nullptr
+    void* dst = nullptr;         // host output (copied out), or nullptr; == src for in place
+    size_t row = 0;              // device bytes per series
+    size_t hstride = 0;          // host bytes between series
+    bool pinned_src = false, pinned_dst = false;
+    size_t dev_off = 0, pin_off = 0;   // per-slot layout (set per chunk size)
+};
+
+Arg in_arg(const void* p, size_t row, size_t hstride) {
+    Arg a;
+    a.src = p;
+    a.row = row;
+    a.hstride = hstride;
+    return a;
+}
+Arg out_arg(void* p, size_t row, size_t hstride) {
+    Arg a;
+    a.dst = p;
+    a.row = row;
+    a.hstride = hstride;
+    return a;
+}
+Arg inout_arg(void* p, size_t row, size_t hstride) {
+    Arg a;
+    a.src = p;
+    a.dst = p;
+    a.row = row;
+    a.hstride = hstride;
+    return a;
+}
+
+// kernel(device pointers per arg (chunk-local, row-contiguous), first series, series, stream)
+using Kernel = std::function<int(void* const* dev, int64_t s0, int64_t ns, hipStream_t st)>;
+
+void copy_rows(void* dst, size_t dstride, const void* src, size_t sstride, size_t row, int64_t n) {
+    if (dstride == row && sstride == row) {
+        std::memcpy(dst, src, row * (size_t)n);
+        return;
+    }
+    for (int64_t i = 0; i < n; i++)
+        std::memcpy(static_cast<char*>(dst) + (size_t)i * dstride, static_cast<const char*>(src) + (size_t)i * sstride,
+                    row);
+}
+
+// Wait for a slot's chunk, account its time, copy its pageable outputs to the caller.
+int reap(Stager& g, Slot& sl, std::vector<Arg>& args) {
+    if (!sl.busy) return STS_OK;
+    sl.busy = false;
+    hipError_t e = hipEventSynchronize(sl.ev[3]);
+    if (e != hipSuccess) return hip_status(e, "staging: chunk");
+    float a = 0, b = 0, c = 0;
+    if (hipEventElapsedTime(&a, sl.ev[0], sl.ev[1]) == hipSuccess) g.st_h2d_ms += a;
+    if (hipEventElapsedTime(&b, sl.ev[1], sl.ev[2]) == hipSuccess) g.st_kernel_ms += b;
+    if (hipEventElapsedTime(&c, sl.ev[2], sl.ev[3]) == hipSuccess) g.st_d2h_ms += c;
+    for (Arg& x : args)
+        if (x.dst && !x.pinned_dst)
+            copy_rows(static_cast<char*>(x.dst) + (size_t)sl.s0 * x.hstride, x.hstride,
+                      static_cast<char*>(sl.pin) + x.pin_off, x.row, x.row, sl.ns);
     return STS_OK;
 }
 
-int finish(int st) {
-    hipError_t e = hipStreamSynchronize(kStream);
-    if (st == STS_OK && e != hipSuccess) return STS_ERR_HIP;
-    return st;
+// Run `kern` over S series in chunks through the calling thread's staging slots.
+int staged(int64_t S, std::vector<Arg> args, const Kernel& kern) {
+    const auto t_start = std::chrono::steady_clock::now();
+    Stager& g = g_stager;
+    g.st_h2d_ms = g.st_kernel_ms = g.st_d2h_ms = g.st_wall_ms = 0;
+    g.st_bytes_h2d = g.st_bytes_d2h = g.st_chunks = g.st_direct = 0;
+    if (S <= 0) return STS_OK;
+    int r;
+    if ((r = ensure_stager(g))) return r;
+    size_t per_series = 0;
+    for (Arg& x : args) {
+        x.pinned_src = is_pinned(x.src);
+        x.pinned_dst = (x.dst == x.src) ? x.pinned_src : is_pinned(x.dst);
+        per_series += x.row;
+    }
+    int64_t ns = per_series ? (int64_t)(kChunkBytes / per_series) : S;
+    ns = std::max<int64_t>(1, std::min<int64_t>(ns, S));
+    // per-slot layout: one device region per arg; one pinned region per pageable in / out
+    size_t dev_bytes = 0, pin_bytes = 0;
+    for (Arg& x : args) {
+        x.dev_off = dev_bytes;
+        dev_bytes += align_up(x.row * (size_t)ns);
+        x.pin_off = pin_bytes;
+        if ((x.src && !x.pinned_src) || (x.dst && !x.pinned_dst)) pin_bytes += align_up(x.row * (size_t)ns);
+    }
+    hipError_t e;
+    for (Slot& sl : g.slot) {
+        if (sl.dev_cap < dev_bytes) {
+            if (sl.dev) (void)hipFree(sl.dev);
+            sl.dev = nullptr;
+            sl.dev_cap = 0;
+            if ((e = hipMalloc(&sl.dev, dev_bytes)) != hipSuccess) return hip_status(e, "staging: hipMalloc");
+            sl.dev_cap = dev_bytes;
+        }
+        if (sl.pin_cap < pin_bytes) {
+            if (sl.pin) (void)hipHostFree(sl.pin);
+            sl.pin = nullptr;
+            sl.pin_cap = 0;
+            if ((e = hipHostMalloc(&sl.pin, pin_bytes, hipHostMallocDefault)) != hipSuccess)
+                return hip_status(e, "staging: hipHostMalloc");
+            sl.pin_cap = pin_bytes;
+        }
+    }
+    const int64_t nchunks = (S + ns - 1) / ns;
+    int status = STS_OK;
+    for (int64_t i = 0; i < nchunks && status == STS_OK; i++) {
+        Slot& sl = g.slot[i % kSlots];
+        if ((r = reap(g, sl, args))) return r;
+        sl.s0 = i * ns;
+        sl.ns = std::min<int64_t>(ns, S - sl.s0);
+        char* dev = static_cast<char*>(sl.dev);
+        char* pin = static_cast<char*>(sl.pin);
+        // the calling thread stages pageable inputs while earlier chunks are on the device
+        for (Arg& x : args)
+            if (x.src && !x.pinned_src)
+                copy_rows(pin + x.pin_off, x.row, static_cast<const char*>(x.src) + (size_t)sl.s0 * x.hstride,
+                          x.hstride, x.row, sl.ns);
+        if ((e = hipEventRecord(sl.ev[0], sl.st)) != hipSuccess) return hip_status(e, "staging: event");
+        for (Arg& x : args) {
+            if (!x.src) continue;
+            const size_t n = x.row * (size_t)sl.ns;
+            if (x.pinned_src)
+                e = hipMemcpy2DAsync(dev + x.dev_off, x.row, static_cast<const char*>(x.src) + (size_t)sl.s0 * x.hstride,
+                                     x.hstride, x.row, (size_t)sl.ns, hipMemcpyHostToDevice, sl.st);
+            else
+                e = hipMemcpyAsync(dev + x.dev_off, pin + x.pin_off, n, hipMemcpyHostToDevice, sl.st);
+            if (e != hipSuccess) return hip_status(e, "staging: H2D");
+            g.st_bytes_h2d += (double)n;
+            if (x.pinned_src) g.st_direct += (double)n;
+        }
+        if ((e = hipEventRecord(sl.ev[1], sl.st)) != hipSuccess) return hip_status(e, "staging: event");
+        void* ptrs[16];
+        for (size_t k = 0; k < args.size() && k < 16; k++) ptrs[k] = dev + args[k].dev_off;
+        status = kern(ptrs, sl.s0, sl.ns, sl.st);
+        if ((e = hipEventRecord(sl.ev[2], sl.st)) != hipSuccess) return hip_status(e, "staging: event");
+        for (Arg& x : args) {
+            if (!x.dst || status != STS_OK) continue;
+            const size_t n = x.row * (size_t)sl.ns;
+            if (x.pinned_dst)
+                e = hipMemcpy2DAsync(static_cast<char*>(x.dst) + (size_t)sl.s0 * x.hstride, x.hstride, dev + x.dev_off,
+                                     x.row, x.row, (size_t)sl.ns, hipMemcpyDeviceToHost, sl.st);
+            else
+                e = hipMemcpyAsync(pin + x.pin_off, dev + x.dev_off, n, hipMemcpyDeviceToHost, sl.st);
+            if (e != hipSuccess) return hip_status(e, "staging: D2H");
+            g.st_bytes_d2h += (double)n;
+            if (x.pinned_dst) g.st_direct += (double)n;
+        }
+        if ((e = hipEventRecord(sl.ev[3], sl.st)) != hipSuccess) return hip_status(e, "staging: event");
+        sl.busy = true;
+        g.st_chunks += 1;
+    }
+    for (int64_t i = 0; i < kSlots; i++) {   // drain in issue order
+        Slot& sl = g.slot[(nchunks + i) % kSlots];
+        if ((r = reap(g, sl, args)) && status == STS_OK) status = r;
+    }
+    g.st_wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
+    return status;
 }
 
-size_t panel_bytes(int64_t S, int64_t ld) { return (size_t)(S > 0 ? S : 0) * (size_t)(ld > 0 ? ld : 0) * sizeof(double); }
+size_t panel_stride(int64_t ld) { return (size_t)(ld > 0 ? ld : 0) * sizeof(double); }
+
+// Per-series statuses: the caller's host array, or an internal one whose first failure
+// becomes the return status (the reference's exception) once every chunk is back.
+struct ErrOut {
+    std::vector<int32_t> own;
+    int32_t* h;
+    explicit ErrOut(int32_t* user, int64_t S) : h(user) {
+        if (!h) {
+            own.assign((size_t)(S > 0 ? S : 0), 0);
+            h = own.data();
+        }
+    }
+    int finish(int st, int64_t S, const char* what) {
+        if (st != STS_OK || !own.size()) return st;
+        return sts::series_status(h, S, what);
+    }
+};
 
 }  // namespace
 
 extern "C" {
 
+int sts_host_alloc(size_t bytes, void** out) {
+    if (!out) return sts::set_error(STS_ERR_BAD_ARG, "sts_host_alloc: null output");
+    *out = nullptr;
+    hipError_t e = hipHostMalloc(out, bytes ? bytes : 16, hipHostMallocDefault);
+    return e == hipSuccess ? STS_OK : hip_status(e, "hipHostMalloc");
+}
+
+int sts_host_free(void* p) {
+    if (!p) return STS_OK;
+    hipError_t e = hipHostFree(p);
+    return e == hipSuccess ? STS_OK : hip_status(e, "hipHostFree");
+}
+
+int sts_staging_release(void) {
+    release(g_stager);
+    return STS_OK;
+}
+
+int sts_staging_stats(double* out8) {
+    if (!out8) return sts::set_error(STS_ERR_BAD_ARG, "sts_staging_stats: null output");
+    const Stager& g = g_stager;
+    const double tot = g.st_bytes_h2d + g.st_bytes_d2h;
+    const double v[8] = {g.st_wall_ms, g.st_h2d_ms, g.st_kernel_ms, g.st_d2h_ms,
+                         g.st_bytes_h2d, g.st_bytes_d2h, g.st_chunks, tot > 0 ? g.st_direct / tot : 0.0};
+    std::memcpy(out8, v, sizeof v);
+    return STS_OK;
+}
+
 int sts_fill_host(const double* in, double* out, int64_t S, int64_t T, int64_t ld, int method, int32_t* err) {
-    Dev di, dout, de;
-    int r;
-    if ((r = up(di, in, panel_bytes(S, ld))) || (r = up(dout, nullptr, panel_bytes(S, ld))) ||
-        (r = up(de, nullptr, (size_t)S * sizeof(int32_t))))
-        return finish(r);
-    // without a caller error array the device call checks synchronously (exception semantics)
-    r = sts_fill(di.as<double>(), dout.as<double>(), S, T, ld, ld, method, err ? de.as<int32_t>() : nullptr, kStream);
-    if (r == STS_OK) r = down(out, dout, panel_bytes(S, ld));
-    if (r == STS_OK) r = down(err, de, (size_t)S * sizeof(int32_t));
-    return finish(r);
+    const size_t row = (size_t)(T > 0 ? T : 0) * sizeof(double);
+    if (S > 0 && T > 0 && (!in || !out)) return sts::set_error(STS_ERR_BAD_ARG, "fill: null panel pointer");
+    if (in == out && S * T > 0) return sts::set_error(STS_ERR_BAD_ARG, "fill: out must not alias in (fillts returns a new vector)");
+    // validate through the device entry point's own checks first (no staging on bad input)
+    if (method == STS_FILL_SPLINE || method < STS_FILL_LINEAR || method > STS_FILL_PREVIOUS)
+        return sts_fill(nullptr, nullptr, 0, 0, 0, 0, method, nullptr, nullptr);
+    if (ld < T) return sts_fill(in, out, S, T, ld, ld, method, nullptr, nullptr);
+    ErrOut eo(err, S);
+    const int st = staged(S, {in_arg(in, row, panel_stride(ld)), out_arg(out, row, panel_stride(ld)),
+                              out_arg(eo.h, sizeof(int32_t), sizeof(int32_t))},
+                          [&](void* const* d, int64_t, int64_t n, hipStream_t s) {
+                              return sts_fill(static_cast<const double*>(d[0]), static_cast<double*>(d[1]), n, T, T, T,
+                                              method, static_cast<int32_t*>(d[2]), s);
+                          });
+    return eo.finish(st, S, "fill");
 }
 
 int sts_autocorr_host(const double* in, int64_t S, int64_t T, int64_t ld, int K, double* acf) {
-    Dev di, da;
-    int r;
-    if ((r = up(di, in, panel_bytes(S, ld))) || (r = up(da, nullptr, (size_t)S * (K > 0 ? K : 0) * sizeof(double))))
-        return finish(r);
-    r = sts_autocorr(di.as<double>(), S, T, ld, K, da.as<double>(), kStream);
-    if (r == STS_OK) r = down(acf, da, (size_t)S * (K > 0 ? K : 0) * sizeof(double));
-    return finish(r);
+    if (K < 0 || ld < T || (S > 0 && T > 0 && !in) || (S > 0 && K > 0 && !acf))
+        return sts_autocorr(in, S, T, ld, K, acf, nullptr);   // the device entry point's error
+    const size_t row = (size_t)(T > 0 ? T : 0) * sizeof(double), krow = (size_t)K * sizeof(double);
+    return staged(S, {in_arg(in, row, panel_stride(ld)), out_arg(acf, krow, krow)},
+                  [&](void* const* d, int64_t, int64_t n, hipStream_t s) {
+                      return sts_autocorr(static_cast<const double*>(d[0]), n, T, T, K, static_cast<double*>(d[1]), s);
+                  });
+}
+
+int sts_fill_autocorr_host(const double* in, double* filled, int64_t S, int64_t T, int64_t ld, int method, int K,
+                           double* acf, int32_t* err) {
+    if (method == STS_FILL_NONE) {
+        if (filled) return sts::set_error(STS_ERR_BAD_ARG, "fill_autocorr: filled must be NULL for STS_FILL_NONE");
+        return sts_autocorr_host(in, S, T, ld, K, acf);
+    }
+    if (method == STS_FILL_SPLINE || method < STS_FILL_LINEAR || method > STS_FILL_PREVIOUS || K < 0 || ld < T ||
+        (S * T > 0 && (!in || !filled || in == filled)) || (S > 0 && K > 0 && !acf))
+        return sts_fill_autocorr(in, filled, S, T, ld, ld, method, K, acf, nullptr, nullptr);
+    const size_t row = (size_t)(T > 0 ? T : 0) * sizeof(double), krow = (size_t)K * sizeof(double);
+    ErrOut eo(err, S);
+    const int st = staged(S, {in_arg(in, row, panel_stride(ld)), out_arg(filled, row, panel_stride(ld)),
+                              out_arg(acf, krow, krow), out_arg(eo.h, sizeof(int32_t), sizeof(int32_t))},
+                          [&](void* const* d, int64_t, int64_t n, hipStream_t s) {
+                              return sts_fill_autocorr(static_cast<const double*>(d[0]), static_cast<double*>(d[1]), n,
+                                                       T, T, T, method, K, static_cast<double*>(d[2]),
+                                                       static_cast<int32_t*>(d[3]), s);
+                          });
+    return eo.finish(st, S, "fill_autocorr");
 }
 
 int sts_diff_at_lag_host(const double* in, double* out, int64_t S, int64_t T, int64_t ld, int lag, int start) {
-    if (!(start >= lag))  // validate before staging, like the reference's require() (:361)
-        return sts_diff_at_lag(nullptr, nullptr, 0, 0, 0, 0, lag, start, kStream);
-    Dev di, dout;
-    int r;
-    const bool inplace = (in == out);
-    if ((r = up(di, in, panel_bytes(S, ld)))) return finish(r);
-    if (!inplace && (r = up(dout, out, panel_bytes(S, ld)))) return finish(r);   // dest contents matter for lag 0
-    double* o = inplace ? di.as<double>() : dout.as<double>();
-    r = sts_diff_at_lag(di.as<double>(), o, S, T, ld, ld, lag, start, kStream);
-    if (r == STS_OK) r = down(out, inplace ? di : dout, panel_bytes(S, ld));
-    return finish(r);
+    if (!(start >= lag) || lag <= 0 || ld < T || S * T == 0 || !in || !out)   // require(), lag 0: dest untouched
+        return sts_diff_at_lag(in, out, S, T, ld, ld, lag, start, nullptr);
+    const size_t row = (size_t)T * sizeof(double);
+    if (in == out)   // dest eq ts: the reference's in-place recurrence, per series
+        return staged(S, {inout_arg(out, row, panel_stride(ld))}, [&](void* const* d, int64_t, int64_t n, hipStream_t s) {
+            return sts_diff_at_lag(static_cast<double*>(d[0]), static_cast<double*>(d[0]), n, T, T, T, lag, start, s);
+        });
+    // out-of-place: dest(i) = ts(i) for i < start (:363-369), so dest is fully written
+    return staged(S, {in_arg(in, row, panel_stride(ld)), out_arg(out, row, panel_stride(ld))},
+                  [&](void* const* d, int64_t, int64_t n, hipStream_t s) {
+                      return sts_diff_at_lag(static_cast<const double*>(d[0]), static_cast<double*>(d[1]), n, T, T, T,
+                                             lag, start, s);
+                  });
 }
 
 int sts_lag_matrix_host(const double* in, double* out, int64_t S, int64_t T, int64_t ld, int max_lag, int inc) {
-    Dev di, dout;
-    int r;
-    const int64_t rows = T - max_lag;
-    const size_t ob = (size_t)((S > 0 && rows > 0) ? S * rows * (max_lag + (inc ? 1 : 0)) : 0) * sizeof(double);
-    if ((r = up(di, in, panel_bytes(S, ld))) || (r = up(dout, nullptr, ob))) return finish(r);
-    r = sts_lag_matrix(di.as<double>(), dout.as<double>(), S, T, ld, max_lag, inc, kStream);
-    if (r == STS_OK) r = down(out, dout, ob);
-    return finish(r);
+    if (max_lag < 0 || max_lag > T || ld < T || (S * T > 0 && !in))
+        return sts_lag_matrix(in, out, S, T, ld, max_lag, inc, nullptr);
+    const int64_t rows = T - max_lag, cols = max_lag + (inc ? 1 : 0);
+    const size_t orow = (size_t)(rows * cols) * sizeof(double), row = (size_t)T * sizeof(double);
+    if (orow == 0 || S == 0) return STS_OK;
+    if (!out) return sts_lag_matrix(in, nullptr, S, T, ld, max_lag, inc, nullptr);
+    return staged(S, {in_arg(in, row, panel_stride(ld)), out_arg(out, orow, orow)},
+                  [&](void* const* d, int64_t, int64_t n, hipStream_t s) {
+                      return sts_lag_matrix(static_cast<const double*>(d[0]), static_cast<double*>(d[1]), n, T, T,
+                                            max_lag, inc, s);
+                  });
 }
 
 static int ewma_host(bool add, const double* in, double* out, int64_t S, int64_t T, int64_t ld, const double* sm) {
-    if (!out) return add ? sts_ewma_add(in, nullptr, S, T, ld, ld, sm, kStream)
-                         : sts_ewma_remove(in, nullptr, S, T, ld, ld, sm, kStream);
-    Dev di, dout, ds;
-    int r;
-    const bool inplace = (in == out);
-    if ((r = up(di, in, panel_bytes(S, ld))) || (r = up(ds, sm, (size_t)S * sizeof(double)))) return finish(r);
-    if (!inplace && (r = up(dout, nullptr, panel_bytes(S, ld)))) return finish(r);
-    double* o = inplace ? di.as<double>() : dout.as<double>();
-    r = add ? sts_ewma_add(di.as<double>(), o, S, T, ld, ld, ds.as<double>(), kStream)
-            : sts_ewma_remove(di.as<double>(), o, S, T, ld, ld, ds.as<double>(), kStream);
-    if (r == STS_OK) r = down(out, inplace ? di : dout, panel_bytes(S, ld));
-    return finish(r);
+    auto dev_call = [&](const double* i, double* o, int64_t n, const double* m, hipStream_t s) {
+        return add ? sts_ewma_add(i, o, n, T, T, T, m, s) : sts_ewma_remove(i, o, n, T, T, T, m, s);
+    };
+    if (!out || ld < T || (S > 0 && !sm) || (S * T > 0 && !in))
+        return add ? sts_ewma_add(in, out, S, T, ld, ld, sm, nullptr) : sts_ewma_remove(in, out, S, T, ld, ld, sm, nullptr);
+    if (S * T == 0) return STS_OK;
+    const size_t row = (size_t)T * sizeof(double);
+    if (in == out)   // add: safe; remove: the reference's read-after-overwrite, per series
+        return staged(S, {inout_arg(out, row, panel_stride(ld)), in_arg(sm, sizeof(double), sizeof(double))},
+                      [&](void* const* d, int64_t, int64_t n, hipStream_t s) {
+                          return dev_call(static_cast<double*>(d[0]), static_cast<double*>(d[0]), n,
+                                          static_cast<const double*>(d[1]), s);
+                      });
+    return staged(S, {in_arg(in, row, panel_stride(ld)), out_arg(out, row, panel_stride(ld)),
+                      in_arg(sm, sizeof(double), sizeof(double))},
+                  [&](void* const* d, int64_t, int64_t n, hipStream_t s) {
+                      return dev_call(static_cast<const double*>(d[0]), static_cast<double*>(d[1]), n,
+                                      static_cast<const double*>(d[2]), s);
+                  });
 }
 
 int sts_ewma_add_host(const double* in, double* out, int64_t S, int64_t T, int64_t ld, const double* sm) {
@@ -116,77 +423,128 @@ int sts_ewma_remove_host(const double* in, double* out, int64_t S, int64_t T, in
     return ewma_host(false, in, out, S, T, ld, sm);
 }
 
+int sts_fill_diff_ewma_host(const double* in, double* out, int64_t S, int64_t T, int64_t ld, int method, int lag,
+                            const double* smoothing, int32_t* err) {
+    if (method == STS_FILL_SPLINE || method < STS_FILL_NONE || method > STS_FILL_PREVIOUS || lag < 0 || ld < T ||
+        (S > 0 && !smoothing) || (S * T > 0 && (!in || !out || in == out)))
+        return sts_fill_diff_ewma(in, out, S, T, ld, ld, method, lag, smoothing, nullptr, nullptr);
+    if (S * T == 0) return STS_OK;
+    const size_t row = (size_t)T * sizeof(double);
+    ErrOut eo(err, S);
+    const int st = staged(S, {in_arg(in, row, panel_stride(ld)), out_arg(out, row, panel_stride(ld)),
+                              in_arg(smoothing, sizeof(double), sizeof(double)),
+                              out_arg(eo.h, sizeof(int32_t), sizeof(int32_t))},
+                          [&](void* const* d, int64_t, int64_t n, hipStream_t s) {
+                              return sts_fill_diff_ewma(static_cast<const double*>(d[0]), static_cast<double*>(d[1]), n,
+                                                        T, T, T, method, lag, static_cast<const double*>(d[2]),
+                                                        static_cast<int32_t*>(d[3]), s);
+                          });
+    return eo.finish(st, S, "fill_diff_ewma");
+}
+
 int sts_ewma_fit_host(const double* in, int64_t S, int64_t T, int64_t ld, double* smoothing, int32_t* err) {
-    Dev di, ds, de;
-    int r;
-    if ((r = up(di, in, panel_bytes(S, ld))) || (r = up(ds, nullptr, (size_t)S * sizeof(double))) ||
-        (r = up(de, nullptr, (size_t)S * sizeof(int32_t))))
-        return finish(r);
-    r = sts_ewma_fit(di.as<double>(), S, T, ld, ds.as<double>(), err ? de.as<int32_t>() : nullptr, kStream);
-    if (r == STS_OK) r = down(smoothing, ds, (size_t)S * sizeof(double));
-    if (r == STS_OK) r = down(err, de, (size_t)S * sizeof(int32_t));
-    return finish(r);
+    if (ld < T || (S > 0 && (T < 1 || !smoothing || !in))) return sts_ewma_fit(in, S, T, ld, smoothing, nullptr, nullptr);
+    const size_t row = (size_t)T * sizeof(double);
+    ErrOut eo(err, S);
+    const int st = staged(S, {in_arg(in, row, panel_stride(ld)), out_arg(smoothing, sizeof(double), sizeof(double)),
+                              out_arg(eo.h, sizeof(int32_t), sizeof(int32_t))},
+                          [&](void* const* d, int64_t, int64_t n, hipStream_t s) {
+                              return sts_ewma_fit(static_cast<const double*>(d[0]), n, T, T, static_cast<double*>(d[1]),
+                                                  static_cast<int32_t*>(d[2]), s);
+                          });
+    return eo.finish(st, S, "EWMA.fitModel");
 }
 
 int sts_ar_fit_host(const double* in, int64_t S, int64_t T, int64_t ld, int p, int no_intercept, double* c,
                     double* coef, int32_t* err) {
-    Dev di, dc, dk, de;
-    int r;
-    if ((r = up(di, in, panel_bytes(S, ld))) || (r = up(dc, nullptr, (size_t)S * sizeof(double))) ||
-        (r = up(dk, nullptr, (size_t)S * (p > 0 ? p : 0) * sizeof(double))) ||
-        (r = up(de, nullptr, (size_t)S * sizeof(int32_t))))
-        return finish(r);
-    r = sts_ar_fit(di.as<double>(), S, T, ld, p, no_intercept, dc.as<double>(), dk.as<double>(),
-                   err ? de.as<int32_t>() : nullptr, kStream);
-    if (r == STS_OK) r = down(c, dc, (size_t)S * sizeof(double));
-    if (r == STS_OK) r = down(coef, dk, (size_t)S * p * sizeof(double));
-    if (r == STS_OK) r = down(err, de, (size_t)S * sizeof(int32_t));
-    return finish(r);
+    if (ld < T || p < 1 || p > 31 || T - p < (int64_t)p + 1 || (S > 0 && (!c || !coef || !in)))
+        return sts_ar_fit(in, S, T, ld, p, no_intercept, c, coef, nullptr, nullptr);
+    const size_t row = (size_t)T * sizeof(double), prow = (size_t)p * sizeof(double);
+    ErrOut eo(err, S);
+    const int st = staged(S, {in_arg(in, row, panel_stride(ld)), out_arg(c, sizeof(double), sizeof(double)),
+                              out_arg(coef, prow, prow), out_arg(eo.h, sizeof(int32_t), sizeof(int32_t))},
+                          [&](void* const* d, int64_t, int64_t n, hipStream_t s) {
+                              return sts_ar_fit(static_cast<const double*>(d[0]), n, T, T, p, no_intercept,
+                                                static_cast<double*>(d[1]), static_cast<double*>(d[2]),
+                                                static_cast<int32_t*>(d[3]), s);
+                          });
+    return eo.finish(st, S, "ar_fit");
+}
+
+int sts_ar_fit_remove_host(const double* in, double* out, int64_t S, int64_t T, int64_t ld, int p, int no_intercept,
+                           double* c, double* coef, int32_t* err) {
+    if (!out || in == out || ld < T || p < 1 || p > 31 || T - p < (int64_t)p + 1 || (S > 0 && (!c || !coef || !in)))
+        return sts_ar_fit_remove(in, out, S, T, ld, ld, p, no_intercept, c, coef, nullptr, nullptr);
+    const size_t row = (size_t)T * sizeof(double), prow = (size_t)p * sizeof(double);
+    ErrOut eo(err, S);
+    const int st = staged(S, {in_arg(in, row, panel_stride(ld)), out_arg(out, row, panel_stride(ld)),
+                              out_arg(c, sizeof(double), sizeof(double)), out_arg(coef, prow, prow),
+                              out_arg(eo.h, sizeof(int32_t), sizeof(int32_t))},
+                          [&](void* const* d, int64_t, int64_t n, hipStream_t s) {
+                              return sts_ar_fit_remove(static_cast<const double*>(d[0]), static_cast<double*>(d[1]), n,
+                                                       T, T, T, p, no_intercept, static_cast<double*>(d[2]),
+                                                       static_cast<double*>(d[3]), static_cast<int32_t*>(d[4]), s);
+                          });
+    return eo.finish(st, S, "ar_fit_remove");
 }
 
 int sts_garch_fit_host(const double* in, int64_t S, int64_t T, int64_t ld, double* params, int32_t* err) {
-    Dev di, dp, de;
-    int r;
-    if ((r = up(di, in, panel_bytes(S, ld))) || (r = up(dp, nullptr, (size_t)S * 3 * sizeof(double))) ||
-        (r = up(de, nullptr, (size_t)S * sizeof(int32_t))))
-        return finish(r);
-    r = sts_garch_fit(di.as<double>(), S, T, ld, dp.as<double>(), err ? de.as<int32_t>() : nullptr, kStream);
-    if (r == STS_OK) r = down(params, dp, (size_t)S * 3 * sizeof(double));
-    if (r == STS_OK) r = down(err, de, (size_t)S * sizeof(int32_t));
-    return finish(r);
+    if (ld < T || (S > 0 && (!params || (T > 0 && !in)))) return sts_garch_fit(in, S, T, ld, params, nullptr, nullptr);
+    const size_t row = (size_t)(T > 0 ? T : 0) * sizeof(double);
+    ErrOut eo(err, S);
+    const int st = staged(S, {in_arg(in, row, panel_stride(ld)), out_arg(params, 3 * sizeof(double), 3 * sizeof(double)),
+                              out_arg(eo.h, sizeof(int32_t), sizeof(int32_t))},
+                          [&](void* const* d, int64_t, int64_t n, hipStream_t s) {
+                              return sts_garch_fit(static_cast<const double*>(d[0]), n, T, T, static_cast<double*>(d[1]),
+                                                   static_cast<int32_t*>(d[2]), s);
+                          });
+    return eo.finish(st, S, "GARCH.fitModel");
 }
 
-int sts_argarch_fit_host(const double* in, int64_t S, int64_t T, int64_t ld, double* c, double* phi,
-                         double* params, int32_t* err) {
-    Dev di, dc, dphi, dp, de;
-    int r;
-    if ((r = up(di, in, panel_bytes(S, ld))) || (r = up(dc, nullptr, (size_t)S * sizeof(double))) ||
-        (r = up(dphi, nullptr, (size_t)S * sizeof(double))) ||
-        (r = up(dp, nullptr, (size_t)S * 3 * sizeof(double))) || (r = up(de, nullptr, (size_t)S * sizeof(int32_t))))
-        return finish(r);
-    r = sts_argarch_fit(di.as<double>(), S, T, ld, dc.as<double>(), dphi.as<double>(), dp.as<double>(),
-                        err ? de.as<int32_t>() : nullptr, kStream);
-    if (r == STS_OK) r = down(c, dc, (size_t)S * sizeof(double));
-    if (r == STS_OK) r = down(phi, dphi, (size_t)S * sizeof(double));
-    if (r == STS_OK) r = down(params, dp, (size_t)S * 3 * sizeof(double));
-    if (r == STS_OK) r = down(err, de, (size_t)S * sizeof(int32_t));
-    return finish(r);
+int sts_argarch_fit_host(const double* in, int64_t S, int64_t T, int64_t ld, double* c, double* phi, double* params,
+                         int32_t* err) {
+    if (ld < T || T - 1 < 2 || (S > 0 && (!c || !phi || !params || !in)))
+        return sts_argarch_fit(in, S, T, ld, c, phi, params, nullptr, nullptr);
+    const size_t row = (size_t)T * sizeof(double);
+    ErrOut eo(err, S);
+    const int st = staged(S, {in_arg(in, row, panel_stride(ld)), out_arg(c, sizeof(double), sizeof(double)),
+                              out_arg(phi, sizeof(double), sizeof(double)),
+                              out_arg(params, 3 * sizeof(double), 3 * sizeof(double)),
+                              out_arg(eo.h, sizeof(int32_t), sizeof(int32_t))},
+                          [&](void* const* d, int64_t, int64_t n, hipStream_t s) {
+                              return sts_argarch_fit(static_cast<const double*>(d[0]), n, T, T,
+                                                     static_cast<double*>(d[1]), static_cast<double*>(d[2]),
+                                                     static_cast<double*>(d[3]), static_cast<int32_t*>(d[4]), s);
+                          });
+    return eo.finish(st, S, "ARGARCH.fitModel");
 }
 
 static int ar_host(bool add, const double* in, double* out, int64_t S, int64_t T, int64_t ld, const double* c,
                    const double* coef, int p) {
-    Dev di, dout, dc, dk;
-    int r;
-    const bool inplace = (in == out);
-    if ((r = up(di, in, panel_bytes(S, ld))) || (r = up(dc, c, (size_t)S * sizeof(double))) ||
-        (r = up(dk, coef, (size_t)S * (p > 0 ? p : 0) * sizeof(double))))
-        return finish(r);
-    if (!inplace && (r = up(dout, nullptr, panel_bytes(S, ld)))) return finish(r);
-    double* o = inplace ? di.as<double>() : dout.as<double>();
-    r = add ? sts_ar_add(di.as<double>(), o, S, T, ld, ld, dc.as<double>(), dk.as<double>(), p, kStream)
-            : sts_ar_remove(di.as<double>(), o, S, T, ld, ld, dc.as<double>(), dk.as<double>(), p, kStream);
-    if (r == STS_OK) r = down(out, inplace ? di : dout, panel_bytes(S, ld));
-    return finish(r);
+    auto dev_call = [&](const double* i, double* o, int64_t n, const double* cc, const double* k, hipStream_t s) {
+        return add ? sts_ar_add(i, o, n, T, T, T, cc, k, p, s) : sts_ar_remove(i, o, n, T, T, T, cc, k, p, s);
+    };
+    if (!out || ld < T || p < 0 || (S > 0 && (!c || (p > 0 && !coef))) || (S * T > 0 && !in))
+        return add ? sts_ar_add(in, out, S, T, ld, ld, c, coef, p, nullptr)
+                   : sts_ar_remove(in, out, S, T, ld, ld, c, coef, p, nullptr);
+    if (S * T == 0) return STS_OK;
+    const size_t row = (size_t)T * sizeof(double), prow = (size_t)(p > 0 ? p : 1) * sizeof(double);
+    const double zero = 0.0;
+    const double* k = p > 0 ? coef : &zero;
+    const size_t kst = p > 0 ? prow : 0;   // (p = 0: no coefficients; a dummy row)
+    if (in == out)
+        return staged(S, {inout_arg(out, row, panel_stride(ld)), in_arg(c, sizeof(double), sizeof(double)),
+                          in_arg(k, prow, kst)},
+                      [&](void* const* d, int64_t, int64_t n, hipStream_t s) {
+                          return dev_call(static_cast<double*>(d[0]), static_cast<double*>(d[0]), n,
+                                          static_cast<const double*>(d[1]), static_cast<const double*>(d[2]), s);
+                      });
+    return staged(S, {in_arg(in, row, panel_stride(ld)), out_arg(out, row, panel_stride(ld)),
+                      in_arg(c, sizeof(double), sizeof(double)), in_arg(k, prow, kst)},
+                  [&](void* const* d, int64_t, int64_t n, hipStream_t s) {
+                      return dev_call(static_cast<const double*>(d[0]), static_cast<double*>(d[1]), n,
+                                      static_cast<const double*>(d[2]), static_cast<const double*>(d[3]), s);
+                  });
 }
 
 int sts_ar_remove_host(const double* in, double* out, int64_t S, int64_t T, int64_t ld, const double* c,

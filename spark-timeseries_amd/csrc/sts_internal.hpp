@@ -58,6 +58,11 @@ inline const char* ab_knob(const char* name) { return std::getenv(name); }
 inline const char* ab_knob(const char*) { return nullptr; }
 #endif
 
+// status helpers of the C-ABI layer (sts_api.cpp): the first failing entry of a host copy of
+// err_per_series as the reference's exception; a status with a thread-local message
+int series_status(const int32_t* h, int64_t S, const char* what);
+int set_error(int status, const char* msg);
+
 // launchers (return hipError_t of the launch)
 hipError_t launch_tile(int method, int tw, const TileArgs& a, hipStream_t st);
 hipError_t launch_acf_finalize(const FinalizeArgs& a, hipStream_t st);

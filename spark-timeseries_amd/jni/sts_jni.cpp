@@ -1,70 +1,226 @@
 // sts_jni.cpp -- JNI shim: com.cloudera.sparkts.StsNative -> libsts_hip.so (include/sts.h).
 //
 // Built only where a JDK is present (`make -C spark-timeseries_amd jni JAVA_HOME=...`); this
-// image has no JDK, so the shim is compiled and exercised on a JVM host.
+// image has no JDK.  tests/test_jni_shim.py compiles it against a minimal
+// stand-in of the JNI C++ interface for a syntax/type check only; it runs on a JVM host.
 // The Scala side gathers a Spark partition's records into ONE
 // series-contiguous double[] panel (S x T) and makes one call per partition.
 //
-// Each native method pins the Java arrays (GetPrimitiveArrayCritical: no copy on HotSpot),
-// calls the `_host` C entry point (which stages through HBM on the calling executor
-// thread's own HIP stream) and maps the status to the SAME exception class and message the
-// reference throws.  Critical sections contain no JNI calls.
+// Memory: a native method never holds a Java array across device work.  It copies the input
+// array into the calling thread's PINNED buffer with GetDoubleArrayRegion (one copy, no
+// critical section, the GC stays free), calls the `_host` entry point on that pinned memory
+// (DMA straight from it, chunked and overlapped with the kernels: sts_host.cpp), and copies
+// the result back with SetDoubleArrayRegion.  Small per-series arrays (smoothing, c, coef,
+// params, acf) go through ordinary native buffers.  Every array's length is checked against
+// what the call will read or write before anything is copied.
+//
+// Errors map to the SAME exception class the reference throws, built with
+// that class's real constructor; classes and constructors are resolved once in JNI_OnLoad
+// (the loader of the class that loaded this library, i.e. the application's, which holds
+// commons-math3) and kept as global references.  A class that cannot be found there is
+// replaced by java.lang.RuntimeException with the library's message.
 #include <jni.h>
+
+#include <cstdint>
+#include <cstring>
+#include <vector>
 
 #include "sts.h"
 
 namespace {
 
-struct Pinned {
-    JNIEnv* env;
-    jarray arr;
-    void* p;
-    Pinned(JNIEnv* e, jarray a) : env(e), arr(a), p(a ? e->GetPrimitiveArrayCritical(a, nullptr) : nullptr) {}
-    ~Pinned() {
-        if (p) env->ReleasePrimitiveArrayCritical(arr, p, 0);
-    }
-    double* d() { return static_cast<double*>(p); }
-    int32_t* i() { return static_cast<int32_t*>(p); }
+// ---- exception classes, resolved once ----
+struct Cls {
+    jclass cls = nullptr;
+    jmethodID ctor = nullptr;
 };
+Cls g_iae, g_uoe, g_npe, g_rte;              // java.lang.*(String)
+Cls g_singular;                               // commons-math3 SingularMatrixException()
+Cls g_tme, g_tmi;                             // TooManyEvaluations / TooManyIterationsException(Number)
+Cls g_miae;                                   // MathIllegalArgumentException(Localizable, Object...)
+jobject g_not_enough = nullptr;               // LocalizedFormats.NOT_ENOUGH_DATA_FOR_NUMBER_OF_PREDICTORS
+jclass g_integer = nullptr;
+jclass g_object = nullptr;
+jmethodID g_int_valueof = nullptr;
 
-void throw_for(JNIEnv* env, int status) {
-    const char* cls = "java/lang/RuntimeException";
+jclass global_class(JNIEnv* env, const char* name) {
+    jclass c = env->FindClass(name);
+    if (!c) {
+        env->ExceptionClear();   // NoClassDefFoundError: leave nothing pending
+        return nullptr;
+    }
+    jclass g = static_cast<jclass>(env->NewGlobalRef(c));
+    env->DeleteLocalRef(c);
+    return g;
+}
+
+Cls resolve(JNIEnv* env, const char* name, const char* sig) {
+    Cls r;
+    r.cls = global_class(env, name);
+    if (r.cls) {
+        r.ctor = env->GetMethodID(r.cls, "<init>", sig);
+        if (!r.ctor) env->ExceptionClear();
+    }
+    return r;
+}
+
+void throw_string(JNIEnv* env, const Cls& c, const char* msg) {
+    const Cls& k = (c.cls && c.ctor) ? c : g_rte;
+    if (k.cls) env->ThrowNew(k.cls, msg);
+}
+
+jobject boxed(JNIEnv* env, jint v) {
+    return (g_integer && g_int_valueof) ? env->CallStaticObjectMethod(g_integer, g_int_valueof, v) : nullptr;
+}
+
+// Throw the reference's exception for a non-OK status.  nobs / nvars: the commons-math3
+// NOT_ENOUGH_DATA_FOR_NUMBER_OF_PREDICTORS arguments (rows, regressors) of an AR fit.
+void throw_for(JNIEnv* env, int status, jint nobs = 0, jint nvars = 0) {
+    if (status == STS_OK || env->ExceptionCheck()) return;
     const char* msg = sts_last_error();
+    jthrowable t = nullptr;
     switch (status) {
-    case STS_OK: return;
-    case STS_ERR_ALL_NAN: cls = "java/lang/IllegalArgumentException"; msg = "Input is all NaNs!"; break;
+    case STS_ERR_ALL_NAN: return throw_string(env, g_iae, "Input is all NaNs!");
     case STS_ERR_REQUIREMENT:
-    case STS_ERR_BAD_ARG: cls = "java/lang/IllegalArgumentException"; break;
-    case STS_ERR_UNSUPPORTED_METHOD: cls = "java/lang/UnsupportedOperationException"; break;
-    case STS_ERR_NULL_DEST: cls = "java/lang/NullPointerException"; break;
-    case STS_ERR_NOT_ENOUGH_DATA: cls = "org/apache/commons/math3/exception/MathIllegalArgumentException"; break;
-    case STS_ERR_SINGULAR: cls = "org/apache/commons/math3/linear/SingularMatrixException"; break;
-    case STS_ERR_TOO_MANY_EVALUATIONS: cls = "org/apache/commons/math3/exception/TooManyEvaluationsException"; break;
-    case STS_ERR_TOO_MANY_ITERATIONS: cls = "org/apache/commons/math3/exception/TooManyIterationsException"; break;
+    case STS_ERR_BAD_ARG: return throw_string(env, g_iae, msg);
+    case STS_ERR_UNSUPPORTED_METHOD: return throw_string(env, g_uoe, msg);
+    case STS_ERR_NULL_DEST: return throw_string(env, g_npe, msg);
+    case STS_ERR_SINGULAR:
+        if (g_singular.cls && g_singular.ctor) t = static_cast<jthrowable>(env->NewObject(g_singular.cls, g_singular.ctor));
+        break;
+    case STS_ERR_TOO_MANY_EVALUATIONS:
+    case STS_ERR_TOO_MANY_ITERATIONS: {
+        const Cls& c = status == STS_ERR_TOO_MANY_EVALUATIONS ? g_tme : g_tmi;
+        jobject max = boxed(env, 10000);   // MaxEval / MaxIter of the reference's optimizers
+        if (c.cls && c.ctor && max) t = static_cast<jthrowable>(env->NewObject(c.cls, c.ctor, max));
+        break;
+    }
+    case STS_ERR_NOT_ENOUGH_DATA:
+        if (g_miae.cls && g_miae.ctor && g_not_enough && g_object) {
+            jobjectArray args = env->NewObjectArray(2, g_object, nullptr);
+            if (args) {
+                env->SetObjectArrayElement(args, 0, boxed(env, nobs));
+                env->SetObjectArrayElement(args, 1, boxed(env, nvars));
+                t = static_cast<jthrowable>(env->NewObject(g_miae.cls, g_miae.ctor, g_not_enough, args));
+            }
+        }
+        break;
     default: break;
     }
-    jclass c = env->FindClass(cls);
-    if (!c) c = env->FindClass("java/lang/RuntimeException");
-    env->ThrowNew(c, msg);
+    if (env->ExceptionCheck()) return;       // a constructor threw: that exception stands
+    if (t) {
+        env->Throw(t);
+        return;
+    }
+    throw_string(env, g_rte, msg);
 }
+
+// ---- the calling thread's pinned buffers (grow-only; freed when the thread ends) ----
+struct PinBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    double* get(size_t bytes) {
+        if (bytes > cap) {
+            if (p) sts_host_free(p);
+            p = nullptr;
+            cap = 0;
+            if (sts_host_alloc(bytes, &p) != STS_OK) return nullptr;
+            cap = bytes;
+        }
+        return static_cast<double*>(p);
+    }
+    ~PinBuf() {
+        if (p) sts_host_free(p);
+    }
+};
+thread_local PinBuf t_in, t_out;
+
+bool check_len(JNIEnv* env, jarray a, int64_t need, const char* what) {
+    if (!a) {
+        throw_string(env, g_npe, what);
+        return false;
+    }
+    if ((int64_t)env->GetArrayLength(a) < need) {
+        throw_string(env, g_iae, what);
+        return false;
+    }
+    return true;
+}
+
+// A Java double[] copied into a native buffer for the call (and, for outputs, back after it).
+struct Region {
+    JNIEnv* env;
+    jdoubleArray arr;
+    jsize n;
+    std::vector<double> own;
+    double* p = nullptr;
+    // pinned: use the thread's pinned buffer `pb` (the panel); copy_in: read the array
+    Region(JNIEnv* e, jdoubleArray a, int64_t count, bool copy_in, PinBuf* pb = nullptr) : env(e), arr(a), n((jsize)count) {
+        if (pb) p = pb->get((size_t)(count > 0 ? count : 1) * sizeof(double));
+        if (!p) {
+            own.resize((size_t)(count > 0 ? count : 1));
+            p = own.data();
+        }
+        if (copy_in && count > 0) env->GetDoubleArrayRegion(arr, 0, n, p);
+    }
+    void copy_out() {
+        if (n > 0 && !env->ExceptionCheck()) env->SetDoubleArrayRegion(arr, 0, n, p);
+    }
+};
+
+int64_t prod(int64_t a, int64_t b) { return (a > 0 && b > 0) ? a * b : 0; }
 
 }  // namespace
 
 extern "C" {
+
+JNIEXPORT jint JNICALL JNI_OnLoad(JavaVM* vm, void*) {
+    JNIEnv* env = nullptr;
+    if (vm->GetEnv(reinterpret_cast<void**>(&env), JNI_VERSION_1_6) != JNI_OK) return JNI_ERR;
+    g_rte = resolve(env, "java/lang/RuntimeException", "(Ljava/lang/String;)V");
+    g_iae = resolve(env, "java/lang/IllegalArgumentException", "(Ljava/lang/String;)V");
+    g_uoe = resolve(env, "java/lang/UnsupportedOperationException", "(Ljava/lang/String;)V");
+    g_npe = resolve(env, "java/lang/NullPointerException", "(Ljava/lang/String;)V");
+    g_singular = resolve(env, "org/apache/commons/math3/linear/SingularMatrixException", "()V");
+    g_tme = resolve(env, "org/apache/commons/math3/exception/TooManyEvaluationsException", "(Ljava/lang/Number;)V");
+    g_tmi = resolve(env, "org/apache/commons/math3/exception/TooManyIterationsException", "(Ljava/lang/Number;)V");
+    g_miae = resolve(env, "org/apache/commons/math3/exception/MathIllegalArgumentException",
+                     "(Lorg/apache/commons/math3/exception/util/Localizable;[Ljava/lang/Object;)V");
+    g_integer = global_class(env, "java/lang/Integer");
+    g_object = global_class(env, "java/lang/Object");
+    if (g_integer) {
+        g_int_valueof = env->GetStaticMethodID(g_integer, "valueOf", "(I)Ljava/lang/Integer;");
+        if (!g_int_valueof) env->ExceptionClear();
+    }
+    if (jclass lf = global_class(env, "org/apache/commons/math3/exception/util/LocalizedFormats")) {
+        jfieldID f = env->GetStaticFieldID(lf, "NOT_ENOUGH_DATA_FOR_NUMBER_OF_PREDICTORS",
+                                           "Lorg/apache/commons/math3/exception/util/LocalizedFormats;");
+        if (f) {
+            jobject v = env->GetStaticObjectField(lf, f);
+            if (v) g_not_enough = env->NewGlobalRef(v);
+        } else {
+            env->ExceptionClear();
+        }
+    }
+    return JNI_VERSION_1_6;
+}
 
 // UnivariateTimeSeries.fillts over a partition panel (S/UnivariateTimeSeries.scala:141-150)
 JNIEXPORT void JNICALL Java_com_cloudera_sparkts_StsNative_fill(JNIEnv* env, jclass, jdoubleArray in,
                                                                  jdoubleArray out, jlong S, jlong T,
                                                                  jstring method) {
     const char* m = env->GetStringUTFChars(method, nullptr);
-    int code = sts_fill_method_from_name(m);
+    if (!m) return;
+    const int code = sts_fill_method_from_name(m);
     env->ReleaseStringUTFChars(method, m);
     if (code < 0) return throw_for(env, STS_ERR_UNSUPPORTED_METHOD);
-    int st;
-    {
-        Pinned pi(env, in), po(env, out);
-        st = sts_fill_host(pi.d(), po.d(), S, T, T, code, nullptr);
-    }
+    const int64_t n = prod(S, T);
+    if (!check_len(env, in, n, "fill: ts array shorter than S * T") ||
+        !check_len(env, out, n, "fill: dest array shorter than S * T"))
+        return;
+    Region ri(env, in, n, true, &t_in), ro(env, out, n, false, &t_out);
+    const int st = sts_fill_host(ri.p, ro.p, S, T, T, code, nullptr);
+    if (st == STS_OK) ro.copy_out();
     throw_for(env, st);
 }
 
@@ -72,10 +228,36 @@ JNIEXPORT void JNICALL Java_com_cloudera_sparkts_StsNative_fill(JNIEnv* env, jcl
 JNIEXPORT void JNICALL Java_com_cloudera_sparkts_StsNative_autocorr(JNIEnv* env, jclass, jdoubleArray in,
                                                                      jlong S, jlong T, jint numLags,
                                                                      jdoubleArray acf) {
-    int st;
-    {
-        Pinned pi(env, in), pa(env, acf);
-        st = sts_autocorr_host(pi.d(), S, T, T, numLags, pa.d());
+    const int64_t n = prod(S, T), na = prod(S, numLags);
+    if (!check_len(env, in, n, "autocorr: ts array shorter than S * T") ||
+        !check_len(env, acf, na, "autocorr: result array shorter than S * numLags"))
+        return;
+    Region ri(env, in, n, true, &t_in), ra(env, acf, na, false);
+    const int st = sts_autocorr_host(ri.p, S, T, T, numLags, ra.p);
+    if (st == STS_OK) ra.copy_out();
+    throw_for(env, st);
+}
+
+// TimeSeriesRDD.fill(method) followed by autocorr of every filled series (C1 / C3), one call
+JNIEXPORT void JNICALL Java_com_cloudera_sparkts_StsNative_fillAutocorr(JNIEnv* env, jclass, jdoubleArray in,
+                                                                         jdoubleArray filled, jlong S, jlong T,
+                                                                         jstring method, jint numLags,
+                                                                         jdoubleArray acf) {
+    const char* m = env->GetStringUTFChars(method, nullptr);
+    if (!m) return;
+    const int code = sts_fill_method_from_name(m);
+    env->ReleaseStringUTFChars(method, m);
+    if (code < 0) return throw_for(env, STS_ERR_UNSUPPORTED_METHOD);
+    const int64_t n = prod(S, T), na = prod(S, numLags);
+    if (!check_len(env, in, n, "fillAutocorr: ts array shorter than S * T") ||
+        !check_len(env, filled, n, "fillAutocorr: filled array shorter than S * T") ||
+        !check_len(env, acf, na, "fillAutocorr: result array shorter than S * numLags"))
+        return;
+    Region ri(env, in, n, true, &t_in), rf(env, filled, n, false, &t_out), ra(env, acf, na, false);
+    const int st = sts_fill_autocorr_host(ri.p, rf.p, S, T, T, code, numLags, ra.p, nullptr);
+    if (st == STS_OK) {
+        rf.copy_out();
+        ra.copy_out();
     }
     throw_for(env, st);
 }
@@ -84,13 +266,20 @@ JNIEXPORT void JNICALL Java_com_cloudera_sparkts_StsNative_autocorr(JNIEnv* env,
 JNIEXPORT void JNICALL Java_com_cloudera_sparkts_StsNative_differencesAtLag(JNIEnv* env, jclass, jdoubleArray in,
                                                                              jdoubleArray dest, jlong S, jlong T,
                                                                              jint lag, jint start) {
+    const int64_t n = prod(S, T);
+    if (!check_len(env, in, n, "differencesAtLag: ts array shorter than S * T") ||
+        !check_len(env, dest, n, "differencesAtLag: dest array shorter than S * T"))
+        return;
     int st;
     if (env->IsSameObject(in, dest)) {
-        Pinned p(env, in);
-        st = sts_diff_at_lag_host(p.d(), p.d(), S, T, T, lag, start);
+        Region r(env, in, n, true, &t_in);
+        st = sts_diff_at_lag_host(r.p, r.p, S, T, T, lag, start);
+        if (st == STS_OK) r.copy_out();
     } else {
-        Pinned pi(env, in), po(env, dest);
-        st = sts_diff_at_lag_host(pi.d(), po.d(), S, T, T, lag, start);
+        // dest is read as well (lag 0 leaves it untouched): copy it in too
+        Region ri(env, in, n, true, &t_in), ro(env, dest, n, true, &t_out);
+        st = sts_diff_at_lag_host(ri.p, ro.p, S, T, T, lag, start);
+        if (st == STS_OK) ro.copy_out();
     }
     throw_for(env, st);
 }
@@ -100,11 +289,14 @@ JNIEXPORT void JNICALL Java_com_cloudera_sparkts_StsNative_differencesAtLag(JNIE
 JNIEXPORT void JNICALL Java_com_cloudera_sparkts_StsNative_lag(JNIEnv* env, jclass, jdoubleArray in,
                                                                 jdoubleArray out, jlong S, jlong T, jint maxLag,
                                                                 jboolean includeOriginal) {
-    int st;
-    {
-        Pinned pi(env, in), po(env, out);
-        st = sts_lag_matrix_host(pi.d(), po.d(), S, T, T, maxLag, includeOriginal ? 1 : 0);
-    }
+    const int64_t n = prod(S, T);
+    const int64_t no = prod(S, prod(T - maxLag, maxLag + (includeOriginal ? 1 : 0)));
+    if (!check_len(env, in, n, "lag: ts array shorter than S * T") ||
+        !check_len(env, out, no, "lag: result array shorter than S * (T - maxLag) * (maxLag + inc)"))
+        return;
+    Region ri(env, in, n, true, &t_in), ro(env, out, no, false, &t_out);
+    const int st = sts_lag_matrix_host(ri.p, ro.p, S, T, T, maxLag, includeOriginal ? 1 : 0);
+    if (st == STS_OK) ro.copy_out();
     throw_for(env, st);
 }
 
@@ -113,38 +305,69 @@ JNIEXPORT void JNICALL Java_com_cloudera_sparkts_StsNative_ewma(JNIEnv* env, jcl
                                                                  jdoubleArray in, jdoubleArray dest, jlong S,
                                                                  jlong T, jdoubleArray smoothing) {
     if (!dest) return throw_for(env, STS_ERR_NULL_DEST);
+    const int64_t n = prod(S, T);
+    if (!check_len(env, in, n, "EWMA: ts array shorter than S * T") ||
+        !check_len(env, dest, n, "EWMA: dest array shorter than S * T") ||
+        !check_len(env, smoothing, S, "EWMA: smoothing array shorter than S"))
+        return;
+    Region rs(env, smoothing, S, true);
     int st;
     if (env->IsSameObject(in, dest)) {
-        Pinned p(env, in), ps(env, smoothing);
-        st = add ? sts_ewma_add_host(p.d(), p.d(), S, T, T, ps.d()) : sts_ewma_remove_host(p.d(), p.d(), S, T, T, ps.d());
+        Region r(env, in, n, true, &t_in);
+        st = add ? sts_ewma_add_host(r.p, r.p, S, T, T, rs.p) : sts_ewma_remove_host(r.p, r.p, S, T, T, rs.p);
+        if (st == STS_OK) r.copy_out();
     } else {
-        Pinned pi(env, in), po(env, dest), ps(env, smoothing);
-        st = add ? sts_ewma_add_host(pi.d(), po.d(), S, T, T, ps.d())
-                 : sts_ewma_remove_host(pi.d(), po.d(), S, T, T, ps.d());
+        Region ri(env, in, n, true, &t_in), ro(env, dest, n, false, &t_out);
+        st = add ? sts_ewma_add_host(ri.p, ro.p, S, T, T, rs.p) : sts_ewma_remove_host(ri.p, ro.p, S, T, T, rs.p);
+        if (st == STS_OK) ro.copy_out();
     }
     throw_for(env, st);
 }
 
-// Autoregression.fitModel(ts, maxLag, noIntercept) (S/models/Autoregression.scala:38-53)
+// mapSeries(fill(method) -> differencesAtLag(lag) -> EWMAModel(s).addTimeDependentEffects), C2
+JNIEXPORT void JNICALL Java_com_cloudera_sparkts_StsNative_fillDiffEwma(JNIEnv* env, jclass, jdoubleArray in,
+                                                                         jdoubleArray out, jlong S, jlong T,
+                                                                         jstring method, jint lag,
+                                                                         jdoubleArray smoothing) {
+    const char* m = env->GetStringUTFChars(method, nullptr);
+    if (!m) return;
+    const int code = sts_fill_method_from_name(m);
+    env->ReleaseStringUTFChars(method, m);
+    if (code < 0) return throw_for(env, STS_ERR_UNSUPPORTED_METHOD);
+    const int64_t n = prod(S, T);
+    if (!check_len(env, in, n, "fillDiffEwma: ts array shorter than S * T") ||
+        !check_len(env, out, n, "fillDiffEwma: dest array shorter than S * T") ||
+        !check_len(env, smoothing, S, "fillDiffEwma: smoothing array shorter than S"))
+        return;
+    Region ri(env, in, n, true, &t_in), ro(env, out, n, false, &t_out), rs(env, smoothing, S, true);
+    const int st = sts_fill_diff_ewma_host(ri.p, ro.p, S, T, T, code, lag, rs.p, nullptr);
+    if (st == STS_OK) ro.copy_out();
+    throw_for(env, st);
+}
+
 // EWMA.fitModel over a partition panel (S/models/EWMA.scala:44-68)
 JNIEXPORT void JNICALL Java_com_cloudera_sparkts_StsNative_ewmaFit(JNIEnv* env, jclass, jdoubleArray in, jlong S,
                                                                     jlong T, jdoubleArray smoothing) {
-    int st;
-    {
-        Pinned pi(env, in), ps(env, smoothing);
-        st = sts_ewma_fit_host(pi.d(), S, T, T, ps.d(), nullptr);
-    }
+    const int64_t n = prod(S, T);
+    if (!check_len(env, in, n, "ewmaFit: ts array shorter than S * T") ||
+        !check_len(env, smoothing, S, "ewmaFit: result array shorter than S"))
+        return;
+    Region ri(env, in, n, true, &t_in), rs(env, smoothing, S, false);
+    const int st = sts_ewma_fit_host(ri.p, S, T, T, rs.p, nullptr);
+    if (st == STS_OK) rs.copy_out();
     throw_for(env, st);
 }
 
 // GARCH.fitModel per series (S/models/GARCH.scala:33-53): params = S x (omega, alpha, beta)
 JNIEXPORT void JNICALL Java_com_cloudera_sparkts_StsNative_garchFit(JNIEnv* env, jclass, jdoubleArray in, jlong S,
                                                                      jlong T, jdoubleArray params) {
-    int st;
-    {
-        Pinned pi(env, in), pp(env, params);
-        st = sts_garch_fit_host(pi.d(), S, T, T, pp.d(), nullptr);
-    }
+    const int64_t n = prod(S, T);
+    if (!check_len(env, in, n, "garchFit: ts array shorter than S * T") ||
+        !check_len(env, params, prod(S, 3), "garchFit: result array shorter than 3 S"))
+        return;
+    Region ri(env, in, n, true, &t_in), rp(env, params, prod(S, 3), false);
+    const int st = sts_garch_fit_host(ri.p, S, T, T, rp.p, nullptr);
+    if (st == STS_OK) rp.copy_out();
     throw_for(env, st);
 }
 
@@ -152,38 +375,82 @@ JNIEXPORT void JNICALL Java_com_cloudera_sparkts_StsNative_garchFit(JNIEnv* env,
 JNIEXPORT void JNICALL Java_com_cloudera_sparkts_StsNative_argarchFit(JNIEnv* env, jclass, jdoubleArray in, jlong S,
                                                                        jlong T, jdoubleArray c, jdoubleArray phi,
                                                                        jdoubleArray params) {
-    int st;
-    {
-        Pinned pi(env, in), pc(env, c), pf(env, phi), pp(env, params);
-        st = sts_argarch_fit_host(pi.d(), S, T, T, pc.d(), pf.d(), pp.d(), nullptr);
+    const int64_t n = prod(S, T);
+    if (!check_len(env, in, n, "argarchFit: ts array shorter than S * T") ||
+        !check_len(env, c, S, "argarchFit: c array shorter than S") ||
+        !check_len(env, phi, S, "argarchFit: phi array shorter than S") ||
+        !check_len(env, params, prod(S, 3), "argarchFit: params array shorter than 3 S"))
+        return;
+    Region ri(env, in, n, true, &t_in), rc(env, c, S, false), rf(env, phi, S, false), rp(env, params, prod(S, 3), false);
+    const int st = sts_argarch_fit_host(ri.p, S, T, T, rc.p, rf.p, rp.p, nullptr);
+    if (st == STS_OK) {
+        rc.copy_out();
+        rf.copy_out();
+        rp.copy_out();
     }
-    throw_for(env, st);
+    throw_for(env, st, (jint)(T - 1), 1);
 }
 
+// Autoregression.fitModel(ts, maxLag, noIntercept) (S/models/Autoregression.scala:38-53)
 JNIEXPORT void JNICALL Java_com_cloudera_sparkts_StsNative_arFit(JNIEnv* env, jclass, jdoubleArray in, jlong S,
                                                                   jlong T, jint p, jboolean noIntercept,
                                                                   jdoubleArray c, jdoubleArray coef) {
-    int st;
-    {
-        Pinned pi(env, in), pc(env, c), pk(env, coef);
-        st = sts_ar_fit_host(pi.d(), S, T, T, p, noIntercept ? 1 : 0, pc.d(), pk.d(), nullptr);
+    const int64_t n = prod(S, T);
+    if (!check_len(env, in, n, "arFit: ts array shorter than S * T") || !check_len(env, c, S, "arFit: c array shorter than S") ||
+        !check_len(env, coef, prod(S, p), "arFit: coefficient array shorter than S * maxLag"))
+        return;
+    Region ri(env, in, n, true, &t_in), rc(env, c, S, false), rk(env, coef, prod(S, p), false);
+    const int st = sts_ar_fit_host(ri.p, S, T, T, p, noIntercept ? 1 : 0, rc.p, rk.p, nullptr);
+    if (st == STS_OK) {
+        rc.copy_out();
+        rk.copy_out();
     }
-    throw_for(env, st);
+    throw_for(env, st, (jint)(T - p), p);
+}
+
+// The README.md:61 closure over a partition: ar(series, p).removeTimeDependentEffects(series)
+// for every series, fit and residuals in one device pass (sts_ar_fit_remove, C4)
+JNIEXPORT void JNICALL Java_com_cloudera_sparkts_StsNative_arFitRemove(JNIEnv* env, jclass, jdoubleArray in,
+                                                                        jdoubleArray out, jlong S, jlong T, jint p,
+                                                                        jboolean noIntercept, jdoubleArray c,
+                                                                        jdoubleArray coef) {
+    const int64_t n = prod(S, T);
+    if (!check_len(env, in, n, "arFitRemove: ts array shorter than S * T") ||
+        !check_len(env, out, n, "arFitRemove: dest array shorter than S * T") ||
+        !check_len(env, c, S, "arFitRemove: c array shorter than S") ||
+        !check_len(env, coef, prod(S, p), "arFitRemove: coefficient array shorter than S * maxLag"))
+        return;
+    Region ri(env, in, n, true, &t_in), ro(env, out, n, false, &t_out), rc(env, c, S, false),
+        rk(env, coef, prod(S, p), false);
+    const int st = sts_ar_fit_remove_host(ri.p, ro.p, S, T, T, p, noIntercept ? 1 : 0, rc.p, rk.p, nullptr);
+    if (st == STS_OK) {
+        ro.copy_out();
+        rc.copy_out();
+        rk.copy_out();
+    }
+    throw_for(env, st, (jint)(T - p), p);
 }
 
 // ARModel.add/removeTimeDependentEffects (S/models/Autoregression.scala:60-88); dest may be ts
 JNIEXPORT void JNICALL Java_com_cloudera_sparkts_StsNative_ar(JNIEnv* env, jclass, jboolean add, jdoubleArray in,
                                                                jdoubleArray dest, jlong S, jlong T, jdoubleArray c,
                                                                jdoubleArray coef, jint p) {
+    const int64_t n = prod(S, T);
+    if (!check_len(env, in, n, "AR: ts array shorter than S * T") || !check_len(env, dest, n, "AR: dest array shorter than S * T") ||
+        !check_len(env, c, S, "AR: c array shorter than S") ||
+        (p > 0 && !check_len(env, coef, prod(S, p), "AR: coefficient array shorter than S * p")))
+        return;
+    Region rc(env, c, S, true), rk(env, coef, p > 0 ? prod(S, p) : 0, p > 0);
     int st;
     if (env->IsSameObject(in, dest)) {
-        Pinned pi(env, in), pc(env, c), pk(env, coef);
-        st = add ? sts_ar_add_host(pi.d(), pi.d(), S, T, T, pc.d(), pk.d(), p)
-                 : sts_ar_remove_host(pi.d(), pi.d(), S, T, T, pc.d(), pk.d(), p);
+        Region r(env, in, n, true, &t_in);
+        st = add ? sts_ar_add_host(r.p, r.p, S, T, T, rc.p, rk.p, p) : sts_ar_remove_host(r.p, r.p, S, T, T, rc.p, rk.p, p);
+        if (st == STS_OK) r.copy_out();
     } else {
-        Pinned pi(env, in), po(env, dest), pc(env, c), pk(env, coef);
-        st = add ? sts_ar_add_host(pi.d(), po.d(), S, T, T, pc.d(), pk.d(), p)
-                 : sts_ar_remove_host(pi.d(), po.d(), S, T, T, pc.d(), pk.d(), p);
+        Region ri(env, in, n, true, &t_in), ro(env, dest, n, false, &t_out);
+        st = add ? sts_ar_add_host(ri.p, ro.p, S, T, T, rc.p, rk.p, p)
+                 : sts_ar_remove_host(ri.p, ro.p, S, T, T, rc.p, rk.p, p);
+        if (st == STS_OK) ro.copy_out();
     }
     throw_for(env, st);
 }

@@ -79,6 +79,13 @@ SIGNATURES = {
     "sts_ar_fit_host": (_c_int, [_c_vp, _c_i64, _c_i64, _c_i64, _c_int, _c_int, _c_vp, _c_vp, _c_vp]),
     "sts_ar_remove_host": (_c_int, [_c_vp, _c_vp, _c_i64, _c_i64, _c_i64, _c_vp, _c_vp, _c_int]),
     "sts_ar_add_host": (_c_int, [_c_vp, _c_vp, _c_i64, _c_i64, _c_i64, _c_vp, _c_vp, _c_int]),
+    "sts_host_alloc": (_c_int, [ctypes.c_size_t, _c_vp]),
+    "sts_host_free": (_c_int, [_c_vp]),
+    "sts_staging_release": (_c_int, []),
+    "sts_staging_stats": (_c_int, [_c_vp]),
+    "sts_fill_autocorr_host": (_c_int, [_c_vp, _c_vp, _c_i64, _c_i64, _c_i64, _c_int, _c_int, _c_vp, _c_vp]),
+    "sts_fill_diff_ewma_host": (_c_int, [_c_vp, _c_vp, _c_i64, _c_i64, _c_i64, _c_int, _c_int, _c_vp, _c_vp]),
+    "sts_ar_fit_remove_host": (_c_int, [_c_vp, _c_vp, _c_i64, _c_i64, _c_i64, _c_int, _c_int, _c_vp, _c_vp, _c_vp]),
 }
 
 _lib = None
