@@ -88,7 +88,7 @@ def main():
 
     from sparkts import _native
     from sparkts.errors import raise_for_status
-    from sparkts.timeseriesrdd import all_gather_results
+    from sparkts.timeseriesrdd import ResultGather
     _native.ensure_device(local)
     lib = _native.lib()
 
@@ -144,12 +144,23 @@ def main():
         lagbuf = torch.empty((LB, P, T - P), dtype=torch.float64, device=dev)
         x[:, 1] = 1.0 + x[:, 1].nan_to_num(0.0)   # keep x[1] valid: fillNearest throws on an all-NaN tail
 
+    # per-job result gathers: partition sizes exchanged once, outside the timed loop
+    gather = None
+    if world > 1 and args.workload in ("c3", "c1"):
+        gather = ResultGather(S, (K,), torch.float64, dev)
+    elif world > 1 and args.workload == "garch_fit":
+        gather = ResultGather(S, (3,), torch.float64, dev)
+    elif world > 1 and args.workload == "ewma_fit":
+        gather = ResultGather(S, (1,), torch.float64, dev)
+    elif world > 1 and args.workload == "c4":
+        gather = ResultGather(S, (1 + p_ar,), torch.float64, dev)
+
     def step():
         if args.workload in ("c3", "c1"):
             raise_for_status(lib.sts_fill_autocorr(x.data_ptr(), out.data_ptr(), S, T, T, T, 0, K, acf.data_ptr(),
                                                    err.data_ptr(), sp), "fill_autocorr")
             if world > 1:
-                all_gather_results(acf)
+                gather(acf)
         elif args.workload in ("c2", "stage_c2"):
             raise_for_status(lib.sts_fill_diff_ewma(x.data_ptr(), out.data_ptr(), S, T, T, T, 3, 1, smooth.data_ptr(),
                                                     err.data_ptr(), sp), "fill_diff_ewma")
@@ -180,18 +191,18 @@ def main():
             raise_for_status(lib.sts_garch_fit(x.data_ptr(), S, T, T, gpar.data_ptr(), err.data_ptr(), sp),
                              "GARCH.fitModel")
             if world > 1:
-                all_gather_results(gpar)
+                gather(gpar)
         elif args.workload == "ewma_fit":
             raise_for_status(lib.sts_ewma_fit(x.data_ptr(), S, T, T, smooth.data_ptr(), err.data_ptr(), sp),
                              "EWMA.fitModel")
             if world > 1:
-                all_gather_results(smooth[:, None])
+                gather(smooth[:, None])
         elif args.workload == "c4":
             raise_for_status(lib.sts_ar_fit_remove(x.data_ptr(), out.data_ptr(), S, T, T, T, p_ar, 0,
                                                    c_fit.data_ptr(), coef_fit.data_ptr(), err.data_ptr(), sp),
                              "ar_fit_remove")
             if world > 1:
-                all_gather_results(torch.cat([c_fit[:, None], coef_fit], 1))
+                gather(torch.cat([c_fit[:, None], coef_fit], 1))
 
     for _ in range(args.warmup):
         step()

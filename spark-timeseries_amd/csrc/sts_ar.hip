@@ -576,6 +576,219 @@ __global__ __launch_bounds__(64 * kRegWaves, STS_AR_WAVES_PER_EU) void ar_fit_bl
 #endif
 }
 
+// ---------------------------------------------------------------------------------------
+// noIntercept = true (Autoregression.fitModel(ts, maxLag, noIntercept = true)).  Without an
+// intercept the data cannot be centred, and on a price-level series (level L, steps sigma)
+// the lag columns are nearly collinear: cond(X) ~ L / sigma, so the normal equations lose
+// cond^2 (1e-4 relative at L / sigma = 1e6) and one refinement step does not recover it.
+// This kernel solves the same least-squares problem in the unimodular "difference basis":
+//   X beta = theta_1 x_{t-1} - sum_{j=1}^{p-1} theta_{j+1} d_{t-j},  d_u = x_u - x_{u-1},
+//   theta_m = sum_{j >= m} beta_j,
+// i.e. it regresses d_t = x_t - x_{t-1} on [x_{t-1}, d_{t-1}, .., d_{t-p+1}] (rows
+// t = p .. T-1, exactly the reference's rows) and maps back:
+//   beta_1 = alpha + gamma_1,  beta_j = gamma_j - gamma_{j-1},  beta_p = -gamma_{p-1},
+// with alpha = 1 + (coefficient of x_{t-1}), gamma_j = coefficient of d_{t-j}.  The level
+// now lives in one column only; the difference columns carry no level and are nearly
+// orthogonal to it, so the column-scaled Gram is well conditioned.  On a level series the
+// differences are exact (Sterbenz: x_u, x_{u-1} within a factor 2), so no information is
+// lost.  Gram entries are full-range lag products (d x d, x_{t-1} x d) minus at most p head /
+// tail terms, as in the kernels above; lane-0 Cholesky, then two refinement steps against
+// exact residual passes.  One wave per series, operands read through the L1 / L2 (this is
+// not a bench path: C4 fits with an intercept).
+template <int PB>
+__global__ __launch_bounds__(64) void ar_fit_noint_kernel(ArArgs a) {
+    __shared__ double G[(kPMax + 1) * kLd];   // [v0 = d_t | v1 = x_{t-1} | v2.. = d_{t-1}..]
+    __shared__ double sol[kPMax + 2];
+    __shared__ double zz[kPMax + 2];
+    __shared__ int stat;
+    const int lane = threadIdx.x;
+    const int64_t s = blockIdx.x;
+    const int64_t T = a.T;
+    const int p = a.p;
+    const double* xg = a.in + s * a.ld_in;
+    auto X = [&](int64_t u) -> double { return xg[u]; };
+    auto D = [&](int64_t u) -> double { return xg[u] - xg[u - 1]; };   // u >= 1
+
+    // ---- full-range sums: Q_k = sum_{u=1+k}^{T-1} d_u d_{u-k},
+    //      R_b = sum_{t=1+b}^{T-1} x_{t-1} d_{t-b}, X2 = sum_{u=p-1}^{T-2} x_u^2 ----
+    double Q[PB], R[PB], x2 = 0.0, nanchk = 0.0;
+#pragma unroll
+    for (int k = 0; k < PB; k++) Q[k] = R[k] = 0.0;
+    for (int64_t u = 1 + lane; u < T; u += 64) {
+        const double du = D(u);
+        const double xm = X(u - 1);
+        nanchk += du;
+        if (u - 1 >= p - 1 && u - 1 <= T - 2) x2 = __builtin_fma(xm, xm, x2);
+#pragma unroll
+        for (int k = 0; k < PB; k++) {
+            if (k < p && u - k >= 1) {
+                const double dk = D(u - k);
+                Q[k] = __builtin_fma(du, dk, Q[k]);
+                R[k] = __builtin_fma(xm, dk, R[k]);
+            }
+        }
+    }
+    nanchk += X(0);
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+        x2 += __shfl_xor(x2, d);
+        nanchk += __shfl_xor(nanchk, d);
+    }
+#pragma unroll
+    for (int k = 0; k < PB; k++) {
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) {
+            Q[k] += __shfl_xor(Q[k], d);
+            R[k] += __shfl_xor(R[k], d);
+        }
+    }
+    const bool bad = __builtin_isnan(nanchk) || __builtin_isnan(x2);
+
+    // ---- Gram of v = [d_t, x_{t-1}, d_{t-1}, .., d_{t-p+1}] over rows t = p .. T-1 ----
+    // index i -> (is_x, d lag): i = 1 is x_{t-1}; i = 0 is lag 0; i >= 2 is lag i - 1
+    const int np1 = p + 1;
+    const int npair = np1 * (np1 + 1) / 2;
+    for (int idx = lane; idx < npair; idx += 64) {
+        int i = 0, rem = idx;
+        while (rem >= np1 - i) { rem -= np1 - i; i++; }
+        const int j = i + rem;                 // i <= j
+        double g;
+        if (i == 1 && j == 1) {
+            g = x2;
+        } else if (i == 1 || j == 1) {         // x_{t-1} x d_{t-lam}
+            const int o = (i == 1) ? j : i;
+            const int lam = o == 0 ? 0 : o - 1;
+            double r = 0.0;
+#pragma unroll
+            for (int k = 0; k < PB; k++)
+                if (k == lam) r = R[k];
+            for (int64_t t = 1 + lam; t <= p - 1; t++) r -= X(t - 1) * D(t - lam);   // head rows
+            g = r;
+        } else {                               // d_{t-la} x d_{t-lb}
+            int la = i == 0 ? 0 : i - 1, lb = j == 0 ? 0 : j - 1;
+            if (la > lb) { const int tmp = la; la = lb; lb = tmp; }
+            const int k = lb - la;
+            double q = 0.0;
+#pragma unroll
+            for (int kk = 0; kk < PB; kk++)
+                if (kk == k) q = Q[kk];
+            for (int64_t u = 1 + k; u <= p - la - 1; u++) q -= D(u) * D(u - k);        // head
+            for (int64_t u = T - la; u <= T - 1; u++) q -= D(u) * D(u - k);             // tail
+            g = q;
+        }
+        G[i * kLd + j] = g;
+        G[j * kLd + i] = g;
+    }
+    __syncthreads();
+
+    // ---- Cholesky of the 1..p block (lane 0); rhs = row 0 ----
+    if (lane == 0) {
+        int status = STS_OK;
+        if (!bad) {
+            for (int j = 1; j <= p && status == STS_OK; j++) {
+                double d = G[j * kLd + j];
+                for (int k = 1; k < j; k++) d -= G[j * kLd + k] * G[j * kLd + k];
+                if (!(d > 0.0)) { status = STS_ERR_SINGULAR; break; }
+                const double l = __builtin_sqrt(d);
+                G[j * kLd + j] = l;
+                for (int i = j + 1; i <= p; i++) {
+                    double v = G[i * kLd + j];
+                    for (int k = 1; k < j; k++) v -= G[i * kLd + k] * G[j * kLd + k];
+                    G[i * kLd + j] = v / l;
+                }
+            }
+            if (status == STS_OK) {
+                for (int i = 1; i <= p; i++) sol[i] = G[0 * kLd + i];
+            }
+        }
+        stat = status;
+    }
+    __syncthreads();
+    auto solve_lane0 = [&](double* z) {
+        for (int i = 1; i <= p; i++) {
+            double v = z[i];
+            for (int k = 1; k < i; k++) v -= G[i * kLd + k] * z[k];
+            z[i] = v / G[i * kLd + i];
+        }
+        for (int i = p; i >= 1; i--) {
+            double v = z[i];
+            for (int k = i + 1; k <= p; k++) v -= G[k * kLd + i] * z[k];
+            z[i] = v / G[i * kLd + i];
+        }
+    };
+    const int status = stat;
+    const bool ok = !bad && status == STS_OK;
+    if (ok && lane == 0) solve_lane0(sol);
+    __syncthreads();
+
+    // ---- refinement: e_t = d_t - sum_i sol_i v_i(t); g_i = sum e_t v_i(t) ----
+    for (int it = 0; it < 2 && ok; it++) {
+        double g[PB + 1];
+#pragma unroll
+        for (int k = 0; k <= PB; k++) g[k] = 0.0;
+        for (int64_t t = p + lane; t < T; t += 64) {
+            const double xm = X(t - 1);
+            double e = D(t) - sol[1] * xm;
+#pragma unroll
+            for (int k = 1; k < PB; k++)
+                if (k < p) e -= sol[k + 1] * D(t - k);
+            g[1] = __builtin_fma(e, xm, g[1]);
+#pragma unroll
+            for (int k = 1; k < PB; k++)
+                if (k < p) g[k + 1] = __builtin_fma(e, D(t - k), g[k + 1]);
+        }
+#pragma unroll
+        for (int k = 1; k <= PB; k++) {
+            if (k <= p) {
+#pragma unroll
+                for (int d = 32; d >= 1; d >>= 1) g[k] += __shfl_xor(g[k], d);
+                if (lane == 0) zz[k] = g[k];
+            }
+        }
+        __syncthreads();
+        if (lane == 0) {
+            solve_lane0(zz);
+            for (int k = 1; k <= p; k++) sol[k] += zz[k];
+        }
+        __syncthreads();
+    }
+
+    // ---- back to the lag basis ----
+    if (lane == 0) {
+        double beta[kPMax + 1];
+        if (ok) {
+            // alpha = 1 + sol[1]; gamma_j = sol[j + 1] (j = 1 .. p-1)
+            if (p == 1) {
+                beta[1] = 1.0 + sol[1];
+            } else {
+                beta[1] = (1.0 + sol[1]) + sol[2];
+                for (int j = 2; j <= p - 1; j++) beta[j] = sol[j + 1] - sol[j];
+                beta[p] = -sol[p];
+            }
+        } else {
+            for (int j = 1; j <= p; j++) beta[j] = __builtin_nan("");
+        }
+        a.c[s] = ok ? 0.0 : __builtin_nan("");
+        for (int j = 1; j <= p; j++) {
+            a.coef[s * p + j - 1] = beta[j];
+            sol[j] = beta[j];
+        }
+        sol[0] = ok ? 0.0 : __builtin_nan("");
+        if (a.err) a.err[s] = bad ? STS_OK : status;
+    }
+    if (!a.out) return;
+    __syncthreads();
+
+    // ---- fused removeTimeDependentEffects (bit-exact order, c = 0) ----
+    const double c = sol[0];
+    double* dst = a.out + s * a.ld_out;
+    for (int64_t t = lane; t < T; t += 64) {
+        double d = X(t) - c;
+        for (int j = 0; j < p && t - j - 1 >= 0; j++) d -= X(t - j - 1) * sol[1 + j];
+        dst[t] = d;
+    }
+}
+
 }  // namespace
 
 #ifdef STS_STAMPS
@@ -589,6 +802,11 @@ extern "C" int sts_debug_ar_stamps(unsigned long long* out16) {
 hipError_t launch_ar_fit(const ArArgs& a, hipStream_t st) {
     if (a.S <= 0) return hipSuccess;
     if (a.p < 1 || a.p > kPMax) return hipErrorInvalidValue;
+    if (a.no_intercept) {   // difference-basis solve (see ar_fit_noint_kernel)
+        if (a.p <= 8) hipLaunchKernelGGL((ar_fit_noint_kernel<8>), dim3((unsigned)a.S), dim3(64), 0, st, a);
+        else hipLaunchKernelGGL((ar_fit_noint_kernel<kPMax>), dim3((unsigned)a.S), dim3(64), 0, st, a);
+        return hipGetLastError();
+    }
     // register path: p <= 8, T <= 64 * 40 (lane blocks of B steps, B in {8, 16, 24, 32, 40})
     if (a.p <= kRegPB && a.T <= 64 * 40 && !ab_knob("STS_AR_STAGED")) {
         dim3 g((unsigned)((a.S + kRegWaves - 1) / kRegWaves)), b(64 * kRegWaves);

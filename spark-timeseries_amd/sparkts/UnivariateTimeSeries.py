@@ -112,17 +112,28 @@ def differencesAtLag(ts, lag: int, destTs=None, startIndex=None):
         dest = p.t.clone() if p.device else p.t.copy()   # ts.copy (:363)
         dview = dest
         in_place_ptr = False
+        dld = (int(dview.stride(0)) if p.S > 1 else p.T) if p.device else p.T
     else:
-        dview = Panel(destTs, "destTs").t
+        dp = Panel(destTs, "destTs")
+        if dp.device != p.device or (dp.S, dp.T) != (p.S, p.T):
+            raise ValueError("differencesAtLag: destTs must be the same kind and shape as ts: (%d, %d) %s vs "
+                             "(%d, %d) %s" % (dp.S, dp.T, "device" if dp.device else "host", p.S, p.T,
+                                              "device" if p.device else "host"))
+        dview = p.t if destTs is ts else dp.t     # ts may have been made unit-stride: stay in place
         in_place_ptr = dview.data_ptr() == p.t.data_ptr() if p.device else dview.ctypes.data == p.t.ctypes.data
+        dld = dp.ld
         dest = dview
     if p.device:
         check(lib.sts_diff_at_lag(ptr(p.t), ptr(dview), p.S, p.T, p.ld,
-                                  p.ld if in_place_ptr else (dview.stride(0) if p.S > 1 else p.T),
+                                  p.ld if in_place_ptr else dld,
                                   lag, start, p.stream), "differencesAtLag")
     else:
         src = p.t
         check(lib.sts_diff_at_lag_host(ptr(src), ptr(dview), p.S, p.T, p.ld, lag, start), "differencesAtLag")
+    if destTs is not None and p.device and dview.data_ptr() != destTs.data_ptr():
+        # Panel made a unit-stride copy of a strided destTs: write the result back
+        destTs.copy_(dview[0] if dp.squeeze else dview)
+        return destTs
     if destTs is not None and not p.device and dview is not destTs:
         np.copyto(np.asarray(destTs).reshape(dview.shape), dview)
         return destTs

@@ -233,24 +233,60 @@ def exchange_instants(local, group=None):
     return torch.cat(blocks, dim=1), (t0, t1)
 
 
-def all_gather_results(local, group=None):
+class ResultGather:
+    """All-gather of per-series results (S_r, ...) of every partition into one (S, ...)
+    tensor in partition order -- the build's only collective (RCCL over xGMI on ROCm).
+
+    The partition sizes are static for a job, so they are exchanged ONCE here (one tiny
+    all-gather + host sync at construction); every later call is a single
+    all_gather_into_tensor into a buffer allocated once, with no size exchange and no
+    host synchronisation.  Equal partitions return that buffer itself (valid until the
+    next call; clone it to keep it); ragged ones are compacted with one precomputed
+    index_select into a fresh tensor."""
+
+    def __init__(self, n_local: int, row_shape=(), dtype=None, device=None, group=None):
+        import torch
+        import torch.distributed as dist
+        self.group = group
+        self.world = dist.get_world_size(group)
+        n = torch.tensor([int(n_local)], device=device, dtype=torch.int64)
+        sizes = [torch.zeros_like(n) for _ in range(self.world)]
+        dist.all_gather(sizes, n, group=group)
+        self.sizes = [int(x.item()) for x in sizes]
+        self.n_local = int(n_local)
+        self.m = max(self.sizes) if self.sizes else 0
+        self.row_shape = tuple(row_shape)
+        self.pad = torch.zeros((self.m,) + self.row_shape, dtype=dtype, device=device)
+        self.buf = torch.empty((self.world * self.m,) + self.row_shape, dtype=dtype, device=device)
+        self.uniform = all(s == self.m for s in self.sizes)
+        self.keep = None
+        if not self.uniform:
+            idx = [q * self.m + i for q, s in enumerate(self.sizes) for i in range(s)]
+            self.keep = torch.tensor(idx, dtype=torch.int64, device=device)
+
+    def __call__(self, local):
+        import torch.distributed as dist
+        if int(local.shape[0]) != self.n_local or tuple(local.shape[1:]) != self.row_shape:
+            raise ValueError("ResultGather: expected (%d,)+%s rows, got %s" % (self.n_local, self.row_shape,
+                                                                              tuple(local.shape)))
+        src = local
+        if self.n_local != self.m or not local.is_contiguous():
+            self.pad[: self.n_local] = local
+            src = self.pad
+        dist.all_gather_into_tensor(self.buf, src, group=self.group)
+        return self.buf if self.uniform else self.buf.index_select(0, self.keep)
+
+
+def all_gather_results(local, group=None, gather: Optional[ResultGather] = None):
     """All-gather per-series results of every partition (ragged S per rank allowed) into
-    one tensor in partition order -- the build's only collective (RCCL on ROCm)."""
-    import torch
+    one tensor in partition order.  Pass a ResultGather built once per job to keep the
+    size exchange out of a loop; without one, a one-shot gather is built for this call."""
     import torch.distributed as dist
     if not (dist.is_available() and dist.is_initialized()):
         return local
-    world = dist.get_world_size(group)
-    n = torch.tensor([local.shape[0]], device=local.device, dtype=torch.int64)
-    sizes = [torch.zeros_like(n) for _ in range(world)]
-    dist.all_gather(sizes, n, group=group)
-    sizes = [int(x.item()) for x in sizes]
-    m = max(sizes)
-    pad = local.new_zeros((m,) + tuple(local.shape[1:]))
-    pad[: local.shape[0]] = local
-    bufs = [torch.empty_like(pad) for _ in range(world)]
-    dist.all_gather(bufs, pad, group=group)
-    return torch.cat([b[:k] for b, k in zip(bufs, sizes)], dim=0)
+    if gather is None:
+        gather = ResultGather(local.shape[0], local.shape[1:], local.dtype, local.device, group)
+    return gather(local)
 
 
 def _is_uniform(index) -> bool:

@@ -13,7 +13,8 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from sparkts.timeseriesrdd import all_gather_results, all_reduce_nan_flags, exchange_instants, shard_range
+from sparkts.timeseriesrdd import (ResultGather, all_gather_results, all_reduce_nan_flags, exchange_instants,
+                                   shard_range)
 
 
 def test_shard_range_covers_keys_in_order():
@@ -43,6 +44,11 @@ def _worker(rank, world, port, n, q):
     # per-series "results" = global series index, 3 values each (like an S x K ACF block)
     local = torch.arange(a, b, dtype=torch.float64)[:, None].repeat(1, 3)
     got = all_gather_results(local)
+    # the per-job gather (sizes exchanged once) reused over steps, as bench.py does
+    gather = ResultGather(b - a, (3,), torch.float64, torch.device("cpu"))
+    for step in range(3):
+        again = all_gather_results(local + step, gather=gather)
+        assert again.tolist() == (got + step).tolist()
     q.put((rank, got.numpy().tolist()))
     dist.barrier()
     dist.destroy_process_group()

@@ -418,6 +418,29 @@ def test_diff_at_lag(torch, lag, start):
     assert_bits(host(xd), ref2, "in place")
 
 
+def test_diff_dest_checks(torch):
+    # destTs must match ts: a smaller dest is refused instead of overrun; a
+    # strided dest receives the result (the kernel writes a unit-stride copy, copied back)
+    from sparkts import UnivariateTimeSeries as uts
+    rng = np.random.default_rng(5)
+    x = rng.standard_normal((6, 300))
+    ref = np.array([oracle.differences_at_lag(r, 2) for r in x])
+    with pytest.raises(ValueError, match="same kind and shape"):
+        uts.differencesAtLag(dev(torch, x), 2, destTs=dev(torch, x[:5]))
+    wide = torch.zeros((6, 600), dtype=torch.float64, device="cuda:0")
+    dst = wide[:, ::2]                       # time stride 2
+    out = uts.differencesAtLag(dev(torch, x), 2, destTs=dst)
+    assert out is dst
+    assert_bits(host(dst.contiguous()), ref, "strided dest")
+    # strided ts updated in place (dest is ts)
+    xs = torch.zeros((6, 600), dtype=torch.float64, device="cuda:0")
+    xs[:, ::2] = dev(torch, x)
+    v = xs[:, ::2]
+    uts.differencesAtLag(v, 2, destTs=v)
+    ref2 = np.array([oracle.differences_at_lag(r, 2, start=2, inplace=True) for r in x])
+    assert_bits(host(xs[:, ::2].contiguous()), ref2, "strided in place")
+
+
 def test_diff_requirement(torch):
     from sparkts import UnivariateTimeSeries as uts
     from sparkts.errors import IllegalArgumentException
