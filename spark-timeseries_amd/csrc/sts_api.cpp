@@ -48,7 +48,13 @@ hipStream_t as_stream(void* s) { return s ? reinterpret_cast<hipStream_t>(s) : h
 
 std::once_flag g_pool_once[64];
 
+// validate-only mode (sts::validate_call): every entry point validates its arguments
+// before its first device action, ensure_device(), which then stops the call
+thread_local bool g_validate_only = false;
+constexpr int kValidated = -1000;
+
 int ensure_device() {
+    if (g_validate_only) return kValidated;
     int dev = 0;
     hipError_t e = hipGetDevice(&dev);
     if (e != hipSuccess) return hip_fail(e, "hipGetDevice");
@@ -272,6 +278,13 @@ int series_status(const int32_t* h, int64_t S, const char* what) {
 }
 
 int set_error(int status, const char* msg) { return fail(status, "%s", msg); }
+
+int validate_call(int (*fn)(void*), void* ctx) {
+    g_validate_only = true;
+    const int r = fn(ctx);
+    g_validate_only = false;
+    return r == kValidated ? STS_OK : r;
+}
 
 }  // namespace sts
 

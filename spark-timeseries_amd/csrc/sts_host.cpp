@@ -170,8 +170,16 @@ int staged(int64_t S, std::vector<Arg> args, const Kernel& kern) {
     Stager& g = g_stager;
     g.st_h2d_ms = g.st_kernel_ms = g.st_d2h_ms = g.st_wall_ms = 0;
     g.st_bytes_h2d = g.st_bytes_d2h = g.st_chunks = g.st_direct = 0;
-    if (S <= 0) return STS_OK;
     int r;
+    // the device entry point's own argument checks first, on the caller's shapes and host
+    // pointers (never dereferenced in validate-only mode): no staging on bad input
+    {
+        void* hp[16];
+        for (size_t k = 0; k < args.size() && k < 16; k++)
+            hp[k] = const_cast<void*>(args[k].src ? args[k].src : static_cast<const void*>(args[k].dst));
+        if ((r = sts::validate([&] { return kern(hp, 0, S, nullptr); }))) return r;
+    }
+    if (S <= 0) return STS_OK;
     if ((r = ensure_stager(g))) return r;
     size_t per_series = 0;
     for (Arg& x : args) {

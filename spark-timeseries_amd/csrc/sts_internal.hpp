@@ -62,6 +62,14 @@ inline const char* ab_knob(const char*) { return nullptr; }
 // err_per_series as the reference's exception; a status with a thread-local message
 int series_status(const int32_t* h, int64_t S, const char* what);
 int set_error(int status, const char* msg);
+// Run fn(ctx) -- a call of a device entry point -- in validate-only mode: the entry point
+// checks its arguments and returns their status, stopping at its first device action.
+// The `_host` entry points validate this way before staging anything.
+int validate_call(int (*fn)(void*), void* ctx);
+template <class F>
+int validate(F&& f) {
+    return validate_call([](void* c) { return (*static_cast<F*>(c))(); }, static_cast<void*>(&f));
+}
 
 // launchers (return hipError_t of the launch)
 hipError_t launch_tile(int method, int tw, const TileArgs& a, hipStream_t st);

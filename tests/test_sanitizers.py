@@ -1,0 +1,107 @@
+"""AddressSanitizer + UndefinedBehaviorSanitizer builds of the host code (SURVEY.md §5
+"Sanitizers"; CPU only -- GPU sanitizers are not available on the MI355X pool).
+
+* the CPU oracle (oracle/sts_oracle.c, sts_oracle_garch.c) driven over every restated
+  operator on edge shapes (tests/native/oracle_san_driver.c);
+* the device optimizer state machines compiled for the host (csrc/sts_ewma_opt.hpp,
+  csrc/sts_garch_opt.hpp through tests/native/*_sm_harness.cpp) on random, NaN, constant
+  and n = 1 series;
+* the C-ABI argument paths (csrc/sts_api.cpp, csrc/sts_host.cpp compiled for the host with
+  the sanitizers, device objects linked as built): every invalid argument returns its
+  documented status, valid calls fail cleanly without a device
+  (tests/native/host_args_san.cpp).
+
+Every build uses -fno-sanitize-recover=all, so any report fails the run.
+"""
+import os
+import shutil
+import subprocess
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+NATIVE = os.path.join(ROOT, "tests", "native")
+ORACLE = os.path.join(ROOT, "oracle")
+CSRC = os.path.join(ROOT, "spark-timeseries_amd", "csrc")
+SAN = ["-fsanitize=address,undefined", "-fno-sanitize-recover=all", "-g", "-O1"]
+ENV = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=0", UBSAN_OPTIONS="print_stacktrace=1")
+
+
+def need(tool):
+    path = shutil.which(tool) or (tool if os.path.exists(tool) else None)
+    if path is None:
+        pytest.skip("%s not available" % tool)
+    return path
+
+
+@pytest.fixture(scope="module")
+def oracle_objs(tmp_path_factory):
+    gcc = need("gcc")
+    d = tmp_path_factory.mktemp("san_oracle")
+    objs = []
+    for src in ("sts_oracle.c", "sts_oracle_garch.c"):
+        o = str(d / (src + ".o"))
+        subprocess.check_call([gcc, *SAN, "-std=c11", "-ffp-contract=off", "-fopenmp", "-fPIC",
+                               "-I", ORACLE, "-c", os.path.join(ORACLE, src), "-o", o])
+        objs.append(o)
+    return objs
+
+
+def test_oracle_under_asan_ubsan(oracle_objs, tmp_path):
+    gcc = need("gcc")
+    exe = str(tmp_path / "oracle_san")
+    subprocess.check_call([gcc, *SAN, "-std=c11", "-ffp-contract=off", "-fopenmp", "-I", ORACLE,
+                           os.path.join(NATIVE, "oracle_san_driver.c"), *oracle_objs, "-lm", "-o", exe])
+    r = subprocess.run([exe], capture_output=True, text=True, env=ENV, timeout=600)
+    assert r.returncode == 0 and r.stdout.strip() == "ok", r.stdout[-2000:] + r.stderr[-4000:]
+
+
+def _series_input(x):
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    return "%d %d\n" % x.shape + " ".join("%x" % v for v in x.view(np.uint64).ravel())
+
+
+@pytest.mark.parametrize("which", ["ewma", "garch"])
+def test_state_machines_under_asan_ubsan(oracle_objs, tmp_path, which):
+    gxx = need("g++")
+    exe = str(tmp_path / ("%s_sm_san" % which))
+    subprocess.check_call([gxx, *SAN, "-std=c++17", "-ffp-contract=off", "-fopenmp",
+                           "-I", os.path.join(ROOT, "include"), "-I", CSRC,
+                           os.path.join(NATIVE, "%s_sm_harness.cpp" % which), *oracle_objs, "-o", exe])
+    rng = np.random.default_rng(7)
+    T = 120
+    x = np.cumsum(rng.standard_normal((4, T)), axis=1)
+    x[1, 17] = np.nan                        # NaN: every evaluation NaN
+    x[2] = 2.5                               # constant
+    if which == "garch":
+        x = x - x[:, :1]
+    r = subprocess.run([exe], input=_series_input(x), capture_output=True, text=True, env=ENV, timeout=600)
+    assert r.returncode == 0, r.stderr[-4000:]
+    assert len(r.stdout.split("\n")) >= 4
+    one = subprocess.run([exe], input=_series_input(np.array([[0.3]])), capture_output=True, text=True, env=ENV,
+                         timeout=120)
+    assert one.returncode == 0, one.stderr[-4000:]
+
+
+def test_host_entry_points_under_asan_ubsan(tmp_path):
+    hipcc = need("/opt/rocm/bin/hipcc")
+    objdir = os.path.join(ROOT, "spark-timeseries_amd", "build", "obj")
+    dev_objs = sorted(os.path.join(objdir, f) for f in os.listdir(objdir) if f.endswith(".hip.o")) \
+        if os.path.isdir(objdir) else []
+    if not dev_objs:
+        pytest.skip("device objects not built (run __graft_entry__.build())")
+    flags = [*SAN, "-std=c++17", "-fPIC", "-fno-gpu-sanitize", "-I", os.path.join(ROOT, "include"), "-I", CSRC]
+    objs = []
+    for src in (os.path.join(CSRC, "sts_api.cpp"), os.path.join(CSRC, "sts_host.cpp"),
+                os.path.join(NATIVE, "host_args_san.cpp")):
+        o = str(tmp_path / (os.path.basename(src) + ".o"))
+        subprocess.check_call([hipcc, *flags, "-c", src, "-o", o])
+        objs.append(o)
+    exe = str(tmp_path / "host_args_san")
+    subprocess.check_call([hipcc, "-fsanitize=address,undefined", "-fno-gpu-sanitize", "--offload-arch=gfx950",
+                           *objs, *dev_objs, "-o", exe])
+    # the HIP runtime's own allocations at exit are not ours: leaks off for this binary
+    env = dict(ENV, ASAN_OPTIONS="detect_leaks=0", HIP_VISIBLE_DEVICES="")
+    r = subprocess.run([exe], capture_output=True, text=True, env=env, timeout=300)
+    assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stdout[-3000:] + r.stderr[-4000:]
