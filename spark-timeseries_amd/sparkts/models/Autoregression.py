@@ -93,11 +93,17 @@ class Autoregression:
         """The C4 mapSeries closure `series => ar(series, p).removeTimeDependentEffects(series)`
         (README.md:61) fused into one device pass: returns (model, residuals)."""
         p = Panel(ts)
-        if not p.device:
-            m = Autoregression.fitModel(ts, maxLag, noIntercept)
-            return m, m.removeTimeDependentEffects(ts)
-        import torch
         lib = _native.lib()
+        if not p.device:
+            out = p.empty()
+            c = np.empty((p.S,), dtype=np.float64)
+            coef = np.empty((p.S, maxLag), dtype=np.float64)
+            check(lib.sts_ar_fit_remove_host(ptr(p.t), ptr(out), p.S, p.T, p.ld, maxLag, int(noIntercept), ptr(c),
+                                             ptr(coef), None), "ar_fit_remove")
+            if p.squeeze:
+                return ARModel(float(c[0]), coef[0]), out[0]
+            return ARModel(c, coef), out
+        import torch
         out = p.empty()
         c = torch.empty((p.S,), dtype=torch.float64, device=p.t.device)
         coef = torch.empty((p.S, maxLag), dtype=torch.float64, device=p.t.device)

@@ -37,10 +37,13 @@ class TimeSeriesRDD:
 
     # --- S/TimeSeriesRDD.scala:188-199 ---
     def mapSeries(self, f: Callable, index=None) -> "TimeSeriesRDD":
-        """Apply f to every series.  f receives the whole (S, T) partition panel and must
-        be a batched operator (every function of UnivariateTimeSeries / models is), which
-        is how a Spark task's per-record closure becomes one kernel launch."""
-        out = f(self.data)
+        """Apply f to every series; keys (and their order) are unchanged.  A closure marked
+        `sparkts.pipelines.batched` (e.g. pipelines.ar_remove(p), the README.md:61 closure)
+        runs ONCE on the whole (S, T) partition panel -- one kernel launch; any other
+        closure runs per series as in the reference (correct for arbitrary code, one call
+        per series)."""
+        from .pipelines import apply_per_series, is_batched
+        out = f(self.data) if is_batched(f) else apply_per_series(f, self.data)
         return TimeSeriesRDD(self.index if index is None else index, self.keys, out)
 
     def autocorr(self, numLags: int):
