@@ -119,7 +119,9 @@ int sts_lag_matrix(const double* in, double* out, int64_t S, int64_t T, int64_t 
                    int max_lag, int include_original, void* stream);
 
 /* ---- a8: UnivariateTimeSeries.autocorr(ts, numLags) (S/UnivariateTimeSeries.scala:68-93).
- * acf[s*K + (i-1)] = lag-i sample autocorrelation, i = 1..K (K <= 63).  1e-10 relative. */
+ * acf[s*K + (i-1)] = lag-i sample autocorrelation, i = 1..K, any K >= 0 (lags >= T are NaN,
+ * as the reference's empty slices give).  K <= 63 runs fused in the imputation kernels, larger
+ * K in 61-lag MFMA blocks (sts_acf_wide.hip).  1e-10 relative. */
 int sts_autocorr(const double* in, int64_t S, int64_t T, int64_t ld, int K, double* acf,
                  void* stream);
 

@@ -91,10 +91,13 @@ __device__ __forceinline__ bool acf_mid(int64_t t, int64_t T) { return t >= kAcf
 // Slice 1 = x[i..T): head positions j >= i plus the whole tail; slice 2 = x[0..T-i): the
 // whole head plus tail positions T-1-j with j >= i.  Callers must run this with the same
 // operands in the same order to get the same bits (the fused and separate finalizes do).
+// The edge length E is kAcfEdge on the fused K <= 63 paths and K itself on the wide path
+// (sts_acf_wide.hip); T >= 2E, i <= E.
 template <class HY, class TZ>
-__device__ __forceinline__ double acf_combine(double Pi, double Sm, double Qm, int i, int64_t T, HY hy, TZ tz) {
+__device__ __forceinline__ double acf_combine_e(double Pi, double Sm, double Qm, int i, int64_t T, int E, HY hy,
+                                                TZ tz) {
     double sum1 = Sm, sq1 = Qm, sum2 = Sm, sq2 = Qm;
-    for (int j = 0; j < kAcfEdge; j++) {
+    for (int j = 0; j < E; j++) {
         const double y = hy(j), z = tz(j);
         const double yy = y * y, zz = z * z;
         sum2 += y;
@@ -113,6 +116,11 @@ __device__ __forceinline__ double acf_combine(double Pi, double Sm, double Qm, i
     const double v2 = sq2 - sum2 * sum2 / N;
     const double cv = Pi - sum1 * sum2 / N;
     return cv / (__builtin_sqrt(v1) * __builtin_sqrt(v2));   // S/UnivariateTimeSeries.scala:89
+}
+
+template <class HY, class TZ>
+__device__ __forceinline__ double acf_combine(double Pi, double Sm, double Qm, int i, int64_t T, HY hy, TZ tz) {
+    return acf_combine_e(Pi, Sm, Qm, i, T, kAcfEdge, hy, tz);
 }
 
 }  // namespace sts

@@ -381,7 +381,7 @@ int sts_fill_autocorr(const double* in, double* filled, int64_t S, int64_t T, in
     } else if (filled) {
         return fail(STS_ERR_BAD_ARG, "fill_autocorr: filled must be NULL for STS_FILL_NONE");
     }
-    if (K < 0 || K > 63) return fail(STS_ERR_BAD_ARG, "autocorr: numLags %d outside [0, 63]", K);
+    if (K < 0) return fail(STS_ERR_BAD_ARG, "autocorr: negative numLags %d", K);
     if (S > 0 && K > 0 && !acf) return fail(STS_ERR_BAD_ARG, "autocorr: null output");
     if ((r = ensure_device())) return r;
     hipStream_t st = as_stream(stream);
@@ -398,6 +398,28 @@ int sts_fill_autocorr(const double* in, double* filled, int64_t S, int64_t T, in
     if (K == 0) {
         if (method != STS_FILL_NONE && (r = run_tile(in, filled, nullptr, S, T, ld_in, ld_out, method, 0, nullptr, 0, 0,
                                                     es.dev, st, "fill"))) return r;
+        return es.finish("fill_autocorr");
+    }
+    if (K > sts::kFusedMaxLags) {
+        // any numLags (sts_acf_wide.hip): fill first (no ACF), then lag blocks of 61 on MFMA
+        const double* F = in;
+        int64_t ldF = ld_in;
+        if (method != STS_FILL_NONE) {
+            if ((r = run_tile(in, filled, nullptr, S, T, ld_in, ld_out, method, 0, nullptr, 0, 0, es.dev, st, "fill")))
+                return r;
+            F = filled;
+            ldF = ld_out;
+        } else {
+            HIP_TRY(hipMemsetAsync(es.dev, 0, (size_t)S * sizeof(int32_t), st), "hipMemsetAsync(err)");
+        }
+        Scratch sc(st);
+        const size_t np = sts::acf_wide_partials(S, T, K);
+        hipError_t e = sc.alloc(((size_t)S + np) * sizeof(double));
+        if (e != hipSuccess) return hip_fail(e, "hipMallocAsync(acf partials)");
+        double* shift = static_cast<double*>(sc.p);
+        HIP_TRY(sts::launch_acf_shift(F, S, T, ldF, shift, st), "acf shift");
+        HIP_TRY(timed(st, [&] { return sts::launch_acf_wide(F, S, T, ldF, shift, K, shift + S, acf, st); }),
+                "autocorr (wide)");
         return es.finish("fill_autocorr");
     }
     if ((r = run_tile(in, method == STS_FILL_NONE ? nullptr : filled, nullptr, S, T, ld_in, ld_out, method, K, acf, 0,

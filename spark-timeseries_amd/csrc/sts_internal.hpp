@@ -76,6 +76,12 @@ hipError_t launch_tile(int method, int tw, const TileArgs& a, hipStream_t st);
 hipError_t launch_acf_finalize(const FinalizeArgs& a, hipStream_t st);
 // per-series robust ACF shift (sts_acf.hpp) for the tile kernel
 hipError_t launch_acf_shift(const double* in, int64_t S, int64_t T, int64_t ld, double* shift, hipStream_t st);
+// numLags above the fused kernels' 63 (sts_acf_wide.hip): partial count for S x T x K, and the
+// lag-block MFMA pass + finalize on a filled panel F (shift: launch_acf_shift of F)
+constexpr int kFusedMaxLags = 63;
+size_t acf_wide_partials(int64_t S, int64_t T, int K);
+hipError_t launch_acf_wide(const double* F, int64_t S, int64_t T, int64_t ld, const double* shift, int K, double* part,
+                           double* acf, hipStream_t st);
 
 // Wave-private segment kernel (sts_seg.hip): tiles of kSegW steps, kSegTiles tiles per
 // wave.  TileArgs.tiles_per_series = ceil(T / kSegW), tiles_per_chunk = tiles per
