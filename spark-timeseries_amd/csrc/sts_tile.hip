@@ -51,6 +51,18 @@
 #define STS_LDS_BARRIER 1
 #endif
 
+#ifndef STS_DIAG
+#define STS_DIAG 0        // diagnostic builds only (tools/variant.sh): 1 = no MFMA, 2 = no LDS operand reads
+#endif
+
+#ifndef STS_TILE_WGS
+#define STS_TILE_WGS 3    // workgroups per CU the register budget is sized for
+#endif
+
+#ifndef STS_EARLY
+#define STS_EARLY 0       // A/B: 1 = fill-only tiles issue the next loads at tile start, 2 = all tiles
+#endif
+
 
 namespace sts {
 namespace {
@@ -171,7 +183,7 @@ __device__ __forceinline__ int px2_(int q2) { return PAD ? q2 + ((q2 >> 4) << 1)
 // every accumulator; TOEPLITZ (K = 61..63) uses NT = floor((K + 15) / 16) + 1 MFMAs with
 // U_t holding lag 16t + j - i.
 template <int TW, int NT, bool SHIFTED, int NTH>
-__global__ __launch_bounds__(NTH, 3) void tile_kernel(TileArgs a, int method) {
+__global__ __launch_bounds__(NTH, STS_TILE_WGS) void tile_kernel(TileArgs a, int method) {
     constexpr int kThreads = NTH;          // 256 (4 waves) or 128 (2 waves, TW = 2048)
     constexpr int kWaves = NTH / 64;
     static_assert(TW / 64 % kWaves == 0, "whole 64-step chunks per wave");
@@ -320,6 +332,13 @@ __global__ __launch_bounds__(NTH, 3) void tile_kernel(TileArgs a, int method) {
         STAMP(0);
         lds_barrier();
         STAMP(1);
+#if STS_EARLY
+        // A/B: the next tile's loads right after this tile's registers are in LDS
+        if constexpr (STS_EARLY == 2 || NT == 0) {
+            if (have_next) STS_ISSUE(k + 1);
+            else STS_CLEAR();
+        }
+#endif
 
         // positions to produce: [qA, qB) (E-relative); the ACF needs REACH steps past the tile
         const int qA = kHB;
@@ -429,8 +448,17 @@ __global__ __launch_bounds__(NTH, 3) void tile_kernel(TileArgs a, int method) {
                 sh_i[1] = next;
                 sh_i[2] = nnan;
                 sh_i[3] = lg ? 1 : 0;
-                sh_d[1] = (lext >= 0) ? src[lext] : 0.0;
-                sh_d[2] = (next < T) ? src[next] : 0.0;
+            }
+            // the global loads stay inside their (rare, wave-uniform) branches together with
+            // their use, so the vmcnt wait they need is not executed on the common path (it
+            // would also wait for every prefetch load in flight)
+            if (lext >= 0) {
+                const double v = src[lext];
+                if (lane == 0) sh_d[1] = v;
+            }
+            if (next < T) {
+                const double v = src[next];
+                if (lane == 0) sh_d[2] = v;
             }
         }
         STAMP(4);
@@ -631,8 +659,13 @@ __global__ __launch_bounds__(NTH, 3) void tile_kernel(TileArgs a, int method) {
             // the look-back range as y = 0
             if (SHIFTED && NT > 0 && e0 < 0 && tid < kHB / 2) v2[px2(tid)] = make_double2(0.0, 0.0);
         }
-        if (have_next) STS_ISSUE(k + 1);   // in flight during the MFMA phase of tile k
-        else STS_CLEAR();
+#if STS_EARLY
+        if constexpr (!(STS_EARLY == 2 || NT == 0))
+#endif
+        {
+            if (have_next) STS_ISSUE(k + 1);   // in flight during the MFMA phase of tile k
+            else STS_CLEAR();
+        }
         STAMP(8);
 
         if constexpr (NT > 0) {
@@ -703,12 +736,21 @@ __global__ __launch_bounds__(NTH, 3) void tile_kernel(TileArgs a, int method) {
                         double av[NT], bv[NT];
 #pragma unroll
                         for (int t = 0; t < NT; t++) {
+#if STS_DIAG == 2   // diagnostic only: no LDS operand reads
+                            av[t] = (double)(ia[t] + cc);
+                            bv[t] = (double)(ib[t] - cc);
+#else
                             av[t] = vals[ia[t] + 72 * cc];
                             bv[t] = vals[ib[t] + 72 * cc];
+#endif
                         }
 #pragma unroll
                         for (int t = 0; t < NT; t++)
+#if STS_DIAG == 1   // diagnostic only: no MFMA
+                            U[t % NA][t] += av[t] * bv[t];
+#else
                             U[t % NA] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[t], bv[t], U[t % NA], 0, 0, 0);
+#endif
                         acc_s += av[0];   // middle sums: VALU under the MFMA pipe
                         acc_q = __builtin_fma(av[0], av[0], acc_q);
                         __builtin_amdgcn_sched_barrier(0);   // one chunk's operands live at a time

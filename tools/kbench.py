@@ -36,7 +36,8 @@ def main():
     S, T = args.series, args.T
     x = torch.empty((S, T), dtype=torch.float64, device="cuda")
     out = torch.empty_like(x)
-    acf = torch.empty((S, 64), dtype=torch.float64, device="cuda")
+    kmax = max(64, max(int(c.split(":")[2]) for c in args.cases.split(",")))
+    acf = torch.empty((S, kmax), dtype=torch.float64, device="cuda")
     err = torch.zeros(S, dtype=torch.int32, device="cuda")
     sp = torch.cuda.current_stream().cuda_stream
     assert lib.sts_gen_panel(x.data_ptr(), 0, S, T, T, 3, args.nan, sp) == 0
