@@ -274,6 +274,9 @@ def main():
                     "traffic": measured_traffic(args.workload, S, T), "kernel": kernel,
                     "avg_kernel_ms": round(avg_ms, 4), "bytes_per_launch": bytes_per_launch,
                     "kernel_launches_timed": int(launches[0])}
+        fp = measured_fp64(args.workload, S, T, avg_ms)
+        if fp is not None:
+            roofline["fp64"] = fp
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.workload != "stage_c2":   # the CPU leg is an N = 1 report
@@ -381,6 +384,35 @@ def measured_traffic(workload, S, T):
     return rec.get("traffic_bytes_per_launch")
 
 
+FP64_PEAK_TFLOPS = 78.6   # MI355X_MICROARCH.md: dense FP64, vector and matrix alike
+
+
+def measured_fp64(workload, S, T, avg_ms):
+    """FP64 pipe use of the dominant kernel (north_star: "MFMA FP64 utilisation for AR
+    fitting"): per-launch counters from the committed rocprofv3 pass over this same workload
+    (profiles/<round>_<wl>_fp64.json, tools/collect.py), divided by THIS run's launch time."""
+    import glob
+    import re
+    if workload not in ("c3", "c4") or (S, T) != WORKLOADS[workload][:2]:
+        return None
+
+    def version(path):
+        return tuple(int(n) for n in re.findall(r"\d+", os.path.basename(path)))
+
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_%s_fp64.json" % workload)), key=version)
+    if not files:
+        return None
+    with open(files[-1]) as f:
+        rec = json.load(f)
+    sec = avg_ms * 1e-3
+    return {"source": os.path.basename(files[-1]),
+            "tflops": round(rec["fp64_flops_per_launch"] / sec / 1e12, 2),
+            "frac_of_fp64_peak": round(rec["fp64_flops_per_launch"] / sec / 1e12 / FP64_PEAK_TFLOPS, 4),
+            "mfma_tflops": round(rec["mfma_fp64_flops_per_launch"] / sec / 1e12, 2),
+            "valu_tflops": round(rec["valu_fp64_flops_per_launch"] / sec / 1e12, 2),
+            "mfma_pipe_busy_frac": round(rec["mfma_busy_frac"], 4), "peak_tflops": FP64_PEAK_TFLOPS}
+
+
 def cpu_threads():
     """Spark local[N] with N = the host cores this process may use: the CPU affinity set,
     capped by OMP_NUM_THREADS when the environment sets it (the GPU box grants each
@@ -461,6 +493,9 @@ def cpu_baseline(args, S, T, K, seed, nan_p, out, acf, p_ar, smooth=None, gpar_r
         s_next += n
     rate = done * T / elapsed if elapsed > 0 else None
     return {"value": rate, "unit": "series-elements/s", "cores": threads, "kind": "port",
+            "host_nproc": os.cpu_count(),
+            "cores_note": "threads = this process's CPU affinity capped by OMP_NUM_THREADS (the GPU box grants a "
+                          "single-GPU job 16 of its nproc cores); Spark local[N] with N = cores",
             "sample": "%d of the rank-0 series x %d steps (%.1f s of CPU work), oracle/sts_oracle.c restatement of "
                       "the reference loops, one series per thread (Spark local[%d] analogue); the JVM reference "
                       "cannot run here" % (done, T, elapsed, threads),

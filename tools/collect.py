@@ -22,13 +22,45 @@ PROF = os.path.join(ROOT, "profiles")
 KERNEL = "tile_kernel"
 
 
-def pmc_values(d, counter):
+def pmc_values(d, counter, kernel=KERNEL):
     vals = []
     for f in glob.glob(os.path.join(OUT, d, "*counter_collection.csv")):
         for r in csv.DictReader(open(f)):
-            if KERNEL in r["Kernel_Name"] and r["Counter_Name"] == counter:
+            if kernel in r["Kernel_Name"] and r["Counter_Name"] == counter:
                 vals.append(float(r["Counter_Value"]))
     return vals
+
+
+# FP64 pipe counters (tools/gpu_all.sh fp64_<wl>): one --pmc pass per workload
+FP64_COUNTERS = ["SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_ADD_F64",
+                 "SQ_INSTS_VALU_MFMA_MOPS_F64", "SQ_VALU_MFMA_BUSY_CYCLES", "GRBM_GUI_ACTIVE"]
+FP64_KERNELS = {"c3": "tile_kernel", "c4": "ar_fit_blk_kernel"}
+
+
+def collect_fp64(tag, wl):
+    """Per-launch FP64 work of the dominant kernel: flops = (2 FMA + ADD + MUL) x 64 lanes +
+    MFMA_MOPS x 512 (rocprofiler-sdk TOTAL_64_OPS), the MFMA pipe's busy cycles summed over
+    the 1024 SIMDs, and GRBM_GUI_ACTIVE (summed over the 8 XCDs).  bench.py divides by its own
+    launch time for the utilisation figures."""
+    d = "pmc_fp64_%s" % wl
+    vals = {c: pmc_values(d, c, FP64_KERNELS[wl]) for c in FP64_COUNTERS}
+    if not all(vals.values()):
+        return None
+    per = {c: sum(v) / len(v) for c, v in vals.items()}
+    flops = (2 * per["SQ_INSTS_VALU_FMA_F64"] + per["SQ_INSTS_VALU_ADD_F64"] + per["SQ_INSTS_VALU_MUL_F64"]) * 64 \
+        + per["SQ_INSTS_VALU_MFMA_MOPS_F64"] * 512
+    rec = {"kernel": FP64_KERNELS[wl], "workload": "%s (bench.py), --steps 2 --warmup 0" % wl,
+           "launches": len(vals["GRBM_GUI_ACTIVE"]), "counters_per_launch": per,
+           "fp64_flops_per_launch": flops,
+           "valu_fp64_flops_per_launch": flops - per["SQ_INSTS_VALU_MFMA_MOPS_F64"] * 512,
+           "mfma_fp64_flops_per_launch": per["SQ_INSTS_VALU_MFMA_MOPS_F64"] * 512,
+           "mfma_busy_frac": per["SQ_VALU_MFMA_BUSY_CYCLES"] / (1024.0 * per["GRBM_GUI_ACTIVE"] / 8.0),
+           "effective_clock_note": "GRBM_GUI_ACTIVE / 8 = cycles per XCD over the launch",
+           "formula": "TOTAL_64_OPS = (2 FMA_F64 + ADD_F64 + MUL_F64) x 64 + MFMA_MOPS_F64 x 512"}
+    with open(os.path.join(PROF, "%s_%s_fp64.json" % (tag, wl)), "w") as f:
+        json.dump(rec, f, indent=1)
+    print(json.dumps(rec))
+    return rec
 
 
 def main():
@@ -55,6 +87,8 @@ def main():
         with open(os.path.join(PROF, "%s_c3_traffic.json" % tag), "w") as f:
             json.dump(rec, f, indent=1)
         print(json.dumps(rec))
+    for wl in FP64_KERNELS:
+        collect_fp64(tag, wl)
 
 
 if __name__ == "__main__":
