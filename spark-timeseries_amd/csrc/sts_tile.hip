@@ -39,10 +39,6 @@
 
 #include <type_traits>
 
-#ifndef STS_MFMA_PIPE
-#define STS_MFMA_PIPE 0   // experiment knob: software-pipelined MFMA operand loads
-#endif
-
 #ifndef STS_MFMA_UNROLL
 #define STS_MFMA_UNROLL 1 // fully unrolled full-range MFMA phase (A/B: ~1.5 % faster)
 #endif
@@ -53,6 +49,10 @@
 
 #ifndef STS_DIAG
 #define STS_DIAG 0        // diagnostic builds only (tools/variant.sh): 1 = no MFMA, 2 = no LDS operand reads
+#endif
+
+#ifndef STS_TILE_DB
+#define STS_TILE_DB 0     // K <= 60: double-buffered tiles, lag products interleaved into the next tile
 #endif
 
 #ifndef STS_TILE_WGS
@@ -182,8 +182,8 @@ __device__ __forceinline__ int px2_(int q2) { return PAD ? q2 + ((q2 >> 4) << 1)
 // + j%q -- every lag 0 .. 16 NT - q exactly once per step, and the same lag map h(j) - i in
 // every accumulator; TOEPLITZ (K = 61..63) uses NT = floor((K + 15) / 16) + 1 MFMAs with
 // U_t holding lag 16t + j - i.
-template <int TW, int NT, bool SHIFTED, int NTH>
-__global__ __launch_bounds__(NTH, STS_TILE_WGS) void tile_kernel(TileArgs a, int method) {
+template <int TW, int NT, bool SHIFTED, int NTH, bool DB = false>
+__global__ __launch_bounds__(NTH, DB ? 2 : STS_TILE_WGS) void tile_kernel(TileArgs a, int method) {
     constexpr int kThreads = NTH;          // 256 (4 waves) or 128 (2 waves, TW = 2048)
     constexpr int kWaves = NTH / 64;
     static_assert(TW / 64 % kWaves == 0, "whole 64-step chunks per wave");
@@ -202,7 +202,10 @@ __global__ __launch_bounds__(NTH, STS_TILE_WGS) void tile_kernel(TileArgs a, int
     constexpr int RPT = (NP2 + kThreads - 1) / kThreads;     // prefetch registers per thread
     static_assert(EW % 64 == 0, "extended tile must be whole words");
     static_assert(NW <= 128, "word scan handles at most 128 words");
-    __shared__ __attribute__((aligned(16))) double vals[EWP];   // padded (px) for the shifted scheme
+    // padded (px) for the shifted scheme; DB: two tile buffers, tile k in buffer k & 1, so tile
+    // k's lag products can run during tile k + 1's phases
+    __shared__ __attribute__((aligned(16))) double vals_mem[(DB ? 2 : 1) * EWP];
+    double* vals = vals_mem;
     __shared__ unsigned long long mask[NW];
     __shared__ int lastUpTo[NW];           // last valid E-position in words <= w (-1: none)
     __shared__ int firstFrom[NW];          // first valid E-position in words >= w (kBig: none)
@@ -297,7 +300,128 @@ __global__ __launch_bounds__(NTH, STS_TILE_WGS) void tile_kernel(TileArgs a, int
     // ACF shift (sts_acf.hpp: median of 64 raw samples of the series), computed once per
     // series by acf_shift_kernel before this launch: a scalar load
     const double c0 = (NT > 0) ? a.shift[s] : 0.0;
+
+    // ---- lag products on MFMA (§ header) for chunks [FROM, TO) of this wave's CPW chunks of a
+    //      tile whose y sits in buffer vb; chunk order (and so the accumulation order) is the
+    //      same however the range is split into groups ----
+    constexpr int qA0 = kHB;                // E-position of the tile's first step
+    constexpr int NTA = NT > 0 ? NT : 1;    // array extent (NT = 0 instantiates no MFMA code)
+    constexpr int CPW = TW / 64 / kWaves;   // 64-step chunks per wave
+    constexpr int kG1 = (CPW * 3) / 8, kG2 = (CPW * 5) / 8;   // DB group boundaries
+    auto mid_sums = [&](int p, double y) {
+        // sum y / sum y^2 over the series' middle (sts_acf.hpp rule 2): lane l of the chunk
+        // at series position p holds y(p + l)
+        const double z = acf_mid(p + lane, T) ? y : 0.0;
+        acc_s += z;
+        acc_q = __builtin_fma(z, z, acc_q);
+    };
+    auto mfma_group = [&](auto FROM, auto TO, const double* vb, int64_t kk, int tt0, int tt1) {
+        constexpr int F = decltype(FROM)::value, TE = decltype(TO)::value;
+        if constexpr (NT > 0 && F < TE) {
+            // a tile wholly inside the middle takes the unrolled loop with plain sums; the
+            // series' first and last tiles take the per-chunk loop with the per-lane test
+            const bool tile_mid = tt0 >= kAcfEdge && tt1 + kAcfEdge <= T;
+            const int tlen = tt1 - tt0;
+            const int nch = (tlen + 63) / 64;
+            const bool full = wave * CPW + CPW <= nch;
+            int c = wave * CPW + F;
+            int cend = wave * CPW + TE;
+            if (cend > nch) cend = nch;
+            if constexpr (SHIFTED) {
+                // A = y(chunk + QS t + lane), B = y(chunk + QS t + 16 (lane >> 4) + h(lane & 15));
+                // per-lane operand offsets (padded) relative to a chunk start
+                int oa[NTA], ob[NTA];
+#pragma unroll
+                for (int t = 0; t < NT; t++) {
+                    const int j = lane & 15;
+                    const int ra = QS * t + lane;
+                    const int rb = QS * t + 16 * (lane >> 4) + 16 * (j / QS) + (16 - QS) + (j % QS);
+                    oa[t] = px(ra);
+                    ob[t] = px(rb);
+                }
+                auto chunk_mfma = [&](const double* yb) {
+                    double av[NTA], bv[NTA];
+#pragma unroll
+                    for (int t = 0; t < NT; t++) {
+                        av[t] = yb[oa[t]];
+                        bv[t] = yb[ob[t]];
+                    }
+#pragma unroll
+                    for (int t = 0; t < NT; t++)
+                        U[t % NA] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[t], bv[t], U[t % NA], 0, 0, 0);
+                    return av[0];   // y at chunk position lane
+                };
+                // wave 0 of the first tile also runs chunk -1 (the look-back, y = 0), whose
+                // shifted windows hold the series' first QS t steps
+                if (F == 0 && kk == 0 && wave == 0) chunk_mfma(vb);   // y = 0 there: no middle-sum term
+#if STS_MFMA_UNROLL
+                if (full && tile_mid) {
+                    // full chunk range, unrolled: per-lane LDS indices made opaque once per
+                    // group (else LICM hoists all of them out of the tile loop and spills),
+                    // chunk offsets (72 doubles per padded chunk) fold into the ds_read
+                    // immediates
+                    int ia[NTA], ib[NTA];
+                    const int cb = px(qA0 + 64 * (wave * CPW));
+#pragma unroll
+                    for (int t = 0; t < NT; t++) {
+                        ia[t] = cb + oa[t];
+                        ib[t] = cb + ob[t];
+                        asm volatile("" : "+v"(ia[t]), "+v"(ib[t]));
+                    }
+#pragma unroll
+                    for (int cc = F; cc < TE; cc++) {
+                        double av[NTA], bv[NTA];
+#pragma unroll
+                        for (int t = 0; t < NT; t++) {
+#if STS_DIAG == 2   // diagnostic only: no LDS operand reads
+                            av[t] = (double)(ia[t] + cc);
+                            bv[t] = (double)(ib[t] - cc);
+#else
+                            av[t] = vb[ia[t] + 72 * cc];
+                            bv[t] = vb[ib[t] + 72 * cc];
+#endif
+                        }
+#pragma unroll
+                        for (int t = 0; t < NT; t++)
+#if STS_DIAG == 1   // diagnostic only: no MFMA
+                            U[t % NA][t] += av[t] * bv[t];
+#else
+                            U[t % NA] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[t], bv[t], U[t % NA], 0, 0, 0);
+#endif
+                        acc_s += av[0];   // middle sums: VALU under the MFMA pipe
+                        acc_q = __builtin_fma(av[0], av[0], acc_q);
+                        __builtin_amdgcn_sched_barrier(0);   // one chunk's operands live at a time
+                    }
+                    c = cend;
+                }
+#endif
+                for (; c < cend; c++) mid_sums(tt0 + 64 * c, chunk_mfma(vb + px(qA0 + 64 * c)));   // chunk start: a multiple of 32
+            } else {
+                // U_t += y(j0 + l) x y(j0 + 16t + l)
+                for (; c < cend; c++) {
+                    const int jrel = 64 * c + lane;
+                    double bv[NTA];
+#pragma unroll
+                    for (int t = 0; t < NT; t++) bv[t] = vb[px(qA0 + jrel + 16 * t)];
+                    const double av = (jrel < tlen) ? bv[0] : 0.0;   // A only inside the tile
+#pragma unroll
+                    for (int t = 0; t < NT; t++) U[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv[t], U[t], 0, 0, 0);
+                    mid_sums(tt0 + 64 * c, av);
+                }
+            }
+        }
+    };
+    // DB: the previous tile, whose lag products run in groups inside this tile's phases
+    const double* prev_vals = vals_mem;
+    int64_t prev_k = -1;
+    int prev_t0 = 0, prev_t1 = 0;
     for (int64_t k = k_begin; k < k_end; k++) {
+        if constexpr (DB) vals = vals_mem + (k & 1) * EWP;
+        if constexpr (DB && NT > 0) {
+            // group 1: under the wait for this tile's prefetched registers
+            if (prev_k >= 0) mfma_group(std::integral_constant<int, 0>{}, std::integral_constant<int, kG1>{},
+                                        prev_vals, prev_k, prev_t0, prev_t1);
+        }
         const int t0 = (int)(k * TW);
         const int t1 = (t0 + TW < T) ? t0 + TW : (int)T;
         const int e0 = t0 - kHB;
@@ -460,6 +584,11 @@ __global__ __launch_bounds__(NTH, STS_TILE_WGS) void tile_kernel(TileArgs a, int
                 const double v = src[next];
                 if (lane == 0) sh_d[2] = v;
             }
+        }
+        if constexpr (DB && NT > 0) {
+            // group 2: waves 1-3 wait here for wave 0's scan anyway
+            if (prev_k >= 0) mfma_group(std::integral_constant<int, kG1>{}, std::integral_constant<int, kG2>{},
+                                        prev_vals, prev_k, prev_t0, prev_t1);
         }
         STAMP(4);
         lds_barrier();
@@ -669,145 +798,34 @@ __global__ __launch_bounds__(NTH, STS_TILE_WGS) void tile_kernel(TileArgs a, int
         STAMP(8);
 
         if constexpr (NT > 0) {
-            lds_barrier();
-            STAMP(9);
-            // ---- 6. lag products on MFMA ----
-            constexpr int CPW = TW / 64 / kWaves;   // 64-step chunks per wave
-            // sum y / sum y^2 over the series' middle (sts_acf.hpp rule 2): lane l of the chunk
-            // at series position p holds y(p + l)
-            auto mid_sums = [&](int p, double y) {
-                const double z = acf_mid(p + lane, T) ? y : 0.0;
-                acc_s += z;
-                acc_q = __builtin_fma(z, z, acc_q);
-            };
-            // a tile wholly inside the middle takes the unrolled loop with plain sums; the
-            // series' first and last tiles take the per-chunk loop with the per-lane test
-            const bool tile_mid = t0 >= kAcfEdge && t1 + kAcfEdge <= T;
-            const int tlen = t1 - t0;
-            const int nch = (tlen + 63) / 64;
-            int c = wave * CPW;
-            int cend = c + CPW;
-            if (cend > nch) cend = nch;
-            if constexpr (SHIFTED) {
-                // A = y(chunk + QS t + lane), B = y(chunk + QS t + 16 (lane >> 4) + h(lane & 15));
-                // wave 0 of the first tile also runs chunk -1 (the look-back, y = 0), whose
-                // shifted windows hold the series' first QS t steps
-                // per-lane operand offsets (padded) relative to a chunk start
-                int oa[NT], ob[NT];
-#pragma unroll
-                for (int t = 0; t < NT; t++) {
-                    const int j = lane & 15;
-                    const int ra = QS * t + lane;
-                    const int rb = QS * t + 16 * (lane >> 4) + 16 * (j / QS) + (16 - QS) + (j % QS);
-                    oa[t] = px(ra);
-                    ob[t] = px(rb);
-                }
-                auto chunk_mfma = [&](const double* yb) {
-                    double av[NT], bv[NT];
-#pragma unroll
-                    for (int t = 0; t < NT; t++) {
-                        av[t] = yb[oa[t]];
-                        bv[t] = yb[ob[t]];
-                    }
-#pragma unroll
-                    for (int t = 0; t < NT; t++)
-                        U[t % NA] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[t], bv[t], U[t % NA], 0, 0, 0);
-                    return av[0];   // y at chunk position lane
-                };
-                // wave 0 of the first tile also runs chunk -1 (the look-back, y = 0), whose
-                // shifted windows hold the series' first QS t steps
-                if (k == 0 && wave == 0) chunk_mfma(vals);   // y = 0 there: no middle-sum term
-#if STS_MFMA_UNROLL
-                if (cend - c == CPW && tile_mid) {
-                    // full chunk range, unrolled: per-lane LDS indices made opaque once per
-                    // tile (else LICM hoists all 16 x 2NT of them out of the tile loop and
-                    // spills), chunk offsets (72 doubles per padded chunk) fold into the
-                    // ds_read immediates
-                    int ia[NT], ib[NT];
-                    const int cb = px(qA + 64 * c);
-#pragma unroll
-                    for (int t = 0; t < NT; t++) {
-                        ia[t] = cb + oa[t];
-                        ib[t] = cb + ob[t];
-                        asm volatile("" : "+v"(ia[t]), "+v"(ib[t]));
-                    }
-#pragma unroll
-                    for (int cc = 0; cc < CPW; cc++) {
-                        double av[NT], bv[NT];
-#pragma unroll
-                        for (int t = 0; t < NT; t++) {
-#if STS_DIAG == 2   // diagnostic only: no LDS operand reads
-                            av[t] = (double)(ia[t] + cc);
-                            bv[t] = (double)(ib[t] - cc);
-#else
-                            av[t] = vals[ia[t] + 72 * cc];
-                            bv[t] = vals[ib[t] + 72 * cc];
-#endif
-                        }
-#pragma unroll
-                        for (int t = 0; t < NT; t++)
-#if STS_DIAG == 1   // diagnostic only: no MFMA
-                            U[t % NA][t] += av[t] * bv[t];
-#else
-                            U[t % NA] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[t], bv[t], U[t % NA], 0, 0, 0);
-#endif
-                        acc_s += av[0];   // middle sums: VALU under the MFMA pipe
-                        acc_q = __builtin_fma(av[0], av[0], acc_q);
-                        __builtin_amdgcn_sched_barrier(0);   // one chunk's operands live at a time
-                    }
-                    c = cend;
-                }
-#endif
-#if STS_MFMA_PIPE
-                // software pipeline: chunk c + 1's operands load while chunk c's MFMAs run
-                if (c < cend) {
-                    double av[NT], bv[NT];
-                    const double* yb = vals + px(qA + 64 * c);
-#pragma unroll
-                    for (int t = 0; t < NT; t++) {
-                        av[t] = yb[oa[t]];
-                        bv[t] = yb[ob[t]];
-                    }
-                    for (; c < cend; c++) {
-                        double an[NT], bn[NT];
-                        const double* yn = vals + px(qA + 64 * (c + 1 < cend ? c + 1 : c));
-#pragma unroll
-                        for (int t = 0; t < NT; t++) {
-                            an[t] = yn[oa[t]];
-                            bn[t] = yn[ob[t]];
-                        }
-#pragma unroll
-                        for (int t = 0; t < NT; t++)
-                            U[t % NA] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[t], bv[t], U[t % NA], 0, 0, 0);
-#pragma unroll
-                        for (int t = 0; t < NT; t++) {
-                            av[t] = an[t];
-                            bv[t] = bn[t];
-                        }
-                    }
-                }
-#else
-                for (; c < cend; c++) mid_sums(t0 + 64 * c, chunk_mfma(vals + px(qA + 64 * c)));   // chunk start: a multiple of 32
-#endif
+            if constexpr (DB) {
+                // group 3 of the previous tile, then the barrier that publishes this tile's y
+                if (prev_k >= 0) mfma_group(std::integral_constant<int, kG2>{}, std::integral_constant<int, CPW>{},
+                                            prev_vals, prev_k, prev_t0, prev_t1);
+                lds_barrier();
+                STAMP(9);
+                prev_vals = vals;
+                prev_k = k;
+                prev_t0 = t0;
+                prev_t1 = t1;
             } else {
-                // U_t += y(j0 + l) x y(j0 + 16t + l)
-                for (; c < cend; c++) {
-                    const int jrel = 64 * c + lane;
-                    double bv[NT];
-#pragma unroll
-                    for (int t = 0; t < NT; t++) bv[t] = vals[px(qA + jrel + 16 * t)];
-                    const double av = (jrel < tlen) ? bv[0] : 0.0;   // A only inside the tile
-#pragma unroll
-                    for (int t = 0; t < NT; t++) U[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv[t], U[t], 0, 0, 0);
-                    mid_sums(t0 + 64 * c, av);
-                }
+                lds_barrier();
+                STAMP(9);
+                // ---- 6. lag products on MFMA ----
+                mfma_group(std::integral_constant<int, 0>{}, std::integral_constant<int, CPW>{}, vals, k, t0, t1);
             }
         }
         have = have_next;
         STAMP(10);
-        lds_barrier();   // vals / mask / lists are reused by the next tile
+        if constexpr (!(DB && NT > 0)) lds_barrier();   // vals / mask / lists are reused by the next tile
         STAMP(11);
     }
+    if constexpr (DB && NT > 0) {
+        if (prev_k >= 0) mfma_group(std::integral_constant<int, 0>{}, std::integral_constant<int, CPW>{}, prev_vals,
+                                    prev_k, prev_t0, prev_t1);
+        lds_barrier();   // the finalize below reuses the buffers as scratch
+    }
+    vals = vals_mem;
 #undef STS_ISSUE
 #undef STS_LD1
 #undef STS_ST1
@@ -965,8 +983,8 @@ hipError_t launch_tile(int method, int tw, const TileArgs& a, hipStream_t st) {
 #endif
     } else if (tw == 4096) {
         if (a.K == 0) hipLaunchKernelGGL((tile_kernel<4096, 0, false, kThreads>), grid, block, 0, st, a, method);
-        else if (a.K <= 24) hipLaunchKernelGGL((tile_kernel<4096, 2, true, kThreads>), grid, block, 0, st, a, method);
-        else if (a.K <= 60) hipLaunchKernelGGL((tile_kernel<4096, 4, true, kThreads>), grid, block, 0, st, a, method);
+        else if (a.K <= 24) hipLaunchKernelGGL((tile_kernel<4096, 2, true, kThreads, STS_TILE_DB>), grid, block, 0, st, a, method);
+        else if (a.K <= 60) hipLaunchKernelGGL((tile_kernel<4096, 4, true, kThreads, STS_TILE_DB>), grid, block, 0, st, a, method);
         else if (a.K <= 63) hipLaunchKernelGGL((tile_kernel<4096, 5, false, kThreads>), grid, block, 0, st, a, method);
         else return hipErrorInvalidValue;
     } else {
