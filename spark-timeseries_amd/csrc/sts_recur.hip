@@ -19,6 +19,10 @@
 
 #include <hip/hip_runtime.h>
 
+#ifndef STS_RECUR_V2
+#define STS_RECUR_V2 1   // 16-B global accesses in the C2 recurrence kernel (A/B: 1.673 vs 1.687 ms on C2)
+#endif
+
 namespace sts {
 namespace {
 
@@ -27,12 +31,15 @@ namespace {
 // contiguous bytes); lanes < SPW then run their series' recurrence over the chunk.
 // Longer row segments (fewer series, longer chunks) keep HBM pages open: C2's 1M series
 // x 390 steps are only 3 KB each.
-template <int OP, int H, int SPW = 64, int CH = 32>
+template <int OP, int H, int SPW = 64, int CH = 32, bool V2 = false>
 __global__ __launch_bounds__(64) void recur_kernel(RecurArgs a) {
-    constexpr int kRow = CH + 1;
-    constexpr int NLD = SPW * CH / 64;            // load instructions per chunk per lane
-    static_assert(SPW * CH % 64 == 0 && (CH % 64 == 0 || 64 % CH == 0), "chunk shape");
-    __shared__ double tile[SPW * kRow];
+    // V2: 16-B loads / stores (two consecutive steps per lane, half the memory instructions);
+    // rows padded to an even stride so the 16-B LDS accesses stay aligned
+    constexpr int kRow = V2 ? CH + 2 : CH + 1;
+    constexpr int EPL = V2 ? 2 : 1;               // elements per lane per instruction
+    constexpr int NLD = SPW * CH / (64 * EPL);    // load instructions per chunk per lane
+    static_assert(SPW * CH % (64 * EPL) == 0 && (CH % 64 == 0 || 64 % CH == 0), "chunk shape");
+    __shared__ __attribute__((aligned(16))) double tile[SPW * kRow];
     const int lane = threadIdx.x;
     const int64_t s0 = (int64_t)blockIdx.x * SPW;
     const int64_t sl = s0 + lane;                 // this lane's series (lanes < SPW)
@@ -64,14 +71,25 @@ __global__ __launch_bounds__(64) void recur_kernel(RecurArgs a) {
     double e = 0.0;                                // EWMA state
     double carry = __builtin_nan("");              // fillPrevious carry
 
-    // load instruction i of a chunk: row (i * 64 + lane) / CH, column (i * 64 + lane) % CH
-    double pre[NLD];
+    // load instruction i of a chunk: element e = (i * 64 + lane) * EPL, row e / CH, column e % CH
+    double2 pre[NLD];
     auto fetch = [&](int64_t tc) {
         const int len = (T - tc < CH) ? (int)(T - tc) : CH;
 #pragma unroll
         for (int i = 0; i < NLD; i++) {
-            const int row = (i * 64 + lane) / CH, col = (i * 64 + lane) % CH;
-            pre[i] = (row < ns && col < len) ? a.in[(s0 + row) * a.ld_in + tc + col] : 0.0;
+            const int e = (i * 64 + lane) * EPL;
+            const int row = e / CH, col = e % CH;
+            const double* src = a.in + (s0 + row) * a.ld_in + tc + col;
+            if (V2) {
+                if (row < ns && col + 1 < len) {
+                    pre[i] = *reinterpret_cast<const double2*>(src);
+                } else {
+                    pre[i].x = (row < ns && col < len) ? src[0] : 0.0;
+                    pre[i].y = 0.0;
+                }
+            } else {
+                pre[i].x = (row < ns && col < len) ? src[0] : 0.0;
+            }
         }
     };
     fetch(0);
@@ -79,8 +97,13 @@ __global__ __launch_bounds__(64) void recur_kernel(RecurArgs a) {
         const int len = (T - tc < CH) ? (int)(T - tc) : CH;
 #pragma unroll
         for (int i = 0; i < NLD; i++) {
-            const int row = (i * 64 + lane) / CH, col = (i * 64 + lane) % CH;
-            if (row < ns && col < len) tile[row * kRow + col] = pre[i];
+            const int e = (i * 64 + lane) * EPL;
+            const int row = e / CH, col = e % CH;
+            if (V2) {
+                if (row < ns && col < len) *reinterpret_cast<double2*>(&tile[row * kRow + col]) = pre[i];
+            } else {
+                if (row < ns && col < len) tile[row * kRow + col] = pre[i].x;
+            }
         }
         if (tc + CH < T) fetch(tc + CH);   // next chunk in flight during this one
         __syncthreads();
@@ -139,8 +162,15 @@ __global__ __launch_bounds__(64) void recur_kernel(RecurArgs a) {
         __syncthreads();
 #pragma unroll
         for (int i = 0; i < NLD; i++) {
-            const int row = (i * 64 + lane) / CH, col = (i * 64 + lane) % CH;
-            if (row < ns && col < len) a.out[(s0 + row) * a.ld_out + tc + col] = tile[row * kRow + col];
+            const int e = (i * 64 + lane) * EPL;
+            const int row = e / CH, col = e % CH;
+            double* d = a.out + (s0 + row) * a.ld_out + tc + col;
+            if (V2) {
+                if (row < ns && col + 1 < len) *reinterpret_cast<double2*>(d) = *reinterpret_cast<const double2*>(&tile[row * kRow + col]);
+                else if (row < ns && col < len) d[0] = tile[row * kRow + col];
+            } else {
+                if (row < ns && col < len) d[0] = tile[row * kRow + col];
+            }
         }
         __syncthreads();
     }
@@ -216,10 +246,18 @@ hipError_t launch_recur(RecurOp op, const RecurArgs& a, hipStream_t st) {
 #endif
         if (a.lag <= 8) {   // C2 shape: 32 series x 64-step chunks per wave (A/B: r01 notes)
             dim3 g((unsigned)((a.S + STS_FDE_SPW - 1) / STS_FDE_SPW)), b(64);
-            if (a.lag <= 1) hipLaunchKernelGGL((recur_kernel<kFillDiffEwma, 1, STS_FDE_SPW, STS_FDE_CH>), g, b, 0, st, a);
-            else if (a.lag <= 2) hipLaunchKernelGGL((recur_kernel<kFillDiffEwma, 2, STS_FDE_SPW, STS_FDE_CH>), g, b, 0, st, a);
-            else if (a.lag <= 4) hipLaunchKernelGGL((recur_kernel<kFillDiffEwma, 4, STS_FDE_SPW, STS_FDE_CH>), g, b, 0, st, a);
-            else hipLaunchKernelGGL((recur_kernel<kFillDiffEwma, 8, STS_FDE_SPW, STS_FDE_CH>), g, b, 0, st, a);
+            // 16-B accesses need 16-B aligned rows (base and ld even)
+            const bool v2 = STS_RECUR_V2 &&
+                            ((reinterpret_cast<uintptr_t>(a.in) | reinterpret_cast<uintptr_t>(a.out)) & 15) == 0 &&
+                            a.ld_in % 2 == 0 && a.ld_out % 2 == 0;
+#define STS_FDE(HH)                                                                                           \
+            if (v2) hipLaunchKernelGGL((recur_kernel<kFillDiffEwma, HH, STS_FDE_SPW, STS_FDE_CH, true>), g, b, 0, st, a); \
+            else hipLaunchKernelGGL((recur_kernel<kFillDiffEwma, HH, STS_FDE_SPW, STS_FDE_CH>), g, b, 0, st, a);
+            if (a.lag <= 1) { STS_FDE(1) }
+            else if (a.lag <= 2) { STS_FDE(2) }
+            else if (a.lag <= 4) { STS_FDE(4) }
+            else { STS_FDE(8) }
+#undef STS_FDE
             return hipGetLastError();
         }
         return launch_h<kFillDiffEwma>(a, a.lag, st);
