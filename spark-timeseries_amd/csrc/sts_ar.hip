@@ -288,17 +288,29 @@ struct ArWaveLds {
 #define STS_AR_FMA 1   // explicit FMAs in the fit passes (A/B on C4: 6.26 -> 5.72 ms; remove stays bit-exact)
 #endif
 
+#ifndef STS_AR_STG
+#define STS_AR_STG 0   // A/B: coalesced HBM transfers through a per-wave LDS stage
+#endif
+
 #ifndef STS_AR_WAVES_PER_EU
 #define STS_AR_WAVES_PER_EU 2   // 256 VGPRs: the block (2B), windows and Gram rows stay spill-free
 #endif
-template <int P, int B>
-__global__ __launch_bounds__(64 * kRegWaves, STS_AR_WAVES_PER_EU) void ar_fit_blk_kernel(ArArgs a) {
-    __shared__ ArWaveLds lds[kRegWaves];
+// STG: the series block moves between HBM and registers through a per-wave LDS stage, so
+// every load / store instruction covers 1 KB of consecutive steps (8 lines) instead of one
+// 16-B piece per lane at a B * 8-byte stride (64 lines per instruction: the L1 / TA rate,
+// not HBM, bounded the unstaged kernel).  Rows of the stage are B + 2 doubles apart, which
+// keeps the lanes' 16-B block reads conflict-free.
+template <int P, int B, int NWV = kRegWaves, bool STG = false>
+__global__ __launch_bounds__(64 * NWV, STS_AR_WAVES_PER_EU) void ar_fit_blk_kernel(ArArgs a) {
+    __shared__ ArWaveLds lds[NWV];
+    constexpr int SR = B + 2;
+    __shared__ __attribute__((aligned(16))) double stg_mem[STG ? NWV * 64 * SR : 2];
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int64_t s = (int64_t)blockIdx.x * kRegWaves + wave;
+    const int64_t s = (int64_t)blockIdx.x * NWV + wave;
     if (s >= a.S) return;
     ArWaveLds& w = lds[wave];
+    double* stg = stg_mem + (STG ? wave * 64 * SR : 0);
     const int T = (int)a.T;
     const int t0 = lane * B;                  // this lane's block [t0, t0 + B)
     const double* xg = a.in + s * a.ld_in;
@@ -312,7 +324,30 @@ __global__ __launch_bounds__(64 * kRegWaves, STS_AR_WAVES_PER_EU) void ar_fit_bl
     double x[B];
     const bool full = (t0 + B <= T);
     const bool al = ((reinterpret_cast<uintptr_t>(xg) & 15) == 0) && (B % 2 == 0);
-    if (full && al) {
+    if (STG && al) {
+        // coalesced: pair q = lane + 64 i holds steps 2q, 2q + 1 -> stage row (2q) / B
+#pragma unroll
+        for (int i = 0; i < B / 2; i++) {
+            const int e = 2 * (lane + 64 * i);
+            double2 v;
+            if (e + 1 < T) {
+                v = *reinterpret_cast<const double2*>(xg + e);
+            } else {
+                v.x = (e < T) ? xg[e] : 0.0;
+                v.y = 0.0;
+            }
+            *reinterpret_cast<double2*>(stg + (e / B) * SR + (e % B)) = v;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+#pragma unroll
+        for (int j = 0; j < B / 2; j++) {
+            const double2 v = *reinterpret_cast<const double2*>(stg + lane * SR + 2 * j);
+            x[2 * j] = (t0 + 2 * j < T) ? v.x : 0.0;
+            x[2 * j + 1] = (t0 + 2 * j + 1 < T) ? v.y : 0.0;
+        }
+    } else if (full && al) {
         const double2* s2 = reinterpret_cast<const double2*>(xg + t0);
 #pragma unroll
         for (int j = 0; j < B / 2; j++) {
@@ -544,7 +579,8 @@ __global__ __launch_bounds__(64 * kRegWaves, STS_AR_WAVES_PER_EU) void ar_fit_bl
     // ---- fused removeTimeDependentEffects with the fitted model, in the reference's order
     //      (S/models/Autoregression.scala:60-73): d = x_t - c; d -= x_{t-j-1} * coef_j ----
     double* dst = a.out + s * a.ld_out;
-    const bool st16 = full && al && ((reinterpret_cast<uintptr_t>(dst) & 15) == 0);
+    const bool stg_out = STG && ((reinterpret_cast<uintptr_t>(dst) & 15) == 0);
+    const bool st16 = !stg_out && full && al && ((reinterpret_cast<uintptr_t>(dst) & 15) == 0);
     double xw[P + 1];                          // xw[k] = x_{t-k}
 #pragma unroll
     for (int k = 1; k <= P; k++) xw[k] = xp[k];
@@ -559,11 +595,26 @@ __global__ __launch_bounds__(64 * kRegWaves, STS_AR_WAVES_PER_EU) void ar_fit_bl
 #pragma unroll
         for (int k = P; k >= 2; k--) xw[k] = xw[k - 1];
         xw[1] = x[j];
-        if (st16) {
+        if (stg_out) {
+            if (j & 1) *reinterpret_cast<double2*>(stg + lane * SR + j - 1) = make_double2(rprev, d);
+            rprev = d;
+        } else if (st16) {
             if (j & 1) *reinterpret_cast<double2*>(dst + t - 1) = make_double2(rprev, d);
             rprev = d;
         } else if (t < T) {
             dst[t] = d;
+        }
+    }
+    if (stg_out) {   // coalesced store of the staged results
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+#pragma unroll
+        for (int i = 0; i < B / 2; i++) {
+            const int e = 2 * (lane + 64 * i);
+            const double2 v = *reinterpret_cast<const double2*>(stg + (e / B) * SR + (e % B));
+            if (e + 1 < T) *reinterpret_cast<double2*>(dst + e) = v;
+            else if (e < T) dst[e] = v.x;
         }
     }
 #ifdef STS_STAMPS
@@ -809,17 +860,18 @@ hipError_t launch_ar_fit(const ArArgs& a, hipStream_t st) {
     }
     // register path: p <= 8, T <= 64 * 40 (lane blocks of B steps, B in {8, 16, 24, 32, 40})
     if (a.p <= kRegPB && a.T <= 64 * 40 && !ab_knob("STS_AR_STAGED")) {
-        dim3 g((unsigned)((a.S + kRegWaves - 1) / kRegWaves)), b(64 * kRegWaves);
+        constexpr int NWV = STS_AR_STG ? 2 : kRegWaves;   // staged: 2 waves (2 x 21 KB of LDS) per workgroup
+        dim3 g((unsigned)((a.S + NWV - 1) / NWV)), b(64 * NWV);
         const int64_t need = (a.T + 63) / 64;
         const int B = need <= 8 ? 8 : need <= 16 ? 16 : need <= 24 ? 24 : need <= 32 ? 32 : 40;
 #define STS_AR_BLK(PP)                                                                          \
         case PP:                                                                                \
             switch (B) {                                                                        \
-            case 8: hipLaunchKernelGGL((ar_fit_blk_kernel<PP, 8>), g, b, 0, st, a); break;      \
-            case 16: hipLaunchKernelGGL((ar_fit_blk_kernel<PP, 16>), g, b, 0, st, a); break;    \
-            case 24: hipLaunchKernelGGL((ar_fit_blk_kernel<PP, 24>), g, b, 0, st, a); break;    \
-            case 32: hipLaunchKernelGGL((ar_fit_blk_kernel<PP, 32>), g, b, 0, st, a); break;    \
-            default: hipLaunchKernelGGL((ar_fit_blk_kernel<PP, 40>), g, b, 0, st, a); break;    \
+            case 8: hipLaunchKernelGGL((ar_fit_blk_kernel<PP, 8, NWV, STS_AR_STG>), g, b, 0, st, a); break;      \
+            case 16: hipLaunchKernelGGL((ar_fit_blk_kernel<PP, 16, NWV, STS_AR_STG>), g, b, 0, st, a); break;    \
+            case 24: hipLaunchKernelGGL((ar_fit_blk_kernel<PP, 24, NWV, STS_AR_STG>), g, b, 0, st, a); break;    \
+            case 32: hipLaunchKernelGGL((ar_fit_blk_kernel<PP, 32, NWV, STS_AR_STG>), g, b, 0, st, a); break;    \
+            default: hipLaunchKernelGGL((ar_fit_blk_kernel<PP, 40, NWV, STS_AR_STG>), g, b, 0, st, a); break;    \
             }                                                                                   \
             break;
         switch (a.p) {
