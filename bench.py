@@ -253,7 +253,7 @@ def main():
               "c5": "sts::tile_kernel<4096,0> (fill nearest + lag-matrix columns)",
               "c2": "sts::recur_kernel<kFillDiffEwma> (fillPrevious -> differencesAtLag(1) -> EWMA add, lane per series)",
               "stage_c2": "sts::recur_kernel<kFillDiffEwma> (fillPrevious -> differencesAtLag(1) -> EWMA add, lane per series)",
-              "c4": "sts::ar_fit_blk_kernel<5,40> (AR(5): lane-blocked register lag products, lane-parallel Gram / Cholesky + refinement, fused remove)",
+              "c4": "sts::ar_fit_blk_kernel<5,40,4,dma> (AR(5): series in by LDS-DMA, lane-blocked register lag products, lane-parallel Gram / Cholesky + refinement, fused remove out through LDS)",
               "stats": "sts::stats_kernel<64,32> (StatCounter.merge per lane, LDS-staged series block)",
               "nan_instants": "sts::nan_instants_kernel + sts::gather_instants_kernel",
               "to_instants": "sts::transpose_kernel (64x64 LDS tiles)",

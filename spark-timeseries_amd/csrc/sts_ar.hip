@@ -15,6 +15,7 @@
 // Cholesky in fp64 and one step of iterative refinement against an exact residual pass
 // (corrected semi-normal equations) brings the error back to Householder-QR level.
 #include "sts_internal.hpp"
+#include "sts_dma.hpp"
 
 #include <hip/hip_runtime.h>
 
@@ -288,29 +289,32 @@ struct ArWaveLds {
 #define STS_AR_FMA 1   // explicit FMAs in the fit passes (A/B on C4: 6.26 -> 5.72 ms; remove stays bit-exact)
 #endif
 
-#ifndef STS_AR_STG
-#define STS_AR_STG 0   // A/B: coalesced HBM transfers through a per-wave LDS stage
+#ifndef STS_AR_DMA
+#define STS_AR_DMA 1   // series block in by LDS-DMA, residuals out through the same LDS block
 #endif
 
 #ifndef STS_AR_WAVES_PER_EU
 #define STS_AR_WAVES_PER_EU 2   // 256 VGPRs: the block (2B), windows and Gram rows stay spill-free
 #endif
-// STG: the series block moves between HBM and registers through a per-wave LDS stage, so
-// every load / store instruction covers 1 KB of consecutive steps (8 lines) instead of one
-// 16-B piece per lane at a B * 8-byte stride (64 lines per instruction: the L1 / TA rate,
-// not HBM, bounded the unstaged kernel).  Rows of the stage are B + 2 doubles apart, which
-// keeps the lanes' 16-B block reads conflict-free.
-template <int P, int B, int NWV = kRegWaves, bool STG = false>
+// DMA: the wave's series arrives by LDS-DMA (global_load_lds_dwordx4, 1 KB of consecutive
+// steps per instruction, no VGPR staging) into a per-wave LDS block of 64 B doubles that is
+// exactly the lanes' blocks back to back; each lane then reads its B steps with 16-B LDS
+// reads.  The fit's LDS scratch (ArWaveLds) aliases that block once the series is in
+// registers, and the fused residuals go out through it again (16-B LDS writes at the lanes'
+// block offsets, then 1-KB coalesced stores).  Without DMA every load / store instruction
+// touches one 16-B piece per lane at a B * 8-byte stride: 64 cache lines per instruction.
+template <int P, int B, int NWV = kRegWaves, bool DMA = false>
 __global__ __launch_bounds__(64 * NWV, STS_AR_WAVES_PER_EU) void ar_fit_blk_kernel(ArArgs a) {
-    __shared__ ArWaveLds lds[NWV];
-    constexpr int SR = B + 2;
-    __shared__ __attribute__((aligned(16))) double stg_mem[STG ? NWV * 64 * SR : 2];
+    constexpr int BUFD = 64 * B;              // doubles per wave block
+    static_assert(!DMA || sizeof(ArWaveLds) <= BUFD * sizeof(double), "scratch fits the block");
+    __shared__ __attribute__((aligned(16))) double buf_mem[DMA ? NWV * BUFD : 2];
+    __shared__ ArWaveLds lds_mem[DMA ? 1 : NWV];
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int64_t s = (int64_t)blockIdx.x * NWV + wave;
     if (s >= a.S) return;
-    ArWaveLds& w = lds[wave];
-    double* stg = stg_mem + (STG ? wave * 64 * SR : 0);
+    double* buf = buf_mem + (DMA ? wave * BUFD : 0);
+    ArWaveLds& w = DMA ? *reinterpret_cast<ArWaveLds*>(buf) : lds_mem[wave];
     const int T = (int)a.T;
     const int t0 = lane * B;                  // this lane's block [t0, t0 + B)
     const double* xg = a.in + s * a.ld_in;
@@ -324,29 +328,24 @@ __global__ __launch_bounds__(64 * NWV, STS_AR_WAVES_PER_EU) void ar_fit_blk_kern
     double x[B];
     const bool full = (t0 + B <= T);
     const bool al = ((reinterpret_cast<uintptr_t>(xg) & 15) == 0) && (B % 2 == 0);
-    if (STG && al) {
-        // coalesced: pair q = lane + 64 i holds steps 2q, 2q + 1 -> stage row (2q) / B
+    // DMA needs whole 16-B pieces inside the row: T even (and a 16-B aligned row)
+    const bool dma = DMA && al && !(T & 1);
+    if (dma) {
+        const unsigned lb = lds_addr(buf);
 #pragma unroll
         for (int i = 0; i < B / 2; i++) {
-            const int e = 2 * (lane + 64 * i);
-            double2 v;
-            if (e + 1 < T) {
-                v = *reinterpret_cast<const double2*>(xg + e);
-            } else {
-                v.x = (e < T) ? xg[e] : 0.0;
-                v.y = 0.0;
-            }
-            *reinterpret_cast<double2*>(stg + (e / B) * SR + (e % B)) = v;
+            const int u = 2 * (i * 64 + lane);   // series position of this lane's 16-B piece
+            glds16(xg + (u < T ? u : 0), lb + i * 1024);
         }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+        dma_wait();
+        wave_lds_sync();
 #pragma unroll
         for (int j = 0; j < B / 2; j++) {
-            const double2 v = *reinterpret_cast<const double2*>(stg + lane * SR + 2 * j);
+            const double2 v = *reinterpret_cast<const double2*>(buf + t0 + 2 * j);
             x[2 * j] = (t0 + 2 * j < T) ? v.x : 0.0;
             x[2 * j + 1] = (t0 + 2 * j + 1 < T) ? v.y : 0.0;
         }
+        wave_lds_sync();   // the block is in registers: the LDS block becomes the fit's scratch
     } else if (full && al) {
         const double2* s2 = reinterpret_cast<const double2*>(xg + t0);
 #pragma unroll
@@ -579,8 +578,9 @@ __global__ __launch_bounds__(64 * NWV, STS_AR_WAVES_PER_EU) void ar_fit_blk_kern
     // ---- fused removeTimeDependentEffects with the fitted model, in the reference's order
     //      (S/models/Autoregression.scala:60-73): d = x_t - c; d -= x_{t-j-1} * coef_j ----
     double* dst = a.out + s * a.ld_out;
-    const bool stg_out = STG && ((reinterpret_cast<uintptr_t>(dst) & 15) == 0);
-    const bool st16 = !stg_out && full && al && ((reinterpret_cast<uintptr_t>(dst) & 15) == 0);
+    const bool dma_out = dma && ((reinterpret_cast<uintptr_t>(dst) & 15) == 0);
+    const bool st16 = !dma_out && full && al && ((reinterpret_cast<uintptr_t>(dst) & 15) == 0);
+    if (dma_out) wave_lds_sync();   // every read of the fit's scratch (w) is done before the block is rewritten
     double xw[P + 1];                          // xw[k] = x_{t-k}
 #pragma unroll
     for (int k = 1; k <= P; k++) xw[k] = xp[k];
@@ -595,8 +595,8 @@ __global__ __launch_bounds__(64 * NWV, STS_AR_WAVES_PER_EU) void ar_fit_blk_kern
 #pragma unroll
         for (int k = P; k >= 2; k--) xw[k] = xw[k - 1];
         xw[1] = x[j];
-        if (stg_out) {
-            if (j & 1) *reinterpret_cast<double2*>(stg + lane * SR + j - 1) = make_double2(rprev, d);
+        if (dma_out) {
+            if (j & 1) *reinterpret_cast<double2*>(buf + t - 1) = make_double2(rprev, d);
             rprev = d;
         } else if (st16) {
             if (j & 1) *reinterpret_cast<double2*>(dst + t - 1) = make_double2(rprev, d);
@@ -605,16 +605,12 @@ __global__ __launch_bounds__(64 * NWV, STS_AR_WAVES_PER_EU) void ar_fit_blk_kern
             dst[t] = d;
         }
     }
-    if (stg_out) {   // coalesced store of the staged results
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+    if (dma_out) {   // coalesced 1-KB stores of the staged residuals (T even)
+        wave_lds_sync();
 #pragma unroll
         for (int i = 0; i < B / 2; i++) {
-            const int e = 2 * (lane + 64 * i);
-            const double2 v = *reinterpret_cast<const double2*>(stg + (e / B) * SR + (e % B));
-            if (e + 1 < T) *reinterpret_cast<double2*>(dst + e) = v;
-            else if (e < T) dst[e] = v.x;
+            const int u = 2 * (i * 64 + lane);
+            if (u < T) *reinterpret_cast<double2*>(dst + u) = *reinterpret_cast<const double2*>(buf + u);
         }
     }
 #ifdef STS_STAMPS
@@ -860,18 +856,18 @@ hipError_t launch_ar_fit(const ArArgs& a, hipStream_t st) {
     }
     // register path: p <= 8, T <= 64 * 40 (lane blocks of B steps, B in {8, 16, 24, 32, 40})
     if (a.p <= kRegPB && a.T <= 64 * 40 && !ab_knob("STS_AR_STAGED")) {
-        constexpr int NWV = STS_AR_STG ? 2 : kRegWaves;   // staged: 2 waves (2 x 21 KB of LDS) per workgroup
+        constexpr int NWV = kRegWaves;
         dim3 g((unsigned)((a.S + NWV - 1) / NWV)), b(64 * NWV);
         const int64_t need = (a.T + 63) / 64;
         const int B = need <= 8 ? 8 : need <= 16 ? 16 : need <= 24 ? 24 : need <= 32 ? 32 : 40;
 #define STS_AR_BLK(PP)                                                                          \
         case PP:                                                                                \
             switch (B) {                                                                        \
-            case 8: hipLaunchKernelGGL((ar_fit_blk_kernel<PP, 8, NWV, STS_AR_STG>), g, b, 0, st, a); break;      \
-            case 16: hipLaunchKernelGGL((ar_fit_blk_kernel<PP, 16, NWV, STS_AR_STG>), g, b, 0, st, a); break;    \
-            case 24: hipLaunchKernelGGL((ar_fit_blk_kernel<PP, 24, NWV, STS_AR_STG>), g, b, 0, st, a); break;    \
-            case 32: hipLaunchKernelGGL((ar_fit_blk_kernel<PP, 32, NWV, STS_AR_STG>), g, b, 0, st, a); break;    \
-            default: hipLaunchKernelGGL((ar_fit_blk_kernel<PP, 40, NWV, STS_AR_STG>), g, b, 0, st, a); break;    \
+            case 8: hipLaunchKernelGGL((ar_fit_blk_kernel<PP, 8, NWV, STS_AR_DMA>), g, b, 0, st, a); break;      \
+            case 16: hipLaunchKernelGGL((ar_fit_blk_kernel<PP, 16, NWV, STS_AR_DMA>), g, b, 0, st, a); break;    \
+            case 24: hipLaunchKernelGGL((ar_fit_blk_kernel<PP, 24, NWV, STS_AR_DMA>), g, b, 0, st, a); break;    \
+            case 32: hipLaunchKernelGGL((ar_fit_blk_kernel<PP, 32, NWV, STS_AR_DMA>), g, b, 0, st, a); break;    \
+            default: hipLaunchKernelGGL((ar_fit_blk_kernel<PP, 40, NWV, STS_AR_DMA>), g, b, 0, st, a); break;    \
             }                                                                                   \
             break;
         switch (a.p) {

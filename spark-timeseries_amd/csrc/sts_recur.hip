@@ -19,12 +19,116 @@
 
 #include <hip/hip_runtime.h>
 
+#ifndef STS_FDE_SPW
+#define STS_FDE_SPW 16   // series per wave (A/B on C2, 1M x 390: 16 x 128 1.40 ms, 24 x 128 1.41-1.43,
+#define STS_FDE_CH 128   // 8 x 128 1.42, 32 x 128 1.50-1.52, 32 x 64 1.59-1.67, 16 x 192 2.35, 16 x 256 2.24)
+#endif
+
 #ifndef STS_RECUR_V2
 #define STS_RECUR_V2 1   // 16-B global accesses in the C2 recurrence kernel (A/B: 1.673 vs 1.687 ms on C2)
 #endif
 
 namespace sts {
 namespace {
+
+constexpr int kSpw = STS_FDE_SPW, kCh = STS_FDE_CH;
+
+// One lane's recurrence state and step, shared by the chunk and row kernels (the
+// reference's statement order; -ffp-contract=off keeps every product / sum separate).
+template <int OP, int H>
+struct RecurLane {
+    double sm = 0.0, oms = 0.0, cc = 0.0;
+    double cf[H];
+    double h[H];                   // value at t-1-j (outputs, or filled values for kFillDiffEwma)
+    double e = 0.0;                // EWMA state
+    double carry;                  // fillPrevious carry
+    int hp;
+    int64_t start;
+    // load: the state and the raw per-series parameters (plain loads from clamped indices, no
+    // arithmetic on them, so nothing waits for them until finish()); finish: derived values
+    __device__ __forceinline__ void load(const RecurArgs& a, int64_t sl, bool live) {
+        carry = __builtin_nan("");
+        hp = (OP == kArAdd || OP == kArRemoveInplace) ? a.p : a.lag;   // history length used
+        start = (OP == kFillDiffEwma) ? a.lag : a.start;
+        e = 0.0;
+        const int64_t si = live ? sl : 0;
+#pragma unroll
+        for (int j = 0; j < H; j++) {
+            cf[j] = 0.0;
+            h[j] = 0.0;
+        }
+        if (OP == kEwmaAdd || OP == kEwmaRemoveInplace || OP == kFillDiffEwma) sm = a.sm[si];
+        if (OP == kArAdd || OP == kArRemoveInplace) {
+            cc = a.c[si];
+#pragma unroll
+            for (int j = 0; j < H; j++) cf[j] = a.coef[si * a.p + (j < a.p ? j : 0)];
+        }
+    }
+    __device__ __forceinline__ void finish(const RecurArgs& a) {
+        if (OP == kEwmaAdd || OP == kEwmaRemoveInplace || OP == kFillDiffEwma) oms = 1.0 - sm;
+        if (OP == kArAdd || OP == kArRemoveInplace) {
+#pragma unroll
+            for (int j = 0; j < H; j++) cf[j] = (j < a.p) ? cf[j] : 0.0;
+        }
+    }
+    __device__ __forceinline__ void init(const RecurArgs& a, int64_t sl, bool live) {
+        load(a, sl, live);
+        finish(a);
+    }
+    // STEADY: t >= steady_from() (every t-guard below is then a constant; same operations)
+    __device__ __forceinline__ int64_t steady_from() const {
+        int64_t f = start > H ? start : H;
+        return f > 1 ? f : 1;
+    }
+    template <bool STEADY = false>
+    __device__ __forceinline__ double step(double x, int64_t t) {
+        const bool first = !STEADY && t == 0;
+        const bool before = !STEADY && t < start;
+        double y;
+        if (OP == kEwmaAdd) {
+            // dest(i) = smoothing * ts(i) + (1 - smoothing) * dest(i - 1)
+            e = first ? x : sm * x + oms * e;
+            y = e;
+        } else if (OP == kEwmaRemoveInplace) {
+            // ts(i - 1) already overwritten by dest(i - 1)
+            y = first ? x : (x - oms * h[0]) / sm;
+        } else if (OP == kArAdd) {
+            y = cc + x;
+#pragma unroll
+            for (int j = 0; j < H; j++)
+                if (j < hp && (STEADY || t - j - 1 >= 0)) y += h[j] * cf[j];
+        } else if (OP == kArRemoveInplace) {
+            y = x - cc;
+#pragma unroll
+            for (int j = 0; j < H; j++)
+                if (j < hp && (STEADY || t - j - 1 >= 0)) y -= h[j] * cf[j];
+        } else if (OP == kDiffInplace) {
+            // ts(i - lag) already overwritten when i - lag >= start; for i - lag < start it
+            // equals the original, so h (the outputs) is right in both cases
+            double hl = 0.0;
+#pragma unroll
+            for (int j = 0; j < H; j++) hl = (j == hp - 1) ? h[j] : hl;   // static indexing
+            y = before ? x : x - hl;
+        } else {  // kFillDiffEwma: fillPrevious -> differencesAtLag(lag, start=lag) -> EWMA add
+            carry = (x != x) ? carry : x;
+            const double f = carry;
+            double hl = 0.0;
+#pragma unroll
+            for (int j = 0; j < H; j++) hl = (j == hp - 1) ? h[j] : hl;   // static indexing
+            const double d = before ? f : f - hl;
+            e = first ? d : sm * d + oms * e;
+            // history of FILLED values
+#pragma unroll
+            for (int j = H - 1; j > 0; j--) h[j] = h[j - 1];
+            h[0] = f;
+            return e;
+        }
+#pragma unroll
+        for (int j = H - 1; j > 0; j--) h[j] = h[j - 1];
+        h[0] = y;
+        return y;
+    }
+};
 
 // SPW series per wave, CH steps per chunk: the chunk's SPW x CH block moves through LDS
 // with every load / store instruction covering 64 consecutive steps of ONE series (512
@@ -38,7 +142,7 @@ __global__ __launch_bounds__(64) void recur_kernel(RecurArgs a) {
     constexpr int kRow = V2 ? CH + 2 : CH + 1;
     constexpr int EPL = V2 ? 2 : 1;               // elements per lane per instruction
     constexpr int NLD = SPW * CH / (64 * EPL);    // load instructions per chunk per lane
-    static_assert(SPW * CH % (64 * EPL) == 0 && (CH % 64 == 0 || 64 % CH == 0), "chunk shape");
+    static_assert(SPW * CH % (64 * EPL) == 0 && (V2 ? CH % 2 == 0 : (CH % 64 == 0 || 64 % CH == 0)), "chunk shape");
     __shared__ __attribute__((aligned(16))) double tile[SPW * kRow];
     const int lane = threadIdx.x;
     const int64_t s0 = (int64_t)blockIdx.x * SPW;
@@ -47,29 +151,8 @@ __global__ __launch_bounds__(64) void recur_kernel(RecurArgs a) {
     const int ns = (a.S - s0 < SPW) ? (int)(a.S - s0) : SPW;
     const int64_t T = a.T;
 
-    // per-series parameters
-    double sm = 0.0, oms = 0.0, cc = 0.0;
-    double cf[H];
-#pragma unroll
-    for (int j = 0; j < H; j++) cf[j] = 0.0;
-    const int hp = (OP == kArAdd || OP == kArRemoveInplace) ? a.p : a.lag;  // history length used
-    if (live) {
-        if (OP == kEwmaAdd || OP == kEwmaRemoveInplace || OP == kFillDiffEwma) {
-            sm = a.sm[sl];
-            oms = 1.0 - sm;
-        }
-        if (OP == kArAdd || OP == kArRemoveInplace) {
-            cc = a.c[sl];
-#pragma unroll
-            for (int j = 0; j < H; j++) cf[j] = (j < a.p) ? a.coef[sl * a.p + j] : 0.0;
-        }
-    }
-    // state: h[j] = value at t-1-j (outputs, or filled values for kFillDiffEwma)
-    double h[H];
-#pragma unroll
-    for (int j = 0; j < H; j++) h[j] = 0.0;
-    double e = 0.0;                                // EWMA state
-    double carry = __builtin_nan("");              // fillPrevious carry
+    RecurLane<OP, H> rl;
+    rl.init(a, sl, live);
 
     // load instruction i of a chunk: element e = (i * 64 + lane) * EPL, row e / CH, column e % CH
     double2 pre[NLD];
@@ -109,55 +192,7 @@ __global__ __launch_bounds__(64) void recur_kernel(RecurArgs a) {
         __syncthreads();
         if (live) {
             double* myrow = tile + lane * kRow;
-            for (int c = 0; c < len; c++) {
-                const int64_t t = tc + c;
-                const double x = myrow[c];
-                double y;
-                if (OP == kEwmaAdd) {
-                    // dest(i) = smoothing * ts(i) + (1 - smoothing) * dest(i - 1)
-                    e = (t == 0) ? x : sm * x + oms * e;
-                    y = e;
-                } else if (OP == kEwmaRemoveInplace) {
-                    // ts(i - 1) already overwritten by dest(i - 1)
-                    y = (t == 0) ? x : (x - oms * h[0]) / sm;
-                } else if (OP == kArAdd) {
-                    y = cc + x;
-#pragma unroll
-                    for (int j = 0; j < H; j++)
-                        if (j < hp && t - j - 1 >= 0) y += h[j] * cf[j];
-                } else if (OP == kArRemoveInplace) {
-                    y = x - cc;
-#pragma unroll
-                    for (int j = 0; j < H; j++)
-                        if (j < hp && t - j - 1 >= 0) y -= h[j] * cf[j];
-                } else if (OP == kDiffInplace) {
-                    // ts(i - lag) already overwritten when i - lag >= start; for i - lag < start it
-                    // equals the original, so h (the outputs) is right in both cases
-                    double hl = 0.0;
-#pragma unroll
-                    for (int j = 0; j < H; j++) hl = (j == hp - 1) ? h[j] : hl;   // static indexing
-                    y = (t < a.start) ? x : x - hl;
-                } else {  // kFillDiffEwma: fillPrevious -> differencesAtLag(lag, start=lag) -> EWMA add
-                    carry = (x != x) ? carry : x;
-                    const double f = carry;
-                    double hl = 0.0;
-#pragma unroll
-                    for (int j = 0; j < H; j++) hl = (j == hp - 1) ? h[j] : hl;   // static indexing
-                    const double d = (t < a.lag) ? f : f - hl;
-                    e = (t == 0) ? d : sm * d + oms * e;
-                    y = e;
-                    // history of FILLED values
-#pragma unroll
-                    for (int j = H - 1; j > 0; j--) h[j] = h[j - 1];
-                    h[0] = f;
-                    myrow[c] = y;
-                    continue;
-                }
-#pragma unroll
-                for (int j = H - 1; j > 0; j--) h[j] = h[j - 1];
-                h[0] = y;
-                myrow[c] = y;
-            }
+            for (int c = 0; c < len; c++) myrow[c] = rl.step(myrow[c], tc + c);
         }
         __syncthreads();
 #pragma unroll
@@ -211,8 +246,22 @@ __global__ __launch_bounds__(256) void ar_naive_kernel(RecurArgs a) {
     }
 }
 
+// 16-B accesses need 16-B aligned rows (base and ld even)
+inline bool rows16(const RecurArgs& a) {
+    return STS_RECUR_V2 && ((reinterpret_cast<uintptr_t>(a.in) | reinterpret_cast<uintptr_t>(a.out)) & 15) == 0 &&
+           a.ld_in % 2 == 0 && a.ld_out % 2 == 0;
+}
+
 template <int OP>
 hipError_t launch_h(const RecurArgs& a, int need, hipStream_t st) {
+    if (need <= 8 && rows16(a)) {   // the C2 shape: 16 series x 128-step chunks, 16-B accesses
+        dim3 g((unsigned)((a.S + kSpw - 1) / kSpw)), b(64);
+        if (need <= 1) hipLaunchKernelGGL((recur_kernel<OP, 1, kSpw, kCh, true>), g, b, 0, st, a);
+        else if (need <= 2) hipLaunchKernelGGL((recur_kernel<OP, 2, kSpw, kCh, true>), g, b, 0, st, a);
+        else if (need <= 4) hipLaunchKernelGGL((recur_kernel<OP, 4, kSpw, kCh, true>), g, b, 0, st, a);
+        else hipLaunchKernelGGL((recur_kernel<OP, 8, kSpw, kCh, true>), g, b, 0, st, a);
+        return hipGetLastError();
+    }
     dim3 grid((unsigned)((a.S + 63) / 64)), block(64);
     if (need <= 1) hipLaunchKernelGGL((recur_kernel<OP, 1>), grid, block, 0, st, a);
     else if (need <= 2) hipLaunchKernelGGL((recur_kernel<OP, 2>), grid, block, 0, st, a);
@@ -240,26 +289,6 @@ hipError_t launch_recur(RecurOp op, const RecurArgs& a, hipStream_t st) {
     case kArRemoveInplace: return launch_h<kArRemoveInplace>(a, a.p, st);
     case kDiffInplace: return launch_h<kDiffInplace>(a, a.lag, st);
     case kFillDiffEwma:
-#ifndef STS_FDE_SPW
-#define STS_FDE_SPW 32
-#define STS_FDE_CH 64
-#endif
-        if (a.lag <= 8) {   // C2 shape: 32 series x 64-step chunks per wave (A/B: r01 notes)
-            dim3 g((unsigned)((a.S + STS_FDE_SPW - 1) / STS_FDE_SPW)), b(64);
-            // 16-B accesses need 16-B aligned rows (base and ld even)
-            const bool v2 = STS_RECUR_V2 &&
-                            ((reinterpret_cast<uintptr_t>(a.in) | reinterpret_cast<uintptr_t>(a.out)) & 15) == 0 &&
-                            a.ld_in % 2 == 0 && a.ld_out % 2 == 0;
-#define STS_FDE(HH)                                                                                           \
-            if (v2) hipLaunchKernelGGL((recur_kernel<kFillDiffEwma, HH, STS_FDE_SPW, STS_FDE_CH, true>), g, b, 0, st, a); \
-            else hipLaunchKernelGGL((recur_kernel<kFillDiffEwma, HH, STS_FDE_SPW, STS_FDE_CH>), g, b, 0, st, a);
-            if (a.lag <= 1) { STS_FDE(1) }
-            else if (a.lag <= 2) { STS_FDE(2) }
-            else if (a.lag <= 4) { STS_FDE(4) }
-            else { STS_FDE(8) }
-#undef STS_FDE
-            return hipGetLastError();
-        }
         return launch_h<kFillDiffEwma>(a, a.lag, st);
     }
     return hipErrorInvalidValue;

@@ -1,0 +1,143 @@
+"""Bit-exact parity of the recurrence kernels (recur_kernel: one lane per series, 16 series x
+128-step chunks through LDS with 16-B accesses when rows are 16-B aligned, 64 x 32 with 8-B
+accesses otherwise) with the oracle, through the C ABI.  Shapes cover partial chunks and
+partial series groups (S, T not multiples of 16 / 128), padded row strides (ld > T, different
+in and out strides, odd padding that forces the 8-B kernel) and the in-place operators
+(reference aliasing).  Needs an MI355X.
+"""
+import numpy as np
+import pytest
+
+import oracle
+
+pytestmark = pytest.mark.gpu
+NaN = np.nan
+
+SHAPES = [(37, 2), (37, 8), (33, 14), (33, 64), (65, 390), (9, 512), (41, 100), (70, 16), (1, 390), (17, 510),
+          (19, 129), (21, 1000)]
+
+
+@pytest.fixture(scope="module")
+def torch():
+    import torch as _t
+    if not _t.cuda.is_available():
+        pytest.skip("no GPU")
+    from sparkts import _native
+    _native.ensure_device(0)
+    return _t
+
+
+def padded(torch, x, ld):
+    S, T = x.shape
+    t = torch.full((S, ld), 7.0, dtype=torch.float64, device="cuda:0")
+    t[:, :T] = torch.as_tensor(x, device="cuda:0")
+    return t
+
+
+def host(t, T):
+    return t.detach().cpu().numpy()[:, :T]
+
+
+def assert_bits(got, ref, what=""):
+    got = np.ascontiguousarray(got, dtype=np.float64)
+    ref = np.ascontiguousarray(ref, dtype=np.float64)
+    assert got.shape == ref.shape, (what, got.shape, ref.shape)
+    same = (got.view(np.uint64) == ref.view(np.uint64)) | (np.isnan(got) & np.isnan(ref))
+    if not same.all():
+        idx = np.argwhere(~same)[:5]
+        raise AssertionError("%s: %d mismatches, first %s" % (what, (~same).sum(), idx.tolist()))
+
+
+def dvec(torch, v):
+    return torch.as_tensor(np.ascontiguousarray(v, dtype=np.float64), device="cuda:0")
+
+
+@pytest.mark.parametrize("S,T", SHAPES)
+@pytest.mark.parametrize("pad", [0, 6, 3])
+def test_recur_ewma(torch, S, T, pad):
+    from sparkts import _native
+    lib = _native.lib()
+    rng = np.random.default_rng(S * 1000 + T + pad)
+    x = rng.standard_normal((S, T)) + 10
+    s = rng.uniform(0.05, 0.95, S)
+    sd = dvec(torch, s)
+    xi = padded(torch, x, T + pad)
+    out = padded(torch, np.zeros((S, T)), T + 2 * pad)
+    assert lib.sts_ewma_add(xi.data_ptr(), out.data_ptr(), S, T, T + pad, T + 2 * pad, sd.data_ptr(), None) == 0
+    assert_bits(host(out, T), np.array([oracle.ewma_add(r, v) for r, v in zip(x, s)]), "ewma add")
+    assert (out[:, T:].cpu().numpy() == 7.0).all(), "wrote into the row padding"
+    ip = padded(torch, x, T + pad)
+    assert lib.sts_ewma_remove(ip.data_ptr(), ip.data_ptr(), S, T, T + pad, T + pad, sd.data_ptr(), None) == 0
+    ref = []
+    for r, v in zip(x, s):
+        rr = r.copy()
+        oracle.ewma_remove(rr, v, dest=rr)
+        ref.append(rr)
+    assert_bits(host(ip, T), np.array(ref), "ewma remove in place")
+
+
+@pytest.mark.parametrize("S,T", SHAPES)
+@pytest.mark.parametrize("p", [1, 3, 8])
+def test_recur_ar(torch, S, T, p):
+    from sparkts import _native
+    lib = _native.lib()
+    rng = np.random.default_rng(S * 7 + T + p)
+    x = rng.standard_normal((S, T))
+    c = rng.standard_normal(S)
+    coef = rng.uniform(-0.3, 0.3, (S, p))
+    cd, fd = dvec(torch, c), dvec(torch, coef)
+    xi = padded(torch, x, T + 4)
+    out = padded(torch, np.zeros((S, T)), T)
+    assert lib.sts_ar_add(xi.data_ptr(), out.data_ptr(), S, T, T + 4, T, cd.data_ptr(), fd.data_ptr(), p, None) == 0
+    assert_bits(host(out, T), np.array([oracle.ar_add(x[s], c[s], coef[s]) for s in range(S)]), "ar add")
+    ip = padded(torch, x, T + 4)
+    assert lib.sts_ar_remove(ip.data_ptr(), ip.data_ptr(), S, T, T + 4, T + 4, cd.data_ptr(), fd.data_ptr(), p,
+                             None) == 0
+    ref = []
+    for s in range(S):
+        r = x[s].copy()
+        for i in range(T):
+            v = r[i] - c[s]
+            for j in range(min(p, i)):
+                v -= r[i - j - 1] * coef[s, j]
+            r[i] = v
+        ref.append(r)
+    assert_bits(host(ip, T), np.array(ref), "ar remove in place")
+
+
+@pytest.mark.parametrize("S,T", SHAPES)
+@pytest.mark.parametrize("lag,start", [(1, 1), (3, 3), (2, 5), (8, 8)])
+def test_recur_diff_in_place(torch, S, T, lag, start):
+    from sparkts import _native
+    lib = _native.lib()
+    if start > T:
+        pytest.skip("start beyond the series")
+    x = np.random.default_rng(S + T + lag).standard_normal((S, T))
+    ip = padded(torch, x, T + 2)
+    assert lib.sts_diff_at_lag(ip.data_ptr(), ip.data_ptr(), S, T, T + 2, T + 2, lag, start, None) == 0
+    ref = np.array([oracle.differences_at_lag(r, lag, start=start, inplace=True) for r in x])
+    assert_bits(host(ip, T), ref, "diff in place")
+
+
+@pytest.mark.parametrize("S,T", SHAPES)
+@pytest.mark.parametrize("lag", [1, 2, 8])
+def test_recur_fill_diff_ewma(torch, S, T, lag):
+    from sparkts import _native
+    lib = _native.lib()
+    rng = np.random.default_rng(S + 3 * T + lag)
+    x = 100 + rng.standard_normal((S, T)).cumsum(axis=1)
+    x[rng.random((S, T)) < 0.2] = NaN
+    x[0, : min(T, 5)] = NaN          # leading NaN run (fillPrevious leaves it NaN)
+    if S > 2:
+        x[2, :] = NaN                # all-NaN series
+    s = rng.uniform(0.05, 0.95, S)
+    xi = padded(torch, x, T + 6)
+    out = padded(torch, np.zeros((S, T)), T + 2)
+    assert lib.sts_fill_diff_ewma(xi.data_ptr(), out.data_ptr(), S, T, T + 6, T + 2, 3, lag,
+                                  dvec(torch, s).data_ptr(), None, None) == 0
+    ref = []
+    for r, v in zip(x, s):
+        f = oracle.fill_previous(r)
+        d = oracle.differences_at_lag(f, lag)
+        ref.append(oracle.ewma_add(d, v))
+    assert_bits(host(out, T), np.array(ref), "fill_diff_ewma")
