@@ -34,6 +34,7 @@
 #include "sts_internal.hpp"
 #include "sts_acf.hpp"
 #include "sts_scan.hpp"
+#include "sts_dma.hpp"
 
 #include <hip/hip_runtime.h>
 
@@ -57,6 +58,10 @@
 
 #ifndef STS_TILE_WGS
 #define STS_TILE_WGS 3    // workgroups per CU the register budget is sized for
+#endif
+
+#ifndef STS_TILE_DMA
+#define STS_TILE_DMA 0    // A/B: the next interior tile arrives by LDS-DMA into a staging buffer, issued at tile start
 #endif
 
 #ifndef STS_EARLY
@@ -182,8 +187,8 @@ __device__ __forceinline__ int px2_(int q2) { return PAD ? q2 + ((q2 >> 4) << 1)
 // + j%q -- every lag 0 .. 16 NT - q exactly once per step, and the same lag map h(j) - i in
 // every accumulator; TOEPLITZ (K = 61..63) uses NT = floor((K + 15) / 16) + 1 MFMAs with
 // U_t holding lag 16t + j - i.
-template <int TW, int NT, bool SHIFTED, int NTH, bool DB = false>
-__global__ __launch_bounds__(NTH, DB ? 2 : STS_TILE_WGS) void tile_kernel(TileArgs a, int method) {
+template <int TW, int NT, bool SHIFTED, int NTH, bool DB = false, bool DMA = false>
+__global__ __launch_bounds__(NTH, (DB || DMA) ? 2 : STS_TILE_WGS) void tile_kernel(TileArgs a, int method) {
     constexpr int kThreads = NTH;          // 256 (4 waves) or 128 (2 waves, TW = 2048)
     constexpr int kWaves = NTH / 64;
     static_assert(TW / 64 % kWaves == 0, "whole 64-step chunks per wave");
@@ -206,6 +211,9 @@ __global__ __launch_bounds__(NTH, DB ? 2 : STS_TILE_WGS) void tile_kernel(TileAr
     // k's lag products can run during tile k + 1's phases
     __shared__ __attribute__((aligned(16))) double vals_mem[(DB ? 2 : 1) * EWP];
     double* vals = vals_mem;
+    // DMA: raw staging image of the next interior extended tile (lane-linear 1-KB pieces)
+    constexpr int NDMA = (NP2 + 63) / 64;                    // 1-KB DMA instructions per tile
+    __shared__ __attribute__((aligned(16))) double stg_mem[DMA ? NDMA * 128 : 2];
     __shared__ unsigned long long mask[NW];
     __shared__ int lastUpTo[NW];           // last valid E-position in words <= w (-1: none)
     __shared__ int firstFrom[NW];          // first valid E-position in words >= w (kBig: none)
@@ -279,6 +287,27 @@ __global__ __launch_bounds__(NTH, DB ? 2 : STS_TILE_WGS) void tile_kernel(TileAr
     do {                                                                                    \
         R0 = R1 = R2 = R3 = R4 = R5 = R6 = R7 = R8 = make_double2(0.0, 0.0);                \
     } while (0)
+// DMA: wave w issues the 1-KB pieces m = w, w + kWaves, ... of interior tile kk into the
+// staging image (pieces past the tile read its first piece into the image's tail)
+#define STS_DMA_ISSUE(kk)                                                                   \
+    do {                                                                                    \
+        const double* s0_ = src + ((kk) * TW - kHB);                                        \
+        for (int m_ = wave; m_ < NDMA; m_ += kWaves) {                                      \
+            const int q2_ = m_ * 64 + lane;                                                 \
+            glds16(s0_ + 2 * (q2_ < NP2 ? q2_ : 0), lds_addr(stg_mem) + (unsigned)(m_ << 10)); \
+        }                                                                                   \
+    } while (0)
+#define STS_DMA_TAKE()                                                                      \
+    do {                                                                                    \
+        const double2* g2_ = reinterpret_cast<const double2*>(stg_mem);                     \
+        STS_TK1(0) STS_TK1(1) STS_TK1(2) STS_TK1(3) STS_TK1(4)                              \
+        STS_TK1(5) STS_TK1(6) STS_TK1(7) STS_TK1(8)                                         \
+    } while (0)
+#define STS_TK1(j)                                                                          \
+    if constexpr (j < RPT) {                                                                \
+        const int q2_ = tid + j * kThreads;                                                 \
+        R##j = g2_[q2_ < NP2 ? q2_ : NP2 - 1];                                              \
+    }
 #define STS_ST1(j)                                                                          \
     if constexpr (j < RPT) {                                                                \
         const int q2_ = tid + j * kThreads;                                                 \
@@ -295,11 +324,25 @@ __global__ __launch_bounds__(NTH, DB ? 2 : STS_TILE_WGS) void tile_kernel(TileAr
     unsigned long long st_prev = __builtin_amdgcn_s_memtime();
 #endif
     bool have = interior(k_begin);
-    if (have) STS_ISSUE(k_begin);
-    else STS_CLEAR();
+    if constexpr (DMA) {
+        if (have) STS_DMA_ISSUE(k_begin);
+        STS_CLEAR();
+    } else {
+        if (have) STS_ISSUE(k_begin);
+        else STS_CLEAR();
+    }
     // ACF shift (sts_acf.hpp: median of 64 raw samples of the series), computed once per
     // series by acf_shift_kernel before this launch: a scalar load
-    const double c0 = (NT > 0) ? a.shift[s] : 0.0;
+    // (made wave-uniform in SGPRs here: a VGPR load result used inside the tile loop gets a
+    // vmcnt(0) at its use in every tile, which would also wait for the next tile's DMA)
+    const double c0 = [&] {
+        if constexpr (NT == 0) return 0.0;
+        const double v = a.shift[s];
+        const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
+        const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)u);
+        const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(u >> 32));
+        return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
+    }();
 
     // ---- lag products on MFMA (§ header) for chunks [FROM, TO) of this wave's CPW chunks of a
     //      tile whose y sits in buffer vb; chunk order (and so the accumulation order) is the
@@ -431,6 +474,12 @@ __global__ __launch_bounds__(NTH, DB ? 2 : STS_TILE_WGS) void tile_kernel(TileAr
         //      wave v holds steps 128v + 512j + 2*lane (+1), i.e. words 2v + 8j and 2v + 8j + 1
         //      as an even/odd bit interleave ----
         if (have) {
+            if constexpr (DMA) {
+                // every wave's pieces have landed (own DMA waited, then the barrier for the others)
+                dma_wait();
+                lds_barrier();
+                STS_DMA_TAKE();
+            }
             double2* v2_ = reinterpret_cast<double2*>(vals);
             STS_ST1(0) STS_ST1(1) STS_ST1(2) STS_ST1(3) STS_ST1(4) STS_ST1(5) STS_ST1(6) STS_ST1(7) STS_ST1(8)
 #define STS_BAL1(j)                                                                         \
@@ -456,6 +505,11 @@ __global__ __launch_bounds__(NTH, DB ? 2 : STS_TILE_WGS) void tile_kernel(TileAr
         STAMP(0);
         lds_barrier();
         STAMP(1);
+        // DMA: the staging image is free again (every thread took its pieces before the
+        // barrier): the next tile streams in during this whole tile
+        if constexpr (DMA) {
+            if (have_next) STS_DMA_ISSUE(k + 1);
+        }
 #if STS_EARLY
         // A/B: the next tile's loads right after this tile's registers are in LDS
         if constexpr (STS_EARLY == 2 || NT == 0) {
@@ -792,7 +846,8 @@ __global__ __launch_bounds__(NTH, DB ? 2 : STS_TILE_WGS) void tile_kernel(TileAr
         if constexpr (!(STS_EARLY == 2 || NT == 0))
 #endif
         {
-            if (have_next) STS_ISSUE(k + 1);   // in flight during the MFMA phase of tile k
+            if constexpr (DMA) STS_CLEAR();
+            else if (have_next) STS_ISSUE(k + 1);   // in flight during the MFMA phase of tile k
             else STS_CLEAR();
         }
         STAMP(8);
@@ -827,6 +882,9 @@ __global__ __launch_bounds__(NTH, DB ? 2 : STS_TILE_WGS) void tile_kernel(TileAr
     }
     vals = vals_mem;
 #undef STS_ISSUE
+#undef STS_DMA_ISSUE
+#undef STS_DMA_TAKE
+#undef STS_TK1
 #undef STS_LD1
 #undef STS_ST1
 #undef STS_CLEAR
@@ -982,9 +1040,9 @@ hipError_t launch_tile(int method, int tw, const TileArgs& a, hipStream_t st) {
         else hipLaunchKernelGGL((tile_kernel<2048, 4, true, kThreads / 2>), grid, dim3(kThreads / 2), 0, st, a, method);
 #endif
     } else if (tw == 4096) {
-        if (a.K == 0) hipLaunchKernelGGL((tile_kernel<4096, 0, false, kThreads>), grid, block, 0, st, a, method);
-        else if (a.K <= 24) hipLaunchKernelGGL((tile_kernel<4096, 2, true, kThreads, STS_TILE_DB>), grid, block, 0, st, a, method);
-        else if (a.K <= 60) hipLaunchKernelGGL((tile_kernel<4096, 4, true, kThreads, STS_TILE_DB>), grid, block, 0, st, a, method);
+        if (a.K == 0) hipLaunchKernelGGL((tile_kernel<4096, 0, false, kThreads, false, STS_TILE_DMA>), grid, block, 0, st, a, method);
+        else if (a.K <= 24) hipLaunchKernelGGL((tile_kernel<4096, 2, true, kThreads, STS_TILE_DB, STS_TILE_DMA>), grid, block, 0, st, a, method);
+        else if (a.K <= 60) hipLaunchKernelGGL((tile_kernel<4096, 4, true, kThreads, STS_TILE_DB, STS_TILE_DMA>), grid, block, 0, st, a, method);
         else if (a.K <= 63) hipLaunchKernelGGL((tile_kernel<4096, 5, false, kThreads>), grid, block, 0, st, a, method);
         else return hipErrorInvalidValue;
     } else {
