@@ -366,17 +366,18 @@ def staging_leg(args, lib, x, out, smooth, S, T):
 
 def measured_traffic(workload, S, T):
     """HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC passes
-    (profiles/<round>_c3_traffic.json, written by tools/collect.py from separate FETCH_SIZE
-    / WRITE_SIZE passes over this same default workload); None when no pass covers it."""
+    (profiles/<round>_<workload>_traffic.json, written by tools/collect.py from separate
+    FETCH_SIZE / WRITE_SIZE passes over this same workload at its default shape); None when no
+    pass covers it."""
     import glob
-    if workload != "c3" or (S, T) != WORKLOADS["c3"][:2]:
+    if workload not in WORKLOADS or (S, T) != WORKLOADS[workload][:2]:
         return None
     import re
 
     def version(path):   # r01_v11 after r01_v7: numeric, not lexical, order
         return tuple(int(n) for n in re.findall(r"\d+", os.path.basename(path)))
 
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_c3_traffic.json")), key=version)
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_%s_traffic.json" % workload)), key=version)
     if not files:
         return None
     with open(files[-1]) as f:

@@ -3,9 +3,9 @@
     python tools/collect.py TAG
 
 * gpurun_out/bench_<wl>.log          -> profiles/<TAG>_bench_<wl>.json   (the bench JSON line)
-* gpurun_out/prof_c3/*kernel_stats.csv -> profiles/<TAG>_c3_kernel_stats.csv (rocprofv3 --stats
-  of the default `python bench.py` command)
-* gpurun_out/pmc_{fetch,write}_c3/   -> profiles/<TAG>_c3_traffic.json: HBM bytes per launch of
+* gpurun_out/prof_<wl>/*kernel_stats.csv -> profiles/<TAG>_<wl>_kernel_stats.csv (rocprofv3 --stats
+  of `python bench.py [--workload wl]`)
+* gpurun_out/pmc_{fetch,write}_<wl>/ -> profiles/<TAG>_<wl>_traffic.json: HBM bytes per launch of
   the dominant kernel from separate FETCH_SIZE / WRITE_SIZE passes, corrected as
   MI355X_MICROARCH.md prescribes (FETCH_SIZE x 2 on gfx950; both in KiB).
 """
@@ -35,6 +35,10 @@ def pmc_values(d, counter, kernel=KERNEL):
 FP64_COUNTERS = ["SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_ADD_F64",
                  "SQ_INSTS_VALU_MFMA_MOPS_F64", "SQ_VALU_MFMA_BUSY_CYCLES", "GRBM_GUI_ACTIVE"]
 FP64_KERNELS = {"c3": "tile_kernel", "c4": "ar_fit_blk_kernel"}
+# dominant kernel per workload (the c3 passes are of the default `python bench.py` command;
+# c3 directories keep their round-1 names pmc_fetch_c3 / pmc_write_c3 / prof_c3)
+TRAFFIC_KERNELS = {"c3": "tile_kernel", "c1": "seg_kernel", "c2": "recur_kernel", "c4": "ar_fit_blk_kernel",
+                   "c5": "tile_kernel"}
 
 
 def collect_fp64(tag, wl):
@@ -71,22 +75,24 @@ def main():
         if lines:
             with open(os.path.join(PROF, "%s_bench_%s.json" % (tag, wl)), "w") as f:
                 f.write(lines[-1])
-    stats = glob.glob(os.path.join(OUT, "prof_c3", "*kernel_stats.csv"))
-    if stats:
-        shutil.copy(stats[0], os.path.join(PROF, "%s_c3_kernel_stats.csv" % tag))
-    fetch = pmc_values("pmc_fetch_c3", "FETCH_SIZE")
-    write = pmc_values("pmc_write_c3", "WRITE_SIZE")
-    if fetch and write:
-        rd = 2.0 * 1024.0 * sum(fetch) / len(fetch)     # gfx950: FETCH_SIZE reports half the bytes
-        wr = 1024.0 * sum(write) / len(write)
-        rec = {"kernel": KERNEL, "workload": "c3 (bench.py default shard), --steps 2 --warmup 0",
-               "launches": [len(fetch), len(write)],
-               "read_bytes_per_launch": rd, "write_bytes_per_launch": wr,
-               "traffic_bytes_per_launch": rd + wr,
-               "correction": "FETCH_SIZE (KiB) x 2 on gfx950, WRITE_SIZE (KiB) as is (MI355X_MICROARCH.md HBM)"}
-        with open(os.path.join(PROF, "%s_c3_traffic.json" % tag), "w") as f:
-            json.dump(rec, f, indent=1)
-        print(json.dumps(rec))
+    for wl in TRAFFIC_KERNELS:
+        stats = glob.glob(os.path.join(OUT, "prof_%s" % wl, "*kernel_stats.csv"))
+        if stats:
+            shutil.copy(stats[0], os.path.join(PROF, "%s_%s_kernel_stats.csv" % (tag, wl)))
+        kern = TRAFFIC_KERNELS[wl]
+        fetch = pmc_values("pmc_fetch_%s" % wl, "FETCH_SIZE", kern)
+        write = pmc_values("pmc_write_%s" % wl, "WRITE_SIZE", kern)
+        if fetch and write:
+            rd = 2.0 * 1024.0 * sum(fetch) / len(fetch)     # gfx950: FETCH_SIZE reports half the bytes
+            wr = 1024.0 * sum(write) / len(write)
+            rec = {"kernel": kern, "workload": "%s (bench.py), --steps 2 --warmup 0" % wl,
+                   "launches": [len(fetch), len(write)],
+                   "read_bytes_per_launch": rd, "write_bytes_per_launch": wr,
+                   "traffic_bytes_per_launch": rd + wr,
+                   "correction": "FETCH_SIZE (KiB) x 2 on gfx950, WRITE_SIZE (KiB) as is (MI355X_MICROARCH.md HBM)"}
+            with open(os.path.join(PROF, "%s_%s_traffic.json" % (tag, wl)), "w") as f:
+                json.dump(rec, f, indent=1)
+            print(json.dumps(rec))
     for wl in FP64_KERNELS:
         collect_fp64(tag, wl)
 
