@@ -264,6 +264,35 @@ __device__ __forceinline__ double wave_sum(double v) {
     return v;
 }
 
+// Cross-lane moves without the LDS crossbar (ds_bpermute: ~100+ cycles each, and the
+// register kernel's sums and its lane-parallel Cholesky are chains of them): DPP for the
+// in-row steps and the one-lane shift, v_readlane for broadcasts from a known lane.
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double v) {
+    const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)(unsigned)u, CTRL, 0xf, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(unsigned)(u >> 32), CTRL, 0xf, 0xf, false);
+    return __builtin_bit_cast(double, ((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
+}
+__device__ __forceinline__ double lane_bcast(double v, int l) {
+    const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
+    const unsigned lo = __builtin_amdgcn_readlane((unsigned)u, l);
+    const unsigned hi = __builtin_amdgcn_readlane((unsigned)(u >> 32), l);
+    return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
+}
+// sum over the wave, the same bits in every lane: quad butterfly (quad_perm [1,0,3,2],
+// [2,3,0,1]), row rotations by 4 and 8 (every lane then holds its row's sum), then the four
+// row sums from lanes 0 / 16 / 32 / 48 in a fixed order
+__device__ __forceinline__ double wave_sum_dpp(double v) {
+    v = v + dpp_d<0xB1>(v);
+    v = v + dpp_d<0x4E>(v);
+    v = v + dpp_d<0x124>(v);
+    v = v + dpp_d<0x128>(v);
+    return (lane_bcast(v, 0) + lane_bcast(v, 16)) + (lane_bcast(v, 32) + lane_bcast(v, 48));
+}
+// lane l - 1's value (wave_shr:1; lane 0 gets 0)
+__device__ __forceinline__ double lane_prev(double v) { return dpp_d<0x138>(v); }
+
 #ifdef STS_STAMPS
 __device__ unsigned long long g_ar_stamps[16];
 #define AR_STAMP(i)                                                                          \
@@ -365,14 +394,14 @@ __global__ __launch_bounds__(64 * NWV, STS_AR_WAVES_PER_EU) void ar_fit_blk_kern
     double part = 0.0;
 #pragma unroll
     for (int j = 0; j < B; j++) part += x[j];
-    part = wave_sum(part);
+    part = wave_sum_dpp(part);
     const double mu = intercept ? part / (double)T : 0.0;
     AR_STAMP(0);
     // the previous lane's last P raw values (0 before the series)
     double xp[P + 1];
 #pragma unroll
     for (int k = 1; k <= P; k++) {
-        const double v = __shfl_up(x[B - k], 1);
+        const double v = lane_prev(x[B - k]);
         xp[k] = (lane > 0) ? v : 0.0;
     }
     // y at block offset j - k (k >= 1 may reach into the previous lane's block)
@@ -412,9 +441,9 @@ __global__ __launch_bounds__(64 * NWV, STS_AR_WAVES_PER_EU) void ar_fit_blk_kern
         }
     }
     AR_STAMP(1);
-    sy = wave_sum(sy);
+    sy = wave_sum_dpp(sy);
 #pragma unroll
-    for (int d = 0; d <= P; d++) Pd[d] = wave_sum(Pd[d]);
+    for (int d = 0; d <= P; d++) Pd[d] = wave_sum_dpp(Pd[d]);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
@@ -446,20 +475,20 @@ __global__ __launch_bounds__(64 * NWV, STS_AR_WAVES_PER_EU) void ar_fit_blk_kern
     // ---- centred normal equations (intercept eliminated); rhs_j = row[0] ----
     if (intercept) {
 #pragma unroll
-        for (int k = 0; k <= P; k++) row[k] -= csj * __shfl(csj, k) / fm;
+        for (int k = 0; k <= P; k++) row[k] -= csj * lane_bcast(csj, k) / fm;
     }
     // ---- Cholesky of the 1..P block, lane-parallel (lane i owns row i of L) ----
     bool ok = true;
 #pragma unroll
     for (int j = 1; j <= P; j++) {
-        const double djj = __shfl(row[j], j);
+        const double djj = lane_bcast(row[j], j);
         ok = ok && (djj > 0.0);
         const double l = __builtin_sqrt(djj);
         if (lane == j) row[j] = l;
         else if (lane > j) row[j] = row[j] / l;
 #pragma unroll
         for (int k = j + 1; k <= P; k++) {
-            const double lkj = __shfl(row[j], k);
+            const double lkj = lane_bcast(row[j], k);
             if (lane >= k) row[k] -= row[j] * lkj;
         }
     }
@@ -491,7 +520,7 @@ __global__ __launch_bounds__(64 * NWV, STS_AR_WAVES_PER_EU) void ar_fit_blk_kern
     double phi[P + 1];
     phi[0] = 0.0;
 #pragma unroll
-    for (int i = 1; i <= P; i++) phi[i] = __shfl(row[0], i);
+    for (int i = 1; i <= P; i++) phi[i] = lane_bcast(row[0], i);
     const int status = (!bad && !ok) ? STS_ERR_SINGULAR : STS_OK;
     double cpr = 0.0;
     if (!bad && ok) {
@@ -543,7 +572,7 @@ __global__ __launch_bounds__(64 * NWV, STS_AR_WAVES_PER_EU) void ar_fit_blk_kern
         }
         AR_STAMP(4);
 #pragma unroll
-        for (int k = 0; k <= P; k++) g[k] = wave_sum(g[k]);
+        for (int k = 0; k <= P; k++) g[k] = wave_sum_dpp(g[k]);
         double z[P + 1];
         const double g0 = g[0];
 #pragma unroll
