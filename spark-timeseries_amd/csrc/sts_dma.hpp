@@ -21,6 +21,7 @@ __device__ __forceinline__ unsigned lds_addr(const void* p) {
 // for the DMA itself (dma_wait).  M0 holds the LDS base; it is restored.
 __device__ __forceinline__ void glds16(const double* gsrc, unsigned lds_byte_addr) {
     unsigned keep;
+    lds_byte_addr = __builtin_amdgcn_readfirstlane(lds_byte_addr);   // wave-uniform: pin it to an SGPR
     asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
                  : "=&s"(keep)
                  : "v"(gsrc), "s"(lds_byte_addr)
