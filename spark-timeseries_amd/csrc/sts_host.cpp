@@ -30,8 +30,18 @@
 
 namespace {
 
-constexpr int kSlots = 3;
-constexpr size_t kChunkBytes = size_t(64) << 20;   // device bytes (in + out) per chunk
+// Pipeline shape (A/B on C2 from pinned host memory, profiles/r02_v6_ab_staging.jsonl): 2-D
+// copies on 5 slots 78 ms per call, 3 slots 87 ms, 4 slots 94 ms; linear copies for
+// contiguous rows were bimodal run to run (56-112 ms), so the 2-D form stays.
+#ifndef STS_STAGE_LINEAR
+#define STS_STAGE_LINEAR 0
+#endif
+#ifndef STS_STAGE_SLOTS
+#define STS_STAGE_SLOTS 5
+#define STS_STAGE_MB 64
+#endif
+constexpr int kSlots = STS_STAGE_SLOTS;
+constexpr size_t kChunkBytes = size_t(STS_STAGE_MB) << 20;   // device bytes (in + out) per chunk
 constexpr size_t kAlign = 256;
 
 size_t align_up(size_t b) { return (b + kAlign - 1) / kAlign * kAlign; }
@@ -233,7 +243,10 @@ int staged(int64_t S, std::vector<Arg> args, const Kernel& kern) {
         for (Arg& x : args) {
             if (!x.src) continue;
             const size_t n = x.row * (size_t)sl.ns;
-            if (x.pinned_src)
+            if (STS_STAGE_LINEAR && x.pinned_src && x.hstride == x.row)   // contiguous rows: one linear copy
+                e = hipMemcpyAsync(dev + x.dev_off, static_cast<const char*>(x.src) + (size_t)sl.s0 * x.hstride, n,
+                                   hipMemcpyHostToDevice, sl.st);
+            else if (x.pinned_src)
                 e = hipMemcpy2DAsync(dev + x.dev_off, x.row, static_cast<const char*>(x.src) + (size_t)sl.s0 * x.hstride,
                                      x.hstride, x.row, (size_t)sl.ns, hipMemcpyHostToDevice, sl.st);
             else
@@ -250,7 +263,10 @@ int staged(int64_t S, std::vector<Arg> args, const Kernel& kern) {
         for (Arg& x : args) {
             if (!x.dst || status != STS_OK) continue;
             const size_t n = x.row * (size_t)sl.ns;
-            if (x.pinned_dst)
+            if (STS_STAGE_LINEAR && x.pinned_dst && x.hstride == x.row)
+                e = hipMemcpyAsync(static_cast<char*>(x.dst) + (size_t)sl.s0 * x.hstride, dev + x.dev_off, n,
+                                   hipMemcpyDeviceToHost, sl.st);
+            else if (x.pinned_dst)
                 e = hipMemcpy2DAsync(static_cast<char*>(x.dst) + (size_t)sl.s0 * x.hstride, x.hstride, dev + x.dev_off,
                                      x.row, x.row, (size_t)sl.ns, hipMemcpyDeviceToHost, sl.st);
             else
