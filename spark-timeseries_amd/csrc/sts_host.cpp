@@ -4,7 +4,7 @@
 // A `_host` call is split by series into chunks of ~kChunkBytes of device traffic.  Each
 // chunk runs H2D -> kernel(s) -> D2H on one of kSlots slots, each slot owning a HIP stream,
 // a device buffer and pinned bounce buffers, all reused across calls.  While chunk i's
-// kernel runs, chunk i+1 uploads and chunk i-1 downloads (three streams), and the calling
+// kernel runs, later chunks upload and earlier ones download (one stream per slot), and the calling
 // thread fills the next slot's bounce buffer: copy, compute and the CPU side overlap.
 //
 // Host memory that is already pinned (hipHostMalloc'd, e.g. by sts_host_alloc -- the JNI
