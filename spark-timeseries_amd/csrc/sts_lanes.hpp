@@ -1,0 +1,36 @@
+// sts_lanes.hpp -- cross-lane moves of doubles without the LDS crossbar, for the kernels whose
+// reductions / broadcasts sit on dependency chains (sts_ar.hip, sts_seg.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+
+namespace sts {
+
+// ds_bpermute (what __shfl / __shfl_xor compile to) costs an LDS round trip (~100+ cycles);
+// DPP covers the in-row steps and the one-lane shift, v_readlane broadcasts from a known lane.
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double v) {
+    const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)(unsigned)u, CTRL, 0xf, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(unsigned)(u >> 32), CTRL, 0xf, 0xf, false);
+    return __builtin_bit_cast(double, ((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
+}
+__device__ __forceinline__ double lane_bcast(double v, int l) {
+    const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
+    const unsigned lo = __builtin_amdgcn_readlane((unsigned)u, l);
+    const unsigned hi = __builtin_amdgcn_readlane((unsigned)(u >> 32), l);
+    return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
+}
+// sum over the wave, the same bits in every lane: quad butterfly (quad_perm [1,0,3,2],
+// [2,3,0,1]), row rotations by 4 and 8 (every lane then holds its row's sum), then the four
+// row sums from lanes 0 / 16 / 32 / 48 in a fixed order
+__device__ __forceinline__ double wave_sum_dpp(double v) {
+    v = v + dpp_d<0xB1>(v);
+    v = v + dpp_d<0x4E>(v);
+    v = v + dpp_d<0x124>(v);
+    v = v + dpp_d<0x128>(v);
+    return (lane_bcast(v, 0) + lane_bcast(v, 16)) + (lane_bcast(v, 32) + lane_bcast(v, 48));
+}
+// lane l - 1's value (wave_shr:1; lane 0 gets 0)
+__device__ __forceinline__ double lane_prev(double v) { return dpp_d<0x138>(v); }
+
+}  // namespace sts

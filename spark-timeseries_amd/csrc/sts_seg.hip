@@ -41,6 +41,7 @@
 #include "sts_internal.hpp"
 #include "sts_acf.hpp"
 #include "sts_scan.hpp"
+#include "sts_lanes.hpp"
 
 #include <hip/hip_runtime.h>
 
@@ -601,12 +602,7 @@ __global__ __launch_bounds__(256, 4) void seg_kernel(TileArgs a, int method) {
             const int i = 16 * (j / Q) + (16 - Q) + (j % Q) - lane;
             if (i >= 0 && i < 16) lagacc += scr[i * 16 + j];
         }
-        double sm = st.sm, qm = st.qm;
-#pragma unroll
-        for (int d = 32; d >= 1; d >>= 1) {
-            sm += __shfl_xor(sm, d);
-            qm += __shfl_xor(qm, d);
-        }
+        const double sm = wave_sum_dpp(st.sm), qm = wave_sum_dpp(st.qm);
         if (a.acf_fused == nullptr) {
             double* part = a.partials + unit * kPartStride;
             part[lane] = lagacc;
@@ -626,9 +622,8 @@ __global__ __launch_bounds__(256, 4) void seg_kernel(TileArgs a, int method) {
             const double* tail = tail_base;   // y of the last tile, indexed by series position - kb_last
             const double r = acf_combine(
                 Pi, Sm, Qm, i, T,
-                [&](int j) {
-                    const double hx = __shfl(head.x, j >> 1), hy = __shfl(head.y, j >> 1);
-                    return (j & 1) ? hy : hx;
+                [&](int j) {   // j is wave-uniform: a scalar lane select, not an LDS-crossbar shuffle
+                    return readlane_d((j & 1) ? head.y : head.x, j >> 1);
                 },
                 [&](int j) { return tail[T - 1 - j - kb_last]; });
             if (lane < K) a.acf_fused[s * K + lane] = r;
