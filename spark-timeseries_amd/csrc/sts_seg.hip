@@ -54,6 +54,10 @@ typedef double d4 __attribute__((ext_vector_type(4)));
 // native vector (HIP's double2 is a struct: arrays of it are not promoted to registers)
 typedef double v2d __attribute__((ext_vector_type(2)));
 
+#ifndef STS_SEG_VTAB
+#define STS_SEG_VTAB 1                // word tables lane-parallel (DPP scans) instead of a scalar loop
+#endif
+
 constexpr int kW = 512;               // steps per tile
 constexpr int kWords = kW / 64;       // validity words per tile
 constexpr int kRing = 2 * kW + 128;   // two slots + a mirror of slot 0's head
@@ -227,6 +231,52 @@ __device__ __forceinline__ void impute_tile(WaveLds& w, const double* src, doubl
     const bool needN = (method == STS_FILL_LINEAR || method == STS_FILL_NEXT || method == STS_FILL_NEAREST);
     const int tend = (kb + kW < T) ? kb + kW : T;     // end of the real steps of this tile
     if (method != STS_FILL_NONE) {
+#if STS_SEG_VTAB
+        // ---- word tables, lane-parallel: lane i < kWords owns word i (DPP scans within row 0,
+        //      v_readlane for the few values every lane needs) ----
+        const int wl = lane & (kWords - 1);
+        const unsigned long long m = w.m2[SLOT][wl];
+        const bool own_w = lane < kWords;
+        const int gbase = kb + 64 * wl;
+        const int hiw = tend - gbase;                       // real steps of word wl: bits [0, hiw)
+        unsigned long long r = 0ull;
+        if (own_w && hiw > 0) {
+            r = ~m;
+            if (hiw < 64) r &= (1ull << hiw) - 1ull;
+        }
+        const int cnt = __popcll(r);
+        int incl = cnt;                                     // inclusive prefix count over words
+        incl += __builtin_amdgcn_update_dpp(0, incl, 0x111, 0xf, 0xf, false);
+        incl += __builtin_amdgcn_update_dpp(0, incl, 0x112, 0xf, 0xf, false);
+        incl += __builtin_amdgcn_update_dpp(0, incl, 0x114, 0xf, 0xf, false);
+        const int excl = incl - cnt;
+        int lvw = (own_w && m) ? gbase + 63 - __clzll(m) : -1;   // last valid index in words <= wl
+        lvw = max(lvw, __builtin_amdgcn_update_dpp(-1, lvw, 0x111, 0xf, 0xf, false));
+        lvw = max(lvw, __builtin_amdgcn_update_dpp(-1, lvw, 0x112, 0xf, 0xf, false));
+        lvw = max(lvw, __builtin_amdgcn_update_dpp(-1, lvw, 0x114, 0xf, 0xf, false));
+        const int runw = max(lvw, st.Lc);
+        int lnw = r ? gbase + 63 - __clzll(r) : -1;         // last NaN to impute in words <= wl
+        lnw = max(lnw, __builtin_amdgcn_update_dpp(-1, lnw, 0x111, 0xf, 0xf, false));
+        lnw = max(lnw, __builtin_amdgcn_update_dpp(-1, lnw, 0x112, 0xf, 0xf, false));
+        lnw = max(lnw, __builtin_amdgcn_update_dpp(-1, lnw, 0x114, 0xf, 0xf, false));
+        bool lg = false;   // linear: can a step lie more than kLongRun past its last valid index?
+        if (method == STS_FILL_LINEAR) {   // (conservative, as in sts_tile.hip)
+            const int tz = m ? __ffsll(m) - 1 : 64;
+            lg = __ballot(own_w && (__popcll(~m) > kLongRun / 2 ||
+                                    (lane == 0 && tz > 0 && kb + tz - 1 - st.Lc > kLongRun))) != 0ull;
+        }
+        if (own_w) {
+            w.need[lane] = r;
+            w.lastUp[lane] = runw;
+            w.wbase[lane] = excl;
+        }
+        int wb[kWords + 1];
+#pragma unroll
+        for (int i = 0; i < kWords; i++) wb[i] = __builtin_amdgcn_readlane(excl, i);
+        wb[kWords] = __builtin_amdgcn_readlane(incl, kWords - 1);
+        const int run = __builtin_amdgcn_readlane(runw, kWords - 1);
+        const int lastneed = __builtin_amdgcn_readlane(lnw, kWords - 1);
+#else
         // ---- word tables (wave-uniform scalars, short-lived) ----
         int wb[kWords + 1];
         int run = st.Lc, lastneed = -1;
@@ -256,6 +306,7 @@ __device__ __forceinline__ void impute_tile(WaveLds& w, const double* src, doubl
                 w.wbase[i] = wb[i];
             }
         }
+#endif
         const int lastv = (run >= kb) ? run : -1;     // last valid index in this tile
         const int nnan = wb[kWords];
         if (nnan > 0) {
@@ -278,6 +329,13 @@ __device__ __forceinline__ void impute_tile(WaveLds& w, const double* src, doubl
                         f = T;
                     }
                 }
+#if STS_SEG_VTAB
+                int fw = (own_w && m) ? gbase + __ffsll(m) - 1 : kBig;   // first valid in words >= wl
+                fw = min(fw, __builtin_amdgcn_update_dpp(kBig, fw, 0x101, 0xf, 0xf, false));
+                fw = min(fw, __builtin_amdgcn_update_dpp(kBig, fw, 0x102, 0xf, 0xf, false));
+                fw = min(fw, __builtin_amdgcn_update_dpp(kBig, fw, 0x104, 0xf, 0xf, false));
+                if (own_w) w.firstFrom[lane] = min(fw, f);
+#else
                 int ff = f;
 #pragma unroll
                 for (int i = kWords - 1; i >= 0; i--) {
@@ -285,6 +343,7 @@ __device__ __forceinline__ void impute_tile(WaveLds& w, const double* src, doubl
                     if (m) ff = kb + 64 * i + __ffsll(m) - 1;
                     if (lane == 0) w.firstFrom[i] = ff;
                 }
+#endif
             }
             wave_sync();
             // ---- impute the compacted NaN positions; F goes into the ring in place
