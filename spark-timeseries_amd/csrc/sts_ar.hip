@@ -259,12 +259,6 @@ __global__ __launch_bounds__(64) void ar_fit_kernel(ArArgs a, int NT) {
 constexpr int kRegPB = 8;             // p <= kRegPB
 constexpr int kRegWaves = 4;
 
-__device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d);
-    return v;
-}
-
 #ifdef STS_STAMPS
 __device__ unsigned long long g_ar_stamps[16];
 #define AR_STAMP(i)                                                                          \
