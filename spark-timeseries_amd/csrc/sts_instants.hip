@@ -16,6 +16,19 @@
 
 #include <hip/hip_runtime.h>
 
+#ifndef STS_TR16
+#define STS_TR16 1                    // 16-B transpose when shapes allow
+#endif
+#ifndef STS_NAN16
+#define STS_NAN16 1                   // 16-B NaN-instant scan when shapes allow
+#endif
+#ifndef STS_STATS_FAST
+#define STS_STATS_FAST 1              // seriesStats division off the step chain (see stats_fast_kernel)
+#endif
+#ifndef STS_STATS_CH
+#define STS_STATS_CH 16               // seriesStats chunk (steps staged per series)
+#endif
+
 namespace sts {
 namespace {
 
@@ -87,6 +100,103 @@ __global__ __launch_bounds__(64) void stats_kernel(const double* __restrict__ in
     }
 }
 
+// Branch-free forms of jmax / jmin (same results, selects instead of early returns).
+__device__ __forceinline__ double jmax_sel(double a, double b) {
+    double r = (a >= b) ? a : b;
+    r = (a == 0.0 && b == 0.0 && __builtin_signbit(a)) ? b : r;
+    return (a != a) ? a : r;
+}
+__device__ __forceinline__ double jmin_sel(double a, double b) {
+    double r = (a <= b) ? a : b;
+    r = (a == 0.0 && b == 0.0 && __builtin_signbit(b)) ? b : r;
+    return (a != a) ? a : r;
+}
+
+// The same StatCounter with the Welford division delta / n taken off the per-step chain.
+// The compiler's IEEE f64 division is a Markstein sequence: y = 1/b refined by two Newton
+// steps from v_rcp_f64 (a function of b alone), q0 = a y, r = fma(-b, q0, a), q = fma(r, y,
+// q0), with v_div_scale / v_div_fmas / v_div_fixup scaling or patching only when the operands'
+// exponents are extreme or a is 0 / inf / NaN.  b = n here is the step count, the same in
+// every lane, so y(n) and -n for a chunk's steps are computed once into LDS (lane c: step
+// c) and broadcast; a lane whose delta lies outside [2^-900, 2^700] (or is inf / NaN)
+// takes the library division instead, so every quotient has the division's bits
+// (tests/test_parity_gpu.py::test_series_stats* include the extreme and special values).
+__device__ __forceinline__ double newton_rcp(double b) {
+    double y = __builtin_amdgcn_rcp(b);
+    double e = __builtin_fma(-b, y, 1.0);
+    y = __builtin_fma(y, e, y);
+    e = __builtin_fma(-b, y, 1.0);
+    return __builtin_fma(y, e, y);
+}
+
+template <int SPW, int CH>
+__global__ __launch_bounds__(64) void stats_fast_kernel(const double* __restrict__ in, double* __restrict__ out,
+                                                        int64_t S, int64_t T, int64_t ld) {
+    constexpr int kRow = CH + 1;
+    constexpr int NLD = SPW * CH / 64;
+    static_assert(CH <= 64, "one lane per step of the reciprocal table");
+    __shared__ double tile[SPW * kRow];
+    __shared__ double ytab[CH], nbtab[CH];
+    const int lane = threadIdx.x;
+    const int64_t s0 = (int64_t)blockIdx.x * SPW;
+    const bool live = lane < SPW && s0 + lane < S;
+    const int ns = (S - s0 < SPW) ? (int)(S - s0) : SPW;
+    const double* base = in + s0 * ld;
+    double mu = 0.0, m2 = 0.0, mx = -__builtin_inf(), mn = __builtin_inf();
+    double pre[NLD];
+    auto fetch = [&](int64_t tc) {   // clamped loads, no branches around the prefetch registers
+#pragma unroll
+        for (int i = 0; i < NLD; i++) {
+            const int row = (i * 64 + lane) / CH, col = (i * 64 + lane) % CH;
+            const int rr = row < ns ? row : ns - 1;
+            const int64_t cc = (tc + col < T) ? tc + col : T - 1;
+            pre[i] = base[rr * ld + cc];
+        }
+    };
+    fetch(0);
+    for (int64_t tc = 0; tc < T; tc += CH) {
+        const int len = (T - tc < CH) ? (int)(T - tc) : CH;
+#pragma unroll
+        for (int i = 0; i < NLD; i++) {
+            const int row = (i * 64 + lane) / CH, col = (i * 64 + lane) % CH;
+            tile[row * kRow + col] = pre[i];
+        }
+        if (lane < CH) {
+            const double n = (double)(tc + lane + 1);   // exact (T < 2^53)
+            ytab[lane] = newton_rcp(n);
+            nbtab[lane] = -n;
+        }
+        if (tc + CH < T) fetch(tc + CH);
+        __syncthreads();
+        if (live) {
+            const double* row = tile + lane * kRow;
+            for (int c = 0; c < len; c++) {
+                const double v = row[c];
+                const double y = ytab[c], nb = nbtab[c];
+                const double delta = v - mu;            // StatCounter.merge(value)
+                const double ad = __builtin_fabs(delta);
+                const double q0 = delta * y;
+                const double r = __builtin_fma(nb, q0, delta);
+                double q = __builtin_fma(r, y, q0);
+                q = (ad == 0.0) ? delta : q;            // 0 / n = 0 with the sign of delta
+                if (!(ad == 0.0 || (ad >= 0x1p-900 && ad <= 0x1p700))) q = delta / (-nb);
+                mu += q;
+                m2 += delta * (v - mu);
+                mx = jmax_sel(mx, v);
+                mn = jmin_sel(mn, v);
+            }
+        }
+        __syncthreads();
+    }
+    if (live) {
+        double* o = out + (s0 + lane) * 4;
+        o[0] = mu;
+        o[1] = m2;
+        o[2] = mx;
+        o[3] = mn;
+    }
+}
+
 // flags[t] = 1 if any series of the panel is NaN at instant t (flags are only ever SET,
 // so partial panels, other ranks and repeated calls combine by OR / max).
 constexpr int kNanT = 256;
@@ -102,6 +212,27 @@ __global__ __launch_bounds__(kNanT) void nan_instants_kernel(const double* __res
 #pragma unroll 8
     for (int64_t s = sa; s < sb; s++, p += ld) any |= __builtin_isnan(*p);
     if (any) flags[t] = 1;
+}
+
+// The same scan with 16-B loads (T and ld even, 16-B aligned panel): a lane tests two
+// consecutive instants of each series, every load instruction covering 1 KB of a row.
+__global__ __launch_bounds__(kNanT) void nan_instants16_kernel(const double* __restrict__ in, uint8_t* flags,
+                                                               int64_t S, int64_t T, int64_t ld) {
+    typedef double v2n __attribute__((ext_vector_type(2)));
+    const int64_t t = 2 * ((int64_t)blockIdx.x * kNanT + threadIdx.x);
+    const int64_t sa = (int64_t)blockIdx.y * kNanSeries;
+    const int64_t sb = (sa + kNanSeries < S) ? sa + kNanSeries : S;
+    if (t >= T) return;
+    bool a0 = false, a1 = false;
+    const double* p = in + sa * ld + t;
+#pragma unroll 8
+    for (int64_t s = sa; s < sb; s++, p += ld) {
+        const v2n v = *reinterpret_cast<const v2n*>(p);
+        a0 |= __builtin_isnan(v.x);
+        a1 |= __builtin_isnan(v.y);
+    }
+    if (a0) flags[t] = 1;
+    if (a1) flags[t + 1] = 1;
 }
 
 // active-instant compaction: block b counts the zero flags of its kCompact instants
@@ -165,13 +296,19 @@ __global__ __launch_bounds__(256) void write_active_kernel(const uint8_t* flags,
     }
 }
 
-// out[s, j] = in[s, active[j]], j < n_active
-__global__ __launch_bounds__(256) void gather_instants_kernel(const double* __restrict__ in, double* __restrict__ out,
-                                                              const int64_t* __restrict__ active, int64_t n_active,
-                                                              int64_t ld_in, int64_t ld_out) {
-    const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    const int64_t s = blockIdx.y;
-    if (j < n_active) out[s * ld_out + j] = in[s * ld_in + active[j]];
+// out[s, j] = in[s, active[j]], j < n_active: one wave per series row (4 rows per block), so a
+// short row (a few hundred kept instants) does not leave most of a 256-wide block idle
+constexpr int kGatherRows = 4;
+__global__ __launch_bounds__(64 * kGatherRows) void gather_instants_kernel(const double* __restrict__ in,
+                                                                           double* __restrict__ out,
+                                                                           const int64_t* __restrict__ active,
+                                                                           int64_t n_active, int64_t S, int64_t ld_in,
+                                                                           int64_t ld_out) {
+    const int64_t s = (int64_t)blockIdx.x * kGatherRows + (threadIdx.x >> 6);
+    if (s >= S) return;
+    const double* src = in + s * ld_in;
+    double* dst = out + s * ld_out;
+    for (int64_t j = threadIdx.x & 63; j < n_active; j += 64) dst[j] = src[active[j]];
 }
 
 // toInstants: out[t, s] = in[s, t] (T x S, instant-major), 64 x 64 tiles through LDS
@@ -191,13 +328,52 @@ __global__ __launch_bounds__(256) void transpose_kernel(const double* __restrict
     }
 }
 
+// The same with 16-B accesses (T, S, both leading dimensions even, 16-B aligned panels): a
+// lane moves two consecutive instants of a series in and two consecutive series of an instant
+// out, every load and store instruction covering 2 x 512 B.  The tile is kept t-major with
+// an odd pitch, so the column reads of the store phase spread over the banks.
+typedef double v2t __attribute__((ext_vector_type(2)));
+constexpr int kTrPitch = 64 + 1;
+__global__ __launch_bounds__(256) void transpose16_kernel(const double* __restrict__ in, double* __restrict__ out,
+                                                          int64_t S, int64_t T, int64_t ld_in, int64_t ld_out) {
+    __shared__ double tile[64 * kTrPitch];   // tile[t * pitch + s]
+    const int64_t t0 = (int64_t)blockIdx.x * 64, s0 = (int64_t)blockIdx.y * 64;
+    const int p = threadIdx.x & 31, r0 = threadIdx.x >> 5;   // pair p, row r0 + 8 i
+    v2t v[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        const int64_t s = s0 + r0 + 8 * i, t = t0 + 2 * p;
+        v[i] = (s < S && t < T) ? *reinterpret_cast<const v2t*>(in + s * ld_in + t) : v2t{0.0, 0.0};
+    }
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        const int sr = r0 + 8 * i;
+        tile[(2 * p) * kTrPitch + sr] = v[i].x;
+        tile[(2 * p + 1) * kTrPitch + sr] = v[i].y;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        const int tr = r0 + 8 * i;
+        const int64_t t = t0 + tr, s = s0 + 2 * p;
+        if (s < S && t < T) {
+            const v2t o = {tile[tr * kTrPitch + 2 * p], tile[tr * kTrPitch + 2 * p + 1]};
+            *reinterpret_cast<v2t*>(out + t * ld_out + s) = o;
+        }
+    }
+}
+
 }  // namespace
 
 hipError_t launch_series_stats(const double* in, double* out, int64_t S, int64_t T, int64_t ld, hipStream_t st) {
     if (S <= 0) return hipSuccess;
-    constexpr int SPW = 64, CH = 32;   // A/B on 1M x 390: 1.00 ms vs 1.44 (32 x 64), 1.96 (16 x 64)
-    hipLaunchKernelGGL((stats_kernel<SPW, CH>), dim3((unsigned)((S + SPW - 1) / SPW)), dim3(64), 0, st, in, out, S, T,
-                       ld);
+    constexpr int SPW = 64, CH = STS_STATS_CH;   // A/B on 1M x 390: 1.00 ms vs 1.44 (32 x 64), 1.96 (16 x 64)
+    if (STS_STATS_FAST && T < (1LL << 52))
+        hipLaunchKernelGGL((stats_fast_kernel<SPW, CH>), dim3((unsigned)((S + SPW - 1) / SPW)), dim3(64), 0, st, in, out,
+                           S, T, ld);
+    else
+        hipLaunchKernelGGL((stats_kernel<SPW, CH>), dim3((unsigned)((S + SPW - 1) / SPW)), dim3(64), 0, st, in, out, S,
+                           T, ld);
     return hipGetLastError();
 }
 
@@ -211,6 +387,11 @@ hipError_t launch_nan_instants(const double* in, uint8_t* flags, int64_t S, int6
             if (e != hipSuccess) return e;
         }
         return hipSuccess;
+    }
+    if (STS_NAN16 && T % 2 == 0 && ld % 2 == 0 && reinterpret_cast<uintptr_t>(in) % 16 == 0) {
+        dim3 grid((unsigned)((T / 2 + kNanT - 1) / kNanT), (unsigned)gy);
+        hipLaunchKernelGGL(nan_instants16_kernel, grid, dim3(kNanT), 0, st, in, flags, S, T, ld);
+        return hipGetLastError();
     }
     dim3 grid((unsigned)((T + kNanT - 1) / kNanT), (unsigned)gy);
     hipLaunchKernelGGL(nan_instants_kernel, grid, dim3(kNanT), 0, st, in, flags, S, T, ld);
@@ -232,22 +413,25 @@ hipError_t launch_active_instants(const uint8_t* flags, int64_t T, int64_t* acti
 hipError_t launch_gather_instants(const double* in, double* out, const int64_t* active, int64_t n_active, int64_t S,
                                   int64_t ld_in, int64_t ld_out, hipStream_t st) {
     if (S <= 0 || n_active <= 0) return hipSuccess;
-    for (int64_t s = 0; s < S; s += 65535) {
-        const int64_t n = (S - s < 65535) ? S - s : 65535;
-        dim3 grid((unsigned)((n_active + 255) / 256), (unsigned)n);
-        hipLaunchKernelGGL(gather_instants_kernel, grid, dim3(256), 0, st, in + s * ld_in, out + s * ld_out, active,
-                           n_active, ld_in, ld_out);
-    }
+    const int64_t nblk = (S + kGatherRows - 1) / kGatherRows;
+    if (nblk > 0x7fffffffLL) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(gather_instants_kernel, dim3((unsigned)nblk), dim3(64 * kGatherRows), 0, st, in, out, active,
+                       n_active, S, ld_in, ld_out);
     return hipGetLastError();
 }
 
 hipError_t launch_transpose(const double* in, double* out, int64_t S, int64_t T, int64_t ld_in, int64_t ld_out,
                             hipStream_t st) {
     if (S <= 0 || T <= 0) return hipSuccess;
+    const bool v16 = STS_TR16 && (T % 2 == 0) && (S % 2 == 0) && (ld_in % 2 == 0) && (ld_out % 2 == 0) &&
+                     (reinterpret_cast<uintptr_t>(in) % 16 == 0) && (reinterpret_cast<uintptr_t>(out) % 16 == 0);
     for (int64_t s = 0; s < S; s += 64LL * 65535) {
         const int64_t n = (S - s < 64LL * 65535) ? S - s : 64LL * 65535;
         dim3 grid((unsigned)((T + 63) / 64), (unsigned)((n + 63) / 64));
-        hipLaunchKernelGGL(transpose_kernel, grid, dim3(256), 0, st, in + s * ld_in, out + s, n, T, ld_in, ld_out);
+        if (v16)
+            hipLaunchKernelGGL(transpose16_kernel, grid, dim3(256), 0, st, in + s * ld_in, out + s, n, T, ld_in, ld_out);
+        else
+            hipLaunchKernelGGL(transpose_kernel, grid, dim3(256), 0, st, in + s * ld_in, out + s, n, T, ld_in, ld_out);
     }
     return hipGetLastError();
 }

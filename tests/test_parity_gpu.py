@@ -803,6 +803,29 @@ def test_series_stats(torch):
         assert_bits(host(st.min()), ref[:, 3], "min")
 
 
+def test_series_stats_extremes(torch):
+    # the fast Welford division (stats_fast_kernel) against the oracle where its range check
+    # sends lanes to the library division: huge / tiny / subnormal deltas, zeros, infinities
+    from sparkts.timeseriesrdd import TimeSeriesRDD
+    rng = np.random.default_rng(22)
+    S, T = 130, 300
+    x = rng.standard_normal((S, T)) * 10.0 ** rng.integers(-300, 300, size=(S, 1))
+    x[0] = 1e-310 * rng.standard_normal(T)                     # subnormals
+    x[1] = 7.0                                                 # delta = 0 from step 2 on
+    x[2] = rng.choice([1e300, -1e300, 1e-300, 0.0, -0.0], T)   # mixed extreme magnitudes
+    x[3, ::7] = np.inf
+    x[4, 5] = -np.inf
+    x[5, 9] = NaN
+    x[6] = rng.standard_normal(T) * 1e200
+    x[6, ::3] *= 1e-250
+    x[7] = 2.0 ** 700 * (1 + rng.random(T))                    # at the range bound
+    x[8] = 2.0 ** -900 * (1 + rng.random(T))
+    st = TimeSeriesRDD(None, None, dev(torch, x)).seriesStats()
+    ref = np.array([oracle.stat_counter(r)[1:] for r in x])
+    for c, name in enumerate(["mean", "m2", "max", "min"]):
+        assert_bits(host(st.stats[:, c]), ref[:, c], name)
+
+
 def test_remove_instants_with_nans_kat(torch):
     # T/TimeSeriesRDDSuite.scala:210-231
     from sparkts.timeseriesrdd import TimeSeriesRDD
@@ -814,7 +837,8 @@ def test_remove_instants_with_nans_kat(torch):
 
 
 @pytest.mark.parametrize("S,T,p", [(1, 1, 0.0), (5, 100, 0.01), (64, 5000, 0.0005), (300, 20000, 0.00005),
-                                   (4, 9000, 1.0)])
+                                   (4, 9000, 1.0), (1, 2, 0.3), (130, 390, 0.001), (65, 1023, 0.002),
+                                   (3, 514, 0.05)])
 def test_remove_instants_with_nans_panels(torch, S, T, p):
     from sparkts.timeseriesrdd import TimeSeriesRDD
     rng = np.random.default_rng(S * 7 + T)
@@ -834,7 +858,8 @@ def test_to_instants(torch):
     for t in range(4):
         assert_bits(host(inst[t]), np.arange(t, 20, 4, dtype=np.float64), "kat")
     rng = np.random.default_rng(5)
-    for S, T in [(1, 7), (65, 63), (130, 1000), (3, 70000)]:
+    # odd shapes take the 8-B kernel; even ones the 16-B kernel (ragged last tiles both ways)
+    for S, T in [(1, 7), (65, 63), (130, 1000), (3, 70000), (2, 2), (64, 64), (128, 390), (66, 130), (200, 4098)]:
         x = rng.standard_normal((S, T))
         _, inst = TimeSeriesRDD(None, None, dev(torch, x)).toInstants()
         assert_bits(host(inst), oracle.to_instants(x), "toInstants %dx%d" % (S, T))
