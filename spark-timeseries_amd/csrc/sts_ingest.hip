@@ -16,6 +16,10 @@
 
 #include <hip/hip_runtime.h>
 
+#ifndef STS_WIRE_ROWS
+#define STS_WIRE_ROWS 1               // one wave per record for short series
+#endif
+
 namespace sts {
 namespace {
 
@@ -41,6 +45,30 @@ __global__ __launch_bounds__(256) void wire_decode_kernel(const unsigned char* _
     panel[s * ld + t] = __longlong_as_double((long long)v);
 }
 
+// Short series (T <= kRowT): one wave per record, 4 records per block, so a few-hundred-
+// value record does not leave most of a 256-wide block idle.
+constexpr int kRowT = 4096;
+__global__ __launch_bounds__(256) void wire_decode_rows_kernel(const unsigned char* __restrict__ bytes,
+                                                               const int64_t* __restrict__ val_off,
+                                                               double* __restrict__ panel, int64_t S, int64_t T,
+                                                               int64_t ld) {
+    const int64_t s = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (s >= S) return;
+    const unsigned char* p = bytes + val_off[s];
+    double* o = panel + s * ld;
+    if ((reinterpret_cast<uintptr_t>(p) & 7) == 0) {
+        const unsigned long long* q = reinterpret_cast<const unsigned long long*>(p);
+        for (int64_t t = threadIdx.x & 63; t < T; t += 64) o[t] = __longlong_as_double((long long)bswap64(q[t]));
+    } else {
+        for (int64_t t = threadIdx.x & 63; t < T; t += 64) {
+            unsigned long long v = 0;
+#pragma unroll
+            for (int i = 0; i < 8; i++) v = (v << 8) | p[8 * t + i];
+            o[t] = __longlong_as_double((long long)v);
+        }
+    }
+}
+
 // the reverse: BE doubles of series s into bytes[val_off[s] ...]
 __global__ __launch_bounds__(256) void wire_encode_kernel(const double* __restrict__ panel, int64_t T, int64_t ld,
                                                           const int64_t* __restrict__ val_off,
@@ -55,6 +83,25 @@ __global__ __launch_bounds__(256) void wire_encode_kernel(const double* __restri
     } else {
 #pragma unroll
         for (int i = 0; i < 8; i++) p[i] = (unsigned char)(v >> (56 - 8 * i));
+    }
+}
+
+__global__ __launch_bounds__(256) void wire_encode_rows_kernel(const double* __restrict__ panel, int64_t S, int64_t T,
+                                                               int64_t ld, const int64_t* __restrict__ val_off,
+                                                               unsigned char* __restrict__ bytes) {
+    const int64_t s = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (s >= S) return;
+    unsigned char* p = bytes + val_off[s];
+    const double* x = panel + s * ld;
+    if ((reinterpret_cast<uintptr_t>(p) & 7) == 0) {
+        unsigned long long* q = reinterpret_cast<unsigned long long*>(p);
+        for (int64_t t = threadIdx.x & 63; t < T; t += 64) q[t] = bswap64((unsigned long long)__double_as_longlong(x[t]));
+    } else {
+        for (int64_t t = threadIdx.x & 63; t < T; t += 64) {
+            const unsigned long long v = (unsigned long long)__double_as_longlong(x[t]);
+#pragma unroll
+            for (int i = 0; i < 8; i++) p[8 * t + i] = (unsigned char)(v >> (56 - 8 * i));
+        }
     }
 }
 
@@ -110,6 +157,11 @@ hipError_t per_series_grid(int64_t S, int64_t T, F&& launch) {
 hipError_t launch_wire_decode(const unsigned char* bytes, const int64_t* val_off, double* panel, int64_t S, int64_t T,
                               int64_t ld, hipStream_t st) {
     if (S <= 0 || T <= 0) return hipSuccess;
+    if (STS_WIRE_ROWS && T <= kRowT && (S + 3) / 4 <= 0x7fffffffLL) {
+        hipLaunchKernelGGL(wire_decode_rows_kernel, dim3((unsigned)((S + 3) / 4)), dim3(256), 0, st, bytes, val_off,
+                           panel, S, T, ld);
+        return hipGetLastError();
+    }
     return per_series_grid(S, T, [&](int64_t s, dim3 g) {
         hipLaunchKernelGGL(wire_decode_kernel, g, dim3(256), 0, st, bytes, val_off + s, panel + s * ld, T, ld);
     });
@@ -118,6 +170,11 @@ hipError_t launch_wire_decode(const unsigned char* bytes, const int64_t* val_off
 hipError_t launch_wire_encode(const double* panel, int64_t S, int64_t T, int64_t ld, const int64_t* val_off,
                               unsigned char* bytes, hipStream_t st) {
     if (S <= 0 || T <= 0) return hipSuccess;
+    if (STS_WIRE_ROWS && T <= kRowT && (S + 3) / 4 <= 0x7fffffffLL) {
+        hipLaunchKernelGGL(wire_encode_rows_kernel, dim3((unsigned)((S + 3) / 4)), dim3(256), 0, st, panel, S, T, ld,
+                           val_off, bytes);
+        return hipGetLastError();
+    }
     return per_series_grid(S, T, [&](int64_t s, dim3 g) {
         hipLaunchKernelGGL(wire_encode_kernel, g, dim3(256), 0, st, panel + s * ld, T, ld, val_off + s, bytes);
     });

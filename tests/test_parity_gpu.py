@@ -885,8 +885,9 @@ def test_to_row_matrices(torch):
 def test_wire_decode_encode_round_trip(torch):
     from sparkts import io as sio
     rng = np.random.default_rng(31)
-    for S, T in [(1, 1), (3, 7), (40, 390), (5, 5000)]:
-        keys = ["k%d" % i + "é" * (i % 3) for i in range(S)]     # unaligned value blocks
+    for S, T, aligned in [(1, 1, False), (3, 7, False), (40, 390, False), (5, 5000, False), (70, 390, True),
+                          (9, 4096, True), (6, 4097, True), (65, 33, False)]:
+        keys = ["k%07d" % i for i in range(S)] if aligned else ["k%d" % i + "é" * (i % 3) for i in range(S)]
         x = rng.standard_normal((S, T)) * 1e3
         x.ravel()[rng.random(S * T) < 0.05] = NaN
         if T > 2:
