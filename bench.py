@@ -254,10 +254,10 @@ def main():
               "c2": "sts::recur_kernel<kFillDiffEwma> (fillPrevious -> differencesAtLag(1) -> EWMA add, lane per series)",
               "stage_c2": "sts::recur_kernel<kFillDiffEwma> (fillPrevious -> differencesAtLag(1) -> EWMA add, lane per series)",
               "c4": "sts::ar_fit_blk_kernel<5,40,4,dma> (AR(5): series in by LDS-DMA, lane-blocked register lag products, lane-parallel Gram / Cholesky + refinement, fused remove out through LDS)",
-              "stats": "sts::stats_kernel<64,32> (StatCounter.merge per lane, LDS-staged series block)",
-              "nan_instants": "sts::nan_instants_kernel + sts::gather_instants_kernel",
-              "to_instants": "sts::transpose_kernel (64x64 LDS tiles)",
-              "wire_decode": "sts::wire_decode_kernel (big-endian value blocks -> panel)",
+              "stats": "sts::stats_fast_kernel<64,16> (StatCounter.merge per lane, LDS-staged series block, division off the step chain)",
+              "nan_instants": "sts::nan_instants16_kernel + sts::gather_instants_kernel (wave per row)",
+              "to_instants": "sts::transpose16_kernel (64x64 LDS tiles, 16-B accesses)",
+              "wire_decode": "sts::wire_decode_rows_kernel (big-endian value blocks -> panel, wave per record)",
               "garch_fit": "sts::garch_fit_kernel<64,64> (lane-per-series commons-math3 optimizer; one "
                            "logLikelihood+gradient pass over the wave's series block per optimizer request) + "
                            "sts::garch_tail_kernel<64> (wave per series past 64 passes)",
