@@ -22,6 +22,9 @@
 #ifndef STS_TR_NT
 #define STS_TR_NT 1                   // non-temporal transpose stores (+2.5 %, r02_v10)
 #endif
+#ifndef STS_GATHER_BATCH
+#define STS_GATHER_BATCH 1            // instant gather: batched loads before the stores
+#endif
 #ifndef STS_NAN16
 #define STS_NAN16 1                   // 16-B NaN-instant scan when shapes allow
 #endif
@@ -311,7 +314,25 @@ __global__ __launch_bounds__(64 * kGatherRows) void gather_instants_kernel(const
     if (s >= S) return;
     const double* src = in + s * ld_in;
     double* dst = out + s * ld_out;
-    for (int64_t j = threadIdx.x & 63; j < n_active; j += 64) dst[j] = src[active[j]];
+    const int lane = threadIdx.x & 63;
+    if (STS_GATHER_BATCH) {
+        // 8 loads in flight per lane before the stores (512 kept instants per pass)
+        for (int64_t j0 = 0; j0 < n_active; j0 += 512) {
+            double v[8];
+#pragma unroll
+            for (int k = 0; k < 8; k++) {
+                const int64_t j = j0 + lane + 64 * k;
+                v[k] = src[active[j < n_active ? j : n_active - 1]];
+            }
+#pragma unroll
+            for (int k = 0; k < 8; k++) {
+                const int64_t j = j0 + lane + 64 * k;
+                if (j < n_active) dst[j] = v[k];
+            }
+        }
+    } else {
+        for (int64_t j = lane; j < n_active; j += 64) dst[j] = src[active[j]];
+    }
 }
 
 // toInstants: out[t, s] = in[s, t] (T x S, instant-major), 64 x 64 tiles through LDS
