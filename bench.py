@@ -89,6 +89,8 @@ def main():
     from sparkts import _native
     from sparkts.errors import raise_for_status
     from sparkts.timeseriesrdd import ResultGather
+    if os.environ.get("STS_HIP_LIB"):   # A/B runs of tools/variant.sh builds (tools/*.sh)
+        _native.use_library(os.environ["STS_HIP_LIB"])
     _native.ensure_device(local)
     lib = _native.lib()
 
@@ -493,10 +495,13 @@ def cpu_baseline(args, S, T, K, seed, nan_p, out, acf, p_ar, smooth=None, gpar_r
         done += n
         s_next += n
     rate = done * T / elapsed if elapsed > 0 else None
+    single = args.workload in ("stats", "nan_instants", "to_instants", "wire_decode")
     return {"value": rate, "unit": "series-elements/s", "cores": threads, "kind": "port",
             "host_nproc": os.cpu_count(),
-            "cores_note": "threads = this process's CPU affinity capped by OMP_NUM_THREADS (the GPU box grants a "
-                          "single-GPU job 16 of its nproc cores); Spark local[N] with N = cores",
+            "cores_note": ("SINGLE-THREADED restatement (one partition, 1 core): a GPU / CPU ratio from this line "
+                           "is per core, not against a local[N] executor" if single else
+                           "threads = this process's CPU affinity capped by OMP_NUM_THREADS (the GPU box grants a "
+                           "single-GPU job 16 of its nproc cores); Spark local[N] with N = cores"),
             "sample": "%d of the rank-0 series x %d steps (%.1f s of CPU work), oracle/sts_oracle.c restatement of "
                       "the reference loops, one series per thread (Spark local[%d] analogue); the JVM reference "
                       "cannot run here" % (done, T, elapsed, threads),

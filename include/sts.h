@@ -304,23 +304,36 @@ int sts_gen_panel(double* out, int64_t s0, int64_t S, int64_t T, int64_t ld, uin
 int sts_gen_ar_panel(double* out, double* c, double* phi, int64_t s0, int64_t S, int64_t T,
                      int64_t ld, uint64_t seed, int p, void* stream);
 
-/* ---- host-buffer variants (JNI path).  Each call runs a per-thread PINNED STAGING
- * PIPELINE: the panel is split by series into chunks of ~64 MB of device traffic, and each
- * chunk's H2D copy, kernel(s) and D2H copy run on one of three per-thread HIP streams, so
- * uploads, compute and downloads of consecutive chunks overlap.  Host arrays that are
- * already pinned (sts_host_alloc) move by DMA directly; pageable arrays go through the
- * thread's reused pinned bounce buffers.  err_per_series, c, coef, acf, ... are host arrays;
- * with err_per_series NULL the first failing series becomes the return status (the
- * reference's exception), decided after every chunk is back.  Return after the results are
- * on the host.  Reference operators as for the device entry points above. ---- */
+/* ---- host-buffer variants (JNI path).  Each call runs a PINNED STAGING PIPELINE: the
+ * panel is split by series into chunks of ~64 MB of device traffic, and each chunk's H2D
+ * copy, kernel(s) and D2H copy run on one of the FIVE slots (a HIP stream, a 64 MB device
+ * buffer and a pinned bounce buffer each) of a slot set, so uploads, compute and downloads of
+ * consecutive chunks overlap.  A call borrows one slot set from a process-wide pool for its
+ * duration: at most sts_staging_set_limit() sets per device (default 4), so staging memory is
+ * bounded by 4 x 5 x 64 MB = 1.25 GiB of HBM plus as much pinned host memory however many
+ * executor threads call; a call that finds every set borrowed waits for one.  Nothing is
+ * owned by the calling thread, so retired threads leave nothing behind.  Host arrays that are
+ * already pinned (sts_host_alloc) move by DMA directly; pageable arrays go through the set's
+ * reused pinned bounce buffers.  err_per_series, c, coef, acf, ... are host arrays; with
+ * err_per_series NULL the first failing series becomes the return status (the reference's
+ * exception), decided after every chunk is back.  Every call returns only after all of its
+ * transfers have completed, on success and on error alike.  Reference operators as for the
+ * device entry points above. ---- */
 
 /* Pinned host memory for callers that fill it themselves (the JNI shim copies Java arrays
  * into it with GetDoubleArrayRegion, then calls a _host entry point on it: no JVM array is
  * held across device work). */
 int sts_host_alloc(size_t bytes, void** out);
 int sts_host_free(void* p);
-/* Free the calling thread's staging streams and buffers (they are otherwise reused). */
+/* Free the idle staging slot sets of every device (they are otherwise kept for reuse). */
 int sts_staging_release(void);
+/* At most max_sets (>= 1) staging slot sets per device; lowering it frees idle sets now and
+ * borrowed ones when their calls end. */
+int sts_staging_set_limit(int max_sets);
+/* Staging pool of the current device: out8 = {sets alive, idle, borrowed, limit, high-water
+ * mark of sets alive, sets abandoned after a device error, calls that had to wait for a set,
+ * device bytes per set}. */
+int sts_staging_pool_info(int64_t* out8);
 /* Statistics of the calling thread's last _host call: out8 = {wall ms, H2D ms, kernel ms,
  * D2H ms (summed per-chunk event times on the staging streams; they overlap each other),
  * H2D bytes, D2H bytes, chunks, fraction of the bytes moved by direct DMA from / to pinned

@@ -293,21 +293,42 @@ def to_instants(x):
     out = np.empty((T, S)); lib().orc_to_instants(_p(x), S, T, T, _p(out)); return out
 
 
-def observations_to_panel(target_index, keys, timestamps, values):
-    """S/TimeSeriesRDD.scala:493-542 restated in Python (small cases): sort observations by
-    (key, timestamp) -- a stable sort, so equal (key, timestamp) pairs keep input order --
-    then per key a NaN series with series(locAtDateTime(ts)) = value for every sample whose
-    timestamp is in the index.  Returns (sorted keys, (S, T) panel)."""
+def _java_hash(key):
+    """java.lang.String.hashCode restated with numpy int32 arithmetic (wraps like Java's int)."""
+    units = np.frombuffer(key.encode("utf-16-be", "surrogatepass"), dtype=">u2").astype(np.int64)
+    h = np.int64(0)
+    for u in units:
+        h = np.int64(((h * 31 + u + 2**31) % 2**32) - 2**31)
+    return int(h)
+
+
+def observations_to_panel(target_index, keys, timestamps, values, num_partitions=1):
+    """S/TimeSeriesRDD.scala:493-542 restated in Python (small cases): the observations go to
+    partition nonNegativeMod(key.hashCode, numPartitions) (HashPartitioner, :509-513) and are
+    sorted there by (key, timestamp) with String.compareTo -- UTF-16 code units -- (:502-507;
+    a stable sort, so equal (key, timestamp) pairs keep input order); then per key, in that
+    order, a NaN series with series(locAtDateTime(ts)) = value for every sample whose
+    timestamp is in the index (:517-537).  Returns (keys in record order, (S, T) panel)."""
     idx = {int(t): i for i, t in enumerate(target_index)}
-    obs = sorted(range(len(keys)), key=lambda i: (keys[i], int(timestamps[i])))
+
+    def part(k):
+        h = _java_hash(k)
+        m = int(np.fmod(h, num_partitions))           # Java %: truncates toward zero
+        return m + num_partitions if m < 0 else m
+
+    def u16(k):
+        return k.encode("utf-16-be", "surrogatepass")   # big-endian code units: bytewise = unitwise order
+    obs = sorted(range(len(keys)), key=lambda i: (part(keys[i]), u16(keys[i]), int(timestamps[i])))
     out = {}
+    order = []
     for i in obs:
-        row = out.setdefault(keys[i], np.full(len(target_index), np.nan))
+        if keys[i] not in out:
+            out[keys[i]] = np.full(len(target_index), np.nan)
+            order.append(keys[i])
         loc = idx.get(int(timestamps[i]), -1)
         if loc >= 0:
-            row[loc] = values[i]
-    ks = sorted(out)
-    return ks, np.array([out[k] for k in ks]).reshape(len(ks), len(target_index))
+            out[keys[i]][loc] = values[i]
+    return order, np.array([out[k] for k in order]).reshape(len(order), len(target_index))
 
 
 def wire_records(keys, panel) -> bytes:

@@ -11,13 +11,13 @@
 // about eps * N * (sigma^2 + (mean - c)^2), so (mean - c)^2 / sigma^2 is the number of
 // bits lost.  Two rules keep that ratio O(1):
 //
-//  1. c is the MEDIAN of the valid values among 64 samples of the series (an outlier at
-//     x[0] or a level far from x[0] cannot move it; |median - mean| <= sigma for the sampled
-//     population): spread evenly over the whole series in the tile kernel (robust_shift),
-//     and over its first 512-step tile in the segment kernel (T <= 16384 there, so a first
-//     tile at another level is >= 1/32 of the series and bounds (mean - c)^2 / sigma^2 by
-//     ~32).  Every workgroup / segment of a series computes it from the same raw samples the
-//     same way, so all of them agree bit for bit and the partials combine.
+//  1. c is the MEDIAN of 64 samples that stand for the FILLED series, one per 1/64 of it
+//     (robust_shift below: the first valid step of each range, a NaN-only range taking the
+//     next range's; an outlier at x[0], a level far from x[0], a long leading NaN run or a
+//     98 %-NaN series cannot move it; |median - mean| <= sigma for the sampled population).
+//     The tile kernel loads it per series from acf_shift_kernel, the segment kernel computes
+//     it at its start; both use this one function, so every workgroup / segment of a series
+//     agrees bit for bit and the partials combine.
 //  2. sum y and sum y^2 are accumulated only over the MIDDLE [kAcfEdge, T - kAcfEdge) of
 //     the series; the head and tail (the only positions that differ between the lag
 //     slices, since K <= kAcfEdge) are added explicitly per lag (acf_combine).  The lag
@@ -72,14 +72,91 @@ __device__ __forceinline__ double median_of_lanes(double v, bool ok, int lane) {
     }
 }
 
-// Robust shift of series `src` (length T >= 1), computed by one whole wave: lane l samples
-// x[t_l] (or x[t_l + 1] when x[t_l] is NaN), t_l = l * T / 64, spread over the whole series;
-// the result is the lower median of the valid samples.
+__device__ __forceinline__ int64_t acf_readlane64(int64_t v, int l) {
+    const unsigned long long u = (unsigned long long)v;
+    const unsigned lo = __builtin_amdgcn_readlane((unsigned)u, l);
+    const unsigned hi = __builtin_amdgcn_readlane((unsigned)(u >> 32), l);
+    return (int64_t)(((unsigned long long)hi << 32) | lo);
+}
+
+// Robust shift of series `src` (length T >= 1), computed by one whole wave from what the
+// FILLED series looks like, whatever the NaN pattern of the raw one (round 3: the round-2
+// shift sampled raw steps and fell to 0.0 -- or to an outlier x[0] -- when they were NaN,
+// e.g. fillNext over a long leading NaN run or a 98 %-NaN panel).
+//   * Lane l owns the positions [t0, t1) = [l T / 64, (l + 1) T / 64) and finds the first
+//     valid step in them: lane-parallel probes of 4 steps (kProbeRounds rounds; at 5 % NaN
+//     the first round finds one in every lane but ~1 in 10^5), then, for the lanes still
+//     without one, a wave-cooperative scan of the rest of their range, 512 steps per trip.
+//     Every valid step is a value of the filled series too (no fill rewrites a valid step).
+//   * A lane whose range holds no valid step takes the sample of the next lane that has one
+//     -- the first valid step after t0, i.e. exactly F(t0) of fillNext, and the right end of
+//     a linear / nearest gap -- else that of the last lane before it with one (a trailing
+//     run).  So every lane stands for its 1/64 of the filled series, and a long run filled
+//     by copies of one value weighs in the sample as it weighs in the series.
+//   * c = the lower median of the 64 samples.  0.0 only when the series has no valid step at
+//     all (its ACF is NaN for every fill then).
+// A pure function of the series' values: every workgroup / segment that computes it gets the
+// same bits.
+constexpr int kProbeRounds = 4;
 __device__ __forceinline__ double robust_shift(const double* src, int64_t T, int lane) {
-    const int64_t t = (int64_t)lane * T / 64;
-    double v = src[t];
-    if (__builtin_isnan(v) && t + 1 < T) v = src[t + 1];
-    return median_of_lanes(v, !__builtin_isnan(v), lane);
+    const int64_t t0 = (int64_t)lane * T / 64, t1 = (int64_t)(lane + 1) * T / 64;
+    int64_t cur = t0;
+    double v = 0.0;
+    bool found = false;
+    for (int r = 0; r < kProbeRounds; r++) {
+        const bool pend = !found && cur < t1;
+        if (__ballot(pend) == 0ull) break;
+        if (pend) {
+            double p[4];
+#pragma unroll
+            for (int k = 0; k < 4; k++) p[k] = (cur + k < t1) ? src[cur + k] : __builtin_nan("");
+#pragma unroll
+            for (int k = 3; k >= 0; k--) {   // the first valid of the four
+                if (!__builtin_isnan(p[k])) {
+                    v = p[k];
+                    found = true;
+                }
+            }
+            cur += 4;
+        }
+    }
+    unsigned long long pendm = __ballot(!found && cur < t1);
+    while (pendm) {   // wave-uniform: one pending lane's range at a time, coalesced
+        const int l = __ffsll((long long)pendm) - 1;
+        int64_t c = acf_readlane64(cur, l);
+        const int64_t e = acf_readlane64(t1, l);
+        bool ff = false;
+        double fv = 0.0;
+        while (c < e && !ff) {
+            double q[8];
+#pragma unroll
+            for (int k = 0; k < 8; k++) {
+                const int64_t t = c + 64 * k + lane;
+                q[k] = (t < e) ? src[t] : __builtin_nan("");
+            }
+#pragma unroll
+            for (int k = 0; k < 8; k++) {
+                const unsigned long long m = __ballot(!__builtin_isnan(q[k]));
+                if (!ff && m) {
+                    fv = acf_readlane(q[k], __ffsll((long long)m) - 1);
+                    ff = true;
+                }
+            }
+            c += 512;
+        }
+        if (ff && lane == l) {
+            v = fv;
+            found = true;
+        }
+        pendm &= pendm - 1ull;
+    }
+    const unsigned long long vm = __ballot(found);
+    if (vm == 0ull) return 0.0;
+    const unsigned long long above = vm & ~((2ull << lane) - 1ull);   // lanes > lane (lane 63: none)
+    const unsigned long long below = vm & ((1ull << lane) - 1ull);
+    const int from = found ? lane : (above ? __ffsll((long long)above) - 1 : 63 - __clzll(below));
+    v = __shfl(v, from);
+    return median_of_lanes(v, true, lane);
 }
 
 // True when series position t contributes to the middle sums (rule 2).

@@ -1,5 +1,5 @@
-// sts_host.cpp -- host-buffer entry points (the JNI path): a per-thread
-// PINNED STAGING PIPELINE in front of the device entry points.
+// sts_host.cpp -- host-buffer entry points (the JNI path): a PINNED
+// STAGING PIPELINE in front of the device entry points.
 //
 // A `_host` call is split by series into chunks of ~kChunkBytes of device traffic.  Each
 // chunk runs H2D -> kernel(s) -> D2H on one of kSlots slots, each slot owning a HIP stream,
@@ -15,8 +15,17 @@
 // Every device entry point runs on the slot's stream; per-series statuses always go to a
 // device array and come back with the chunk, so a NULL err_per_series keeps the reference's
 // exception semantics (the first failing series becomes the return status after all
-// chunks) without a synchronisation per chunk.  Staging state is per calling thread, so
-// Spark's N executor threads never share buffers or streams; sts_staging_release frees it.
+// chunks) without a synchronisation per chunk.
+//
+// Reentrancy and memory (round 3).  A call BORROWS a whole slot set from a process-wide pool
+// (sts_stage_pool.hpp) for its duration: at most sts_staging_set_limit() sets per device
+// (default kDefaultSets = 4, i.e. at most 4 x 5 x 64 MB of HBM and as much pinned memory
+// however many executor threads call), a call finding every set borrowed waits for one, and
+// nothing is owned by a thread, so retired threads leak nothing.  A call never returns while
+// a transfer of its own is in flight: every exit path (success, a HIP error in the middle of
+// the pipeline, a failing kernel) drains the set's busy slots first, and a slot whose kernel
+// or copy-out did not run is never copied to the caller.  sts_staging_release frees the idle
+// sets.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -27,6 +36,7 @@
 #include <vector>
 
 #include "sts_internal.hpp"
+#include "sts_stage_pool.hpp"
 
 namespace {
 
@@ -43,6 +53,7 @@ namespace {
 constexpr int kSlots = STS_STAGE_SLOTS;
 constexpr size_t kChunkBytes = size_t(STS_STAGE_MB) << 20;   // device bytes (in + out) per chunk
 constexpr size_t kAlign = 256;
+constexpr int kDefaultSets = 4;                                // slot sets per device (sts_staging_set_limit)
 
 size_t align_up(size_t b) { return (b + kAlign - 1) / kAlign * kAlign; }
 
@@ -53,31 +64,22 @@ struct Slot {
     size_t dev_cap = 0;
     void* pin = nullptr;
     size_t pin_cap = 0;
-    bool busy = false;
+    bool busy = false;       // ev[3] recorded for a chunk not yet reaped
+    bool copy_out = false;   // its kernel and D2H copies were enqueued: pageable outputs may be copied
     int64_t s0 = 0, ns = 0;
 };
 
-struct Stager {
+struct SlotSet {
     int device = -1;
     Slot slot[kSlots];
-    // statistics of this thread's last _host call (sts_staging_stats)
-    double st_h2d_ms = 0, st_kernel_ms = 0, st_d2h_ms = 0, st_wall_ms = 0;
-    double st_bytes_h2d = 0, st_bytes_d2h = 0, st_chunks = 0, st_direct = 0;   // bytes moved by direct DMA
 };
-thread_local Stager g_stager;
 
-void release(Stager& g) {
-    for (Slot& s : g.slot) {
-        if (s.st) (void)hipStreamSynchronize(s.st);
-        if (s.dev) (void)hipFree(s.dev);
-        if (s.pin) (void)hipHostFree(s.pin);
-        for (hipEvent_t& e : s.ev)
-            if (e) (void)hipEventDestroy(e);
-        if (s.st) (void)hipStreamDestroy(s.st);
-        s = Slot();
-    }
-    g.device = -1;
-}
+// statistics of this thread's last _host call (sts_staging_stats)
+struct Stats {
+    double h2d_ms = 0, kernel_ms = 0, d2h_ms = 0, wall_ms = 0;
+    double bytes_h2d = 0, bytes_d2h = 0, chunks = 0, direct = 0;   // bytes moved by direct DMA
+};
+thread_local Stats g_stats;
 
 int hip_status(hipError_t e, const char* where) {
     char buf[256];
@@ -85,20 +87,66 @@ int hip_status(hipError_t e, const char* where) {
     return sts::set_error(STS_ERR_HIP, buf);
 }
 
-int ensure_stager(Stager& g) {
-    int dev = 0;
-    hipError_t e = hipGetDevice(&dev);
-    if (e != hipSuccess) return hip_status(e, "hipGetDevice");
-    if (g.device == dev) return STS_OK;
-    release(g);
-    for (Slot& s : g.slot) {
-        if ((e = hipStreamCreateWithFlags(&s.st, hipStreamNonBlocking)) != hipSuccess) return hip_status(e, "hipStreamCreate");
-        for (hipEvent_t& ev : s.ev)
-            if ((e = hipEventCreate(&ev)) != hipSuccess) return hip_status(e, "hipEventCreate");
+void destroy_set(SlotSet* g) {
+    int cur = -1;
+    const bool switch_dev = hipGetDevice(&cur) == hipSuccess && cur != g->device;
+    if (switch_dev) (void)hipSetDevice(g->device);
+    for (Slot& s : g->slot) {
+        if (s.st) (void)hipStreamSynchronize(s.st);
+        if (s.dev) (void)hipFree(s.dev);
+        if (s.pin) (void)hipHostFree(s.pin);
+        for (hipEvent_t& e : s.ev)
+            if (e) (void)hipEventDestroy(e);
+        if (s.st) (void)hipStreamDestroy(s.st);
     }
-    g.device = dev;
+    if (switch_dev) (void)hipSetDevice(cur);
+    delete g;
+}
+
+int create_set(int dev, SlotSet** out) {
+    SlotSet* g = new SlotSet;
+    g->device = dev;
+    hipError_t e = hipSuccess;
+    for (Slot& s : g->slot) {
+        if ((e = hipStreamCreateWithFlags(&s.st, hipStreamNonBlocking)) != hipSuccess) break;
+        for (hipEvent_t& ev : s.ev)
+            if ((e = hipEventCreate(&ev)) != hipSuccess) break;
+        if (e != hipSuccess) break;
+    }
+    if (e != hipSuccess) {
+        const int r = hip_status(e, "staging: stream / event");
+        destroy_set(g);
+        return r;
+    }
+    *out = g;
     return STS_OK;
 }
+
+// never destroyed: at process exit the HIP runtime may already be gone, and the OS reclaims
+sts::StagePool<SlotSet>& pool() {
+    static sts::StagePool<SlotSet>* p = new sts::StagePool<SlotSet>(create_set, destroy_set, kDefaultSets);
+    return *p;
+}
+
+// A borrowed set; on destruction (every exit path of staged()) all its busy slots are
+// drained WITHOUT copying to the caller, then it goes back to the pool -- or, when a drain
+// fails (device error), it is forgotten rather than reused or freed under a live DMA.
+struct Borrow {
+    SlotSet* set = nullptr;
+    int dev = -1;
+    ~Borrow() {
+        if (!set) return;
+        bool ok = true;
+        for (Slot& sl : set->slot) {
+            if (sl.busy && hipEventSynchronize(sl.ev[3]) != hipSuccess) ok = false;
+            if (sl.st && hipStreamSynchronize(sl.st) != hipSuccess) ok = false;   // a partly enqueued chunk
+            sl.busy = false;
+            sl.copy_out = false;
+        }
+        if (ok) pool().give_back(dev, set);
+        else pool().forget(dev);
+    }
+};
 
 bool is_pinned(const void* p) {
     if (!p) return false;
@@ -157,16 +205,20 @@ void copy_rows(void* dst, size_t dstride, const void* src, size_t sstride, size_
                     row);
 }
 
-// Wait for a slot's chunk, account its time, copy its pageable outputs to the caller.
-int reap(Stager& g, Slot& sl, std::vector<Arg>& args) {
+// Wait for a slot's chunk, account its time, copy its pageable outputs to the caller (only
+// when its kernel and copy-out were enqueued).
+int reap(Slot& sl, std::vector<Arg>& args) {
     if (!sl.busy) return STS_OK;
-    sl.busy = false;
     hipError_t e = hipEventSynchronize(sl.ev[3]);
-    if (e != hipSuccess) return hip_status(e, "staging: chunk");
+    if (e != hipSuccess) return hip_status(e, "staging: chunk");   // stays busy: Borrow drains it
+    sl.busy = false;
+    Stats& g = g_stats;
     float a = 0, b = 0, c = 0;
-    if (hipEventElapsedTime(&a, sl.ev[0], sl.ev[1]) == hipSuccess) g.st_h2d_ms += a;
-    if (hipEventElapsedTime(&b, sl.ev[1], sl.ev[2]) == hipSuccess) g.st_kernel_ms += b;
-    if (hipEventElapsedTime(&c, sl.ev[2], sl.ev[3]) == hipSuccess) g.st_d2h_ms += c;
+    if (hipEventElapsedTime(&a, sl.ev[0], sl.ev[1]) == hipSuccess) g.h2d_ms += a;
+    if (hipEventElapsedTime(&b, sl.ev[1], sl.ev[2]) == hipSuccess) g.kernel_ms += b;
+    if (hipEventElapsedTime(&c, sl.ev[2], sl.ev[3]) == hipSuccess) g.d2h_ms += c;
+    if (!sl.copy_out) return STS_OK;
+    sl.copy_out = false;
     for (Arg& x : args)
         if (x.dst && !x.pinned_dst)
             copy_rows(static_cast<char*>(x.dst) + (size_t)sl.s0 * x.hstride, x.hstride,
@@ -174,12 +226,11 @@ int reap(Stager& g, Slot& sl, std::vector<Arg>& args) {
     return STS_OK;
 }
 
-// Run `kern` over S series in chunks through the calling thread's staging slots.
+// Run `kern` over S series in chunks through a borrowed slot set.
 int staged(int64_t S, std::vector<Arg> args, const Kernel& kern) {
     const auto t_start = std::chrono::steady_clock::now();
-    Stager& g = g_stager;
-    g.st_h2d_ms = g.st_kernel_ms = g.st_d2h_ms = g.st_wall_ms = 0;
-    g.st_bytes_h2d = g.st_bytes_d2h = g.st_chunks = g.st_direct = 0;
+    Stats& g = g_stats;
+    g = Stats();
     int r;
     // the device entry point's own argument checks first, on the caller's shapes and host
     // pointers (never dereferenced in validate-only mode): no staging on bad input
@@ -190,7 +241,13 @@ int staged(int64_t S, std::vector<Arg> args, const Kernel& kern) {
         if ((r = sts::validate([&] { return kern(hp, 0, S, nullptr); }))) return r;
     }
     if (S <= 0) return STS_OK;
-    if ((r = ensure_stager(g))) return r;
+    Borrow bw;
+    {
+        hipError_t e = hipGetDevice(&bw.dev);
+        if (e != hipSuccess) return hip_status(e, "hipGetDevice");
+        if ((r = pool().acquire(bw.dev, &bw.set))) return r > 0 ? r : sts::set_error(STS_ERR_BAD_ARG, "staging: device id");
+    }
+    Slot* slots = bw.set->slot;
     size_t per_series = 0;
     for (Arg& x : args) {
         x.pinned_src = is_pinned(x.src);
@@ -208,7 +265,8 @@ int staged(int64_t S, std::vector<Arg> args, const Kernel& kern) {
         if ((x.src && !x.pinned_src) || (x.dst && !x.pinned_dst)) pin_bytes += align_up(x.row * (size_t)ns);
     }
     hipError_t e;
-    for (Slot& sl : g.slot) {
+    for (int k = 0; k < kSlots; k++) {
+        Slot& sl = slots[k];
         if (sl.dev_cap < dev_bytes) {
             if (sl.dev) (void)hipFree(sl.dev);
             sl.dev = nullptr;
@@ -228,8 +286,8 @@ int staged(int64_t S, std::vector<Arg> args, const Kernel& kern) {
     const int64_t nchunks = (S + ns - 1) / ns;
     int status = STS_OK;
     for (int64_t i = 0; i < nchunks && status == STS_OK; i++) {
-        Slot& sl = g.slot[i % kSlots];
-        if ((r = reap(g, sl, args))) return r;
+        Slot& sl = slots[i % kSlots];
+        if ((r = reap(sl, args))) return r;
         sl.s0 = i * ns;
         sl.ns = std::min<int64_t>(ns, S - sl.s0);
         char* dev = static_cast<char*>(sl.dev);
@@ -252,38 +310,41 @@ int staged(int64_t S, std::vector<Arg> args, const Kernel& kern) {
             else
                 e = hipMemcpyAsync(dev + x.dev_off, pin + x.pin_off, n, hipMemcpyHostToDevice, sl.st);
             if (e != hipSuccess) return hip_status(e, "staging: H2D");
-            g.st_bytes_h2d += (double)n;
-            if (x.pinned_src) g.st_direct += (double)n;
+            g.bytes_h2d += (double)n;
+            if (x.pinned_src) g.direct += (double)n;
         }
         if ((e = hipEventRecord(sl.ev[1], sl.st)) != hipSuccess) return hip_status(e, "staging: event");
         void* ptrs[16];
         for (size_t k = 0; k < args.size() && k < 16; k++) ptrs[k] = dev + args[k].dev_off;
         status = kern(ptrs, sl.s0, sl.ns, sl.st);
         if ((e = hipEventRecord(sl.ev[2], sl.st)) != hipSuccess) return hip_status(e, "staging: event");
-        for (Arg& x : args) {
-            if (!x.dst || status != STS_OK) continue;
-            const size_t n = x.row * (size_t)sl.ns;
-            if (STS_STAGE_LINEAR && x.pinned_dst && x.hstride == x.row)
-                e = hipMemcpyAsync(static_cast<char*>(x.dst) + (size_t)sl.s0 * x.hstride, dev + x.dev_off, n,
-                                   hipMemcpyDeviceToHost, sl.st);
-            else if (x.pinned_dst)
-                e = hipMemcpy2DAsync(static_cast<char*>(x.dst) + (size_t)sl.s0 * x.hstride, x.hstride, dev + x.dev_off,
-                                     x.row, x.row, (size_t)sl.ns, hipMemcpyDeviceToHost, sl.st);
-            else
-                e = hipMemcpyAsync(pin + x.pin_off, dev + x.dev_off, n, hipMemcpyDeviceToHost, sl.st);
-            if (e != hipSuccess) return hip_status(e, "staging: D2H");
-            g.st_bytes_d2h += (double)n;
-            if (x.pinned_dst) g.st_direct += (double)n;
+        if (status == STS_OK) {
+            for (Arg& x : args) {
+                if (!x.dst) continue;
+                const size_t n = x.row * (size_t)sl.ns;
+                if (STS_STAGE_LINEAR && x.pinned_dst && x.hstride == x.row)
+                    e = hipMemcpyAsync(static_cast<char*>(x.dst) + (size_t)sl.s0 * x.hstride, dev + x.dev_off, n,
+                                       hipMemcpyDeviceToHost, sl.st);
+                else if (x.pinned_dst)
+                    e = hipMemcpy2DAsync(static_cast<char*>(x.dst) + (size_t)sl.s0 * x.hstride, x.hstride,
+                                         dev + x.dev_off, x.row, x.row, (size_t)sl.ns, hipMemcpyDeviceToHost, sl.st);
+                else
+                    e = hipMemcpyAsync(pin + x.pin_off, dev + x.dev_off, n, hipMemcpyDeviceToHost, sl.st);
+                if (e != hipSuccess) return hip_status(e, "staging: D2H");
+                g.bytes_d2h += (double)n;
+                if (x.pinned_dst) g.direct += (double)n;
+            }
         }
         if ((e = hipEventRecord(sl.ev[3], sl.st)) != hipSuccess) return hip_status(e, "staging: event");
         sl.busy = true;
-        g.st_chunks += 1;
+        sl.copy_out = (status == STS_OK);
+        g.chunks += 1;
     }
     for (int64_t i = 0; i < kSlots; i++) {   // drain in issue order
-        Slot& sl = g.slot[(nchunks + i) % kSlots];
-        if ((r = reap(g, sl, args)) && status == STS_OK) status = r;
+        Slot& sl = slots[(nchunks + i) % kSlots];
+        if ((r = reap(sl, args))) return r;
     }
-    g.st_wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
+    g.wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
     return status;
 }
 
@@ -324,16 +385,34 @@ int sts_host_free(void* p) {
 }
 
 int sts_staging_release(void) {
-    release(g_stager);
+    (void)pool().trim();
+    return STS_OK;
+}
+
+int sts_staging_set_limit(int max_sets) {
+    if (max_sets < 1) return sts::set_error(STS_ERR_BAD_ARG, "sts_staging_set_limit: max_sets must be >= 1");
+    (void)pool().set_cap(max_sets);
+    return STS_OK;
+}
+
+int sts_staging_pool_info(int64_t* out8) {
+    if (!out8) return sts::set_error(STS_ERR_BAD_ARG, "sts_staging_pool_info: null output");
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return hip_status(e, "hipGetDevice");
+    const auto in = pool().info(dev);
+    const int64_t v[8] = {in.live, in.idle, in.borrowed, in.cap, in.high, in.lost, in.waits,
+                          (int64_t)kSlots * (int64_t)kChunkBytes};
+    std::memcpy(out8, v, sizeof v);
     return STS_OK;
 }
 
 int sts_staging_stats(double* out8) {
     if (!out8) return sts::set_error(STS_ERR_BAD_ARG, "sts_staging_stats: null output");
-    const Stager& g = g_stager;
-    const double tot = g.st_bytes_h2d + g.st_bytes_d2h;
-    const double v[8] = {g.st_wall_ms, g.st_h2d_ms, g.st_kernel_ms, g.st_d2h_ms,
-                         g.st_bytes_h2d, g.st_bytes_d2h, g.st_chunks, tot > 0 ? g.st_direct / tot : 0.0};
+    const Stats& g = g_stats;
+    const double tot = g.bytes_h2d + g.bytes_d2h;
+    const double v[8] = {g.wall_ms, g.h2d_ms, g.kernel_ms, g.d2h_ms,
+                         g.bytes_h2d, g.bytes_d2h, g.chunks, tot > 0 ? g.direct / tot : 0.0};
     std::memcpy(out8, v, sizeof v);
     return STS_OK;
 }
@@ -360,10 +439,17 @@ int sts_autocorr_host(const double* in, int64_t S, int64_t T, int64_t ld, int K,
     if (K < 0 || ld < T || (S > 0 && T > 0 && !in) || (S > 0 && K > 0 && !acf))
         return sts_autocorr(in, S, T, ld, K, acf, nullptr);   // the device entry point's error
     const size_t row = (size_t)(T > 0 ? T : 0) * sizeof(double), krow = (size_t)K * sizeof(double);
-    return staged(S, {in_arg(in, row, panel_stride(ld)), out_arg(acf, krow, krow)},
-                  [&](void* const* d, int64_t, int64_t n, hipStream_t s) {
-                      return sts_autocorr(static_cast<const double*>(d[0]), n, T, T, K, static_cast<double*>(d[1]), s);
-                  });
+    // a device err array per chunk (it stays all zero: raw autocorr has no failing series), so
+    // the device entry point never synchronises inside the pipeline
+    ErrOut eo(nullptr, S);
+    const int st = staged(S, {in_arg(in, row, panel_stride(ld)), out_arg(acf, krow, krow),
+                              out_arg(eo.h, sizeof(int32_t), sizeof(int32_t))},
+                          [&](void* const* d, int64_t, int64_t n, hipStream_t s) {
+                              return sts_fill_autocorr(static_cast<const double*>(d[0]), nullptr, n, T, T, T,
+                                                       STS_FILL_NONE, K, static_cast<double*>(d[1]),
+                                                       static_cast<int32_t*>(d[2]), s);
+                          });
+    return eo.finish(st, S, "autocorr");
 }
 
 int sts_fill_autocorr_host(const double* in, double* filled, int64_t S, int64_t T, int64_t ld, int method, int K,

@@ -597,22 +597,9 @@ __global__ __launch_bounds__(256, 4) void seg_kernel(TileArgs a, int method) {
     v2d RA[4], RB[4];
     load_tile(RA, cx.src, cx.k0 * kW, cx.T, lane);
     if (cx.k0 + 1 <= cx.kLast) load_tile(RB, cx.src, (cx.k0 + 1) * kW, cx.T, lane);
-    if (NT > 0) {
-        // ACF shift (sts_acf.hpp): median of 64 samples of the series' first tile, lane l taking
-        // step 128 (l & 3) + 2 l (or the step after it when NaN) from the registers -- no
-        // extra load for segment 0; later segments (A/B build only) load tile 0 themselves
-        v2d R0[4];
-        if (g == 0) {
-#pragma unroll
-            for (int u = 0; u < 4; u++) R0[u] = RA[u];
-        } else {
-            load_tile(R0, cx.src, 0, cx.T, lane);
-        }
-        const int u = lane & 3;
-        const v2d r = (u == 0) ? R0[0] : (u == 1) ? R0[1] : (u == 2) ? R0[2] : R0[3];
-        const double v = __builtin_isnan(r.x) ? r.y : r.x;
-        st.c0 = median_of_lanes(v, !__builtin_isnan(v), lane);
-    }
+    // ACF shift (sts_acf.hpp robust_shift): 64 samples spread over the whole series that
+    // stand for the filled values; its probe loads are in flight with the first two tiles'
+    if (NT > 0) st.c0 = robust_shift(cx.src, cx.T, lane);
     masks_to_lds(RA, w.m2[0], lane);
     raw_to_slot(w.ring, RA, lane);
     if (NT > 0 && g == 0) zero_slot<1>(w, lane);     // "tile -1": y = 0 before the series

@@ -49,7 +49,8 @@
 #endif
 
 #ifndef STS_DIAG
-#define STS_DIAG 0        // diagnostic builds only (tools/variant.sh): 1 = no MFMA, 2 = no LDS operand reads
+#define STS_DIAG 0        // diagnostic builds only (tools/variant.sh): 1 = no MFMA, 2 = no LDS operand reads,
+                          // 3 / 4 = cost models of I8 (Ozaki-split) lag products (timing only, see below)
 #endif
 
 #ifndef STS_TILE_DB
@@ -318,6 +319,30 @@ __global__ __launch_bounds__(NTH, (DB || DMA) ? 2 : STS_TILE_WGS) void tile_kern
 #pragma unroll
     for (int t = 0; t < NA; t++) U[t] = d4{0.0, 0.0, 0.0, 0.0};
     bool series_err = false;
+#if STS_DIAG >= 3
+    // COST MODEL of the lag products on the I8 MFMA (timing only, the
+    // numbers it produces are not the ACF).  An Ozaki split of y into D = 7 signed 8-bit digits
+    // relative to a per-tile power-of-two scale needs the 28 digit pairs of weight <= 6, each a
+    // v_mfma_i32_16x16x64_i8 per 1024 steps and window shift (4 shifts): 112 I8 MFMAs per wave
+    // per tile (16 cycles each) instead of 64 FP64 ones (64 cycles each), with 7 exact int32
+    // accumulators (one per weight) flushed into the FP64 lag sums once per tile.
+    //   STS_DIAG 3: the I8 MFMAs (7 per 64-step chunk) with their operand fetches (4 x 16 B per
+    //               chunk from LDS + 14 byte aligns for the unaligned digit windows) in place of
+    //               the FP64 ones, mid sums in the store pass, per-tile flush;
+    //   STS_DIAG 4: 3 + the digit split itself: the tile's max |y| (wave reductions + LDS),
+    //               a quantisation pass after the store pass (re-read y, scale, floor / cvt into
+    //               a 56-bit integer, balanced digits, byte transposes, 7 bytes per step into
+    //               LDS digit planes) and one more barrier; the MFMAs read the planes.
+    typedef int i4 __attribute__((ext_vector_type(4)));
+    i4 UI[7];
+#pragma unroll
+    for (int w = 0; w < 7; w++) UI[w] = i4{0, 0, 0, 0};
+#endif
+#if STS_DIAG == 4
+    __shared__ __attribute__((aligned(16))) unsigned planes[7 * (EW / 4)];
+    __shared__ double wmax[kWaves];
+    double tmax = 0.0;
+#endif
 
 #ifdef STS_STAMPS
     unsigned long long st_acc[12] = {0};
@@ -413,6 +438,38 @@ __global__ __launch_bounds__(NTH, (DB || DMA) ? 2 : STS_TILE_WGS) void tile_kern
                     }
 #pragma unroll
                     for (int cc = F; cc < TE; cc++) {
+#if STS_DIAG >= 3   // I8 cost model (see the declaration of UI)
+                        {
+#if STS_DIAG == 4
+                            const i4* pq = reinterpret_cast<const i4*>(planes);
+                            constexpr int SH = 2;
+#else
+                            const i4* pq = reinterpret_cast<const i4*>(vb);
+                            constexpr int SH = 1;
+#endif
+                            i4 o[4];
+                            o[0] = pq[(ia[0] + 72 * cc) >> SH];
+                            o[1] = pq[(ib[0] + 72 * cc) >> SH];
+                            o[2] = pq[(ia[1] + 72 * cc) >> SH];
+                            o[3] = pq[(ib[1] + 72 * cc) >> SH];
+                            const unsigned sa = (unsigned)lane & 3u;
+#pragma unroll
+                            for (int u = 0; u < 4; u++) {
+                                o[u].x = (int)__builtin_amdgcn_alignbyte((unsigned)o[u].y, (unsigned)o[u].x, sa);
+                                o[u].y = (int)__builtin_amdgcn_alignbyte((unsigned)o[u].z, (unsigned)o[u].y, sa);
+                                o[u].z = (int)__builtin_amdgcn_alignbyte((unsigned)o[u].w, (unsigned)o[u].z, sa);
+                                if (u < 2) o[u].w = (int)__builtin_amdgcn_alignbyte((unsigned)o[u].x, (unsigned)o[u].w, sa);
+                            }
+                            UI[0] = __builtin_amdgcn_mfma_i32_16x16x64_i8(o[0], o[1], UI[0], 0, 0, 0);
+                            UI[1] = __builtin_amdgcn_mfma_i32_16x16x64_i8(o[0], o[3], UI[1], 0, 0, 0);
+                            UI[2] = __builtin_amdgcn_mfma_i32_16x16x64_i8(o[2], o[1], UI[2], 0, 0, 0);
+                            UI[3] = __builtin_amdgcn_mfma_i32_16x16x64_i8(o[2], o[3], UI[3], 0, 0, 0);
+                            UI[4] = __builtin_amdgcn_mfma_i32_16x16x64_i8(o[1], o[0], UI[4], 0, 0, 0);
+                            UI[5] = __builtin_amdgcn_mfma_i32_16x16x64_i8(o[3], o[0], UI[5], 0, 0, 0);
+                            UI[6] = __builtin_amdgcn_mfma_i32_16x16x64_i8(o[3], o[2], UI[6], 0, 0, 0);
+                        }
+                        __builtin_amdgcn_sched_barrier(0);
+#else
                         double av[NTA], bv[NTA];
 #pragma unroll
                         for (int t = 0; t < NT; t++) {
@@ -434,6 +491,7 @@ __global__ __launch_bounds__(NTH, (DB || DMA) ? 2 : STS_TILE_WGS) void tile_kern
                         acc_s += av[0];   // middle sums: VALU under the MFMA pipe
                         acc_q = __builtin_fma(av[0], av[0], acc_q);
                         __builtin_amdgcn_sched_barrier(0);   // one chunk's operands live at a time
+#endif
                     }
                     c = cend;
                 }
@@ -805,6 +863,13 @@ __global__ __launch_bounds__(NTH, (DB || DMA) ? 2 : STS_TILE_WGS) void tile_kern
                             y.x = fv[j].x - c0;
                             y.y = fv[j].y - c0;
                             v2[px2(vq + jj * kThreads)] = y;
+#if STS_DIAG >= 3   // cost model: the middle sums move from the MFMA loop to this pass
+                            acc_s += y.x + y.y;
+                            acc_q = __builtin_fma(y.x, y.x, __builtin_fma(y.y, y.y, acc_q));
+#endif
+#if STS_DIAG == 4
+                            tmax = __builtin_fmax(tmax, __builtin_fmax(__builtin_fabs(y.x), __builtin_fabs(y.y)));
+#endif
                         }
                     }
                 }
@@ -864,10 +929,67 @@ __global__ __launch_bounds__(NTH, (DB || DMA) ? 2 : STS_TILE_WGS) void tile_kern
                 prev_t0 = t0;
                 prev_t1 = t1;
             } else {
+#if STS_DIAG == 4   // cost model: the tile's max |y| -> scale, then the digit split into LDS planes
+                {
+#pragma unroll
+                    for (int d = 32; d >= 1; d >>= 1) tmax = __builtin_fmax(tmax, __shfl_xor(tmax, d));
+                    if (lane == 0) wmax[wave] = tmax;
+                }
+#endif
                 lds_barrier();
                 STAMP(9);
+#if STS_DIAG == 4
+                {
+                    double m = wmax[0];
+#pragma unroll
+                    for (int w = 1; w < kWaves; w++) m = __builtin_fmax(m, wmax[w]);
+                    int ex;
+                    (void)__builtin_frexp(m, &ex);
+                    const double sc_hi = __builtin_ldexp(1.0, 23 - ex), sc_lo = __builtin_ldexp(1.0, 55 - ex);
+                    const double2* v2q = reinterpret_cast<const double2*>(vals);
+                    for (int q2 = tid; q2 < NP2; q2 += kThreads) {
+                        const double2 y = v2q[px2(q2)];
+                        unsigned dl[2], dh[2];
+#pragma unroll
+                        for (int e = 0; e < 2; e++) {
+                            const double yy = e ? y.y : y.x;
+                            const double h = __builtin_floor(yy * sc_hi);
+                            const double r = __builtin_floor(__builtin_fma(h, -0x1p32, yy * sc_lo));
+                            const unsigned lo = (unsigned)r;
+                            const int hi = (int)h;
+                            const unsigned lo2 = lo + 0x80808080u;
+                            const int hi2 = hi + 0x808080 + (lo2 < lo ? 1 : 0);
+                            dl[e] = lo2 ^ 0x80808080u;
+                            dh[e] = (unsigned)hi2 ^ 0x808080u;
+                        }
+                        // byte transposes into the digit planes (7 bytes per step)
+                        const unsigned w0 = __builtin_amdgcn_perm(dl[1], dl[0], 0x05010400u);
+                        const unsigned w1 = __builtin_amdgcn_perm(dl[1], dl[0], 0x07030602u);
+                        const unsigned w2 = __builtin_amdgcn_perm(dh[1], dh[0], 0x05010400u);
+                        const unsigned w3 = __builtin_amdgcn_perm(dh[1], dh[0], 0x07030602u);
+                        unsigned* pl = planes + (q2 >> 1);
+                        pl[0 * (EW / 4)] = __builtin_amdgcn_perm(w0, w1, 0x05040100u);
+                        pl[1 * (EW / 4)] = __builtin_amdgcn_perm(w0, w1, 0x07060302u);
+                        pl[2 * (EW / 4)] = __builtin_amdgcn_perm(w2, w3, 0x05040100u);
+                        pl[3 * (EW / 4)] = __builtin_amdgcn_perm(w2, w3, 0x07060302u);
+                        pl[4 * (EW / 4)] = w0 ^ w2;
+                        pl[5 * (EW / 4)] = w1 ^ w3;
+                        pl[6 * (EW / 4)] = w0 ^ w3;
+                    }
+                    tmax = 0.0;
+                }
+                lds_barrier();
+#endif
                 // ---- 6. lag products on MFMA ----
                 mfma_group(std::integral_constant<int, 0>{}, std::integral_constant<int, CPW>{}, vals, k, t0, t1);
+#if STS_DIAG >= 3   // cost model: the per-tile flush of the 7 exact accumulators into the FP64 sums
+#pragma unroll
+                for (int w = 0; w < 7; w++) {
+#pragma unroll
+                    for (int r = 0; r < 4; r++) U[w & 1][r] = __builtin_fma((double)UI[w][r], c0 + (double)w, U[w & 1][r]);
+                    UI[w] = i4{0, 0, 0, 0};
+                }
+#endif
             }
         }
         have = have_next;

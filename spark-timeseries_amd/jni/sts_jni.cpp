@@ -3,8 +3,12 @@
 // Built only where a JDK is present (`make -C spark-timeseries_amd jni JAVA_HOME=...`); this
 // image has no JDK.  tests/test_jni_shim.py compiles it against a minimal
 // stand-in of the JNI C++ interface for a syntax/type check only; it runs on a JVM host.
-// The Scala side gathers a Spark partition's records into ONE
-// series-contiguous double[] panel (S x T) and makes one call per partition.
+// The Scala side makes one call per partition: either with the partition's
+// records gathered into ONE series-contiguous double[] panel (S x T), or -- the form the
+// TimeSeriesRDD drop-ins use -- with the records' own arrays (Array[Array[Double]]): the
+// *Records methods gather them into the pinned panel and return a FRESH double[] per record,
+// so every output record owns its vector as in the reference (TimeSeriesRDD.scala:538) and
+// no record pins a partition-sized array (findSeries, :80-82, keeps one record).
 //
 // Memory: a native method never holds a Java array across device work.  It copies the input
 // array into the calling thread's PINNED buffer with GetDoubleArrayRegion (one copy, no
@@ -41,6 +45,7 @@ Cls g_miae;                                   // MathIllegalArgumentException(Lo
 jobject g_not_enough = nullptr;               // LocalizedFormats.NOT_ENOUGH_DATA_FOR_NUMBER_OF_PREDICTORS
 jclass g_integer = nullptr;
 jclass g_object = nullptr;
+jclass g_double_array = nullptr;              // "[D": element class of the *Records results
 jmethodID g_int_valueof = nullptr;
 
 jclass global_class(JNIEnv* env, const char* name) {
@@ -170,6 +175,76 @@ struct Region {
 
 int64_t prod(int64_t a, int64_t b) { return (a > 0 && b > 0) ? a * b : 0; }
 
+// ---- per-record arrays: a partition's records in, one fresh array per record out ----
+
+// Gather the S records (each a double[] of length T, one shared DateTimeIndex) into the
+// series-contiguous panel dst.  Throws and returns false on a null or short record.
+bool gather_records(JNIEnv* env, jobjectArray recs, int64_t S, int64_t T, double* dst) {
+    for (int64_t s = 0; s < S; s++) {
+        jdoubleArray a = static_cast<jdoubleArray>(env->GetObjectArrayElement(recs, (jsize)s));
+        if (env->ExceptionCheck()) return false;
+        if (!a) {
+            throw_string(env, g_npe, "record vector is null");
+            return false;
+        }
+        const bool ok = (int64_t)env->GetArrayLength(a) == T;
+        if (ok && T > 0) env->GetDoubleArrayRegion(a, 0, (jsize)T, dst + s * T);
+        env->DeleteLocalRef(a);
+        if (!ok) {
+            throw_string(env, g_iae, "record vectors differ in length (a TimeSeriesRDD shares one DateTimeIndex)");
+            return false;
+        }
+    }
+    return true;
+}
+
+// A NEW double[T] per record from the panel src, in record order (nullptr + pending
+// exception when the JVM cannot allocate).
+jobjectArray scatter_records(JNIEnv* env, const double* src, int64_t S, int64_t T) {
+    if (!g_double_array) {
+        throw_string(env, g_rte, "double[] class not resolved");
+        return nullptr;
+    }
+    jobjectArray out = env->NewObjectArray((jsize)S, g_double_array, nullptr);
+    if (!out) return nullptr;
+    for (int64_t s = 0; s < S; s++) {
+        jdoubleArray a = env->NewDoubleArray((jsize)T);
+        if (!a) return nullptr;
+        if (T > 0) env->SetDoubleArrayRegion(a, 0, (jsize)T, src + s * T);
+        env->SetObjectArrayElement(out, (jsize)s, a);
+        env->DeleteLocalRef(a);
+        if (env->ExceptionCheck()) return nullptr;
+    }
+    return out;
+}
+
+// The record count and panel size of a *Records call; throws on a null record array or T < 0.
+bool records_shape(JNIEnv* env, jobjectArray recs, jlong T, int64_t* S) {
+    if (!recs) {
+        throw_string(env, g_npe, "records array is null");
+        return false;
+    }
+    if (T < 0) {
+        throw_string(env, g_iae, "negative series length");
+        return false;
+    }
+    *S = env->GetArrayLength(recs);
+    return true;
+}
+
+int method_code(JNIEnv* env, jstring method) {
+    if (!method) {
+        throw_string(env, g_npe, "fill method is null");
+        return -3;
+    }
+    const char* m = env->GetStringUTFChars(method, nullptr);
+    if (!m) return -3;
+    const int code = sts_fill_method_from_name(m);
+    env->ReleaseStringUTFChars(method, m);
+    if (code < 0) throw_for(env, STS_ERR_UNSUPPORTED_METHOD);
+    return code;
+}
+
 }  // namespace
 
 extern "C" {
@@ -188,6 +263,7 @@ JNIEXPORT jint JNICALL JNI_OnLoad(JavaVM* vm, void*) {
                      "(Lorg/apache/commons/math3/exception/util/Localizable;[Ljava/lang/Object;)V");
     g_integer = global_class(env, "java/lang/Integer");
     g_object = global_class(env, "java/lang/Object");
+    g_double_array = global_class(env, "[D");
     if (g_integer) {
         g_int_valueof = env->GetStaticMethodID(g_integer, "valueOf", "(I)Ljava/lang/Integer;");
         if (!g_int_valueof) env->ExceptionClear();
@@ -453,6 +529,70 @@ JNIEXPORT void JNICALL Java_com_cloudera_sparkts_StsNative_ar(JNIEnv* env, jclas
         if (st == STS_OK) ro.copy_out();
     }
     throw_for(env, st);
+}
+
+// ---- record-level forms (the TimeSeriesRDD drop-ins): each output
+//      record gets its own new double[] (TimeSeriesRDD.scala:538), in record order ----
+
+// TimeSeriesRDD.fill(method) over a partition's records (S/TimeSeriesRDD.scala:180-182)
+JNIEXPORT jobjectArray JNICALL Java_com_cloudera_sparkts_StsNative_fillRecords(JNIEnv* env, jclass,
+                                                                               jobjectArray recs, jlong T,
+                                                                               jstring method) {
+    int64_t S = 0;
+    if (!records_shape(env, recs, T, &S)) return nullptr;
+    const int code = method_code(env, method);
+    if (code < 0) return nullptr;
+    const int64_t n = prod(S, T);
+    double* in = t_in.get((size_t)(n > 0 ? n : 1) * sizeof(double));
+    double* out = t_out.get((size_t)(n > 0 ? n : 1) * sizeof(double));
+    if (!in || !out) return throw_for(env, STS_ERR_HIP), nullptr;
+    if (!gather_records(env, recs, S, T, in)) return nullptr;
+    const int st = sts_fill_host(in, out, S, T, T, code, nullptr);
+    if (st != STS_OK) return throw_for(env, st), nullptr;
+    return scatter_records(env, out, S, T);
+}
+
+// fill(method).mapSeries(differencesAtLag(_, lag)).mapSeries(EWMAModel(s).add...) per record (C2)
+JNIEXPORT jobjectArray JNICALL Java_com_cloudera_sparkts_StsNative_fillDiffEwmaRecords(
+    JNIEnv* env, jclass, jobjectArray recs, jlong T, jstring method, jint lag, jdoubleArray smoothing) {
+    int64_t S = 0;
+    if (!records_shape(env, recs, T, &S)) return nullptr;
+    const int code = method_code(env, method);
+    if (code < 0) return nullptr;
+    if (!check_len(env, smoothing, S, "fillDiffEwmaRecords: smoothing array shorter than the record count"))
+        return nullptr;
+    const int64_t n = prod(S, T);
+    double* in = t_in.get((size_t)(n > 0 ? n : 1) * sizeof(double));
+    double* out = t_out.get((size_t)(n > 0 ? n : 1) * sizeof(double));
+    if (!in || !out) return throw_for(env, STS_ERR_HIP), nullptr;
+    if (!gather_records(env, recs, S, T, in)) return nullptr;
+    Region rs(env, smoothing, S, true);
+    const int st = sts_fill_diff_ewma_host(in, out, S, T, T, code, lag, rs.p, nullptr);
+    if (st != STS_OK) return throw_for(env, st), nullptr;
+    return scatter_records(env, out, S, T);
+}
+
+// README.md:61 per record: ar(series, p).removeTimeDependentEffects(series); c (S) and
+// coef (S x p) receive the fitted models (S/models/Autoregression.scala:38-73, C4)
+JNIEXPORT jobjectArray JNICALL Java_com_cloudera_sparkts_StsNative_arFitRemoveRecords(
+    JNIEnv* env, jclass, jobjectArray recs, jlong T, jint p, jboolean noIntercept, jdoubleArray c,
+    jdoubleArray coef) {
+    int64_t S = 0;
+    if (!records_shape(env, recs, T, &S)) return nullptr;
+    if (!check_len(env, c, S, "arFitRemoveRecords: c array shorter than the record count") ||
+        !check_len(env, coef, prod(S, p), "arFitRemoveRecords: coefficient array shorter than S * maxLag"))
+        return nullptr;
+    const int64_t n = prod(S, T);
+    double* in = t_in.get((size_t)(n > 0 ? n : 1) * sizeof(double));
+    double* out = t_out.get((size_t)(n > 0 ? n : 1) * sizeof(double));
+    if (!in || !out) return throw_for(env, STS_ERR_HIP), nullptr;
+    if (!gather_records(env, recs, S, T, in)) return nullptr;
+    Region rc(env, c, S, false), rk(env, coef, prod(S, p), false);
+    const int st = sts_ar_fit_remove_host(in, out, S, T, T, p, noIntercept ? 1 : 0, rc.p, rk.p, nullptr);
+    if (st != STS_OK) return throw_for(env, st, (jint)(T - p), p), nullptr;
+    rc.copy_out();
+    rk.copy_out();
+    return scatter_records(env, out, S, T);
 }
 
 }  // extern "C"

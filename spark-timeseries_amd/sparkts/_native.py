@@ -13,7 +13,10 @@ import threading
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 PKG_ROOT = os.path.dirname(HERE)
-LIB_PATH = os.environ.get("STS_HIP_LIB", os.path.join(PKG_ROOT, "build", "libsts_hip.so"))
+# The product library is the in-tree build; the package reads no environment variable (an
+# executor's environment must not be able to swap the library).  Measurement tools select
+# another build explicitly with use_library() before the first call.
+LIB_PATH = os.path.join(PKG_ROOT, "build", "libsts_hip.so")
 
 _c_i64 = ctypes.c_int64
 _c_int = ctypes.c_int
@@ -83,6 +86,8 @@ SIGNATURES = {
     "sts_host_free": (_c_int, [_c_vp]),
     "sts_staging_release": (_c_int, []),
     "sts_staging_stats": (_c_int, [_c_vp]),
+    "sts_staging_set_limit": (_c_int, [_c_int]),
+    "sts_staging_pool_info": (_c_int, [_c_vp]),
     "sts_fill_autocorr_host": (_c_int, [_c_vp, _c_vp, _c_i64, _c_i64, _c_i64, _c_int, _c_int, _c_vp, _c_vp]),
     "sts_fill_diff_ewma_host": (_c_int, [_c_vp, _c_vp, _c_i64, _c_i64, _c_i64, _c_int, _c_int, _c_vp, _c_vp]),
     "sts_ar_fit_remove_host": (_c_int, [_c_vp, _c_vp, _c_i64, _c_i64, _c_i64, _c_int, _c_int, _c_vp, _c_vp, _c_vp]),
@@ -117,6 +122,19 @@ def load_library(path: str = LIB_PATH):
 
 def lib():
     return load_library()
+
+
+def use_library(path: str) -> None:
+    """Bind the process to ANOTHER build of the library (same C ABI) before its first use:
+    bench.py / tools/ pass their STS_HIP_LIB here for same-box A/B runs of tools/variant.sh
+    builds.  Not called by the product path."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            raise NativeLibraryError("use_library(%s): a library is already loaded" % path)
+    v = load_variant(path)
+    with _lock:
+        _lib = v
 
 
 _variants = {}

@@ -98,15 +98,55 @@ def toWire(rdd) -> bytes:
     return bytes(out)
 
 
-def timeSeriesRDDFromObservations(targetIndex, keys, timestamps, values, device=None):
+def java_string_hash(s: str) -> int:
+    """java.lang.String.hashCode: h = 31 h + c over the UTF-16 code units, int32 wrap-around."""
+    h = 0
+    for cu in utf16_units(s):
+        h = (31 * h + cu) & 0xFFFFFFFF
+    return h - (1 << 32) if h >= (1 << 31) else h
+
+
+def utf16_units(s: str):
+    """The UTF-16 code units of s (java.lang.String's chars): String.compareTo orders by them."""
+    b = s.encode("utf-16-be", "surrogatepass")
+    return struct.unpack(">%dH" % (len(b) // 2), b)
+
+
+def hash_partition(key: str, num_partitions: int) -> int:
+    """Spark's HashPartitioner.getPartition for a String key: Utils.nonNegativeMod(
+    key.hashCode, numPartitions) (Java's % truncates toward zero; a negative remainder is
+    shifted up by numPartitions)."""
+    h = java_string_hash(key)
+    raw = abs(h) % num_partitions
+    if h < 0:
+        raw = -raw
+    return raw + num_partitions if raw < 0 else raw
+
+
+def observation_key_order(keys, num_partitions: int = 1):
+    """The record order of timeSeriesRDDFromObservations (S/TimeSeriesRDD.scala:502-514): the
+    observations are shuffled by HashPartitioner(numPartitions) on the key and sorted within
+    each partition by (key, timestamp) with String.compareTo; one record per key, partition
+    0's keys first.  Returns (ordered unique keys, partition of each)."""
+    uniq = set(keys)
+    part = {k: hash_partition(k, num_partitions) for k in uniq}
+    ordered = sorted(uniq, key=lambda k: (part[k], utf16_units(k)))
+    return ordered, [part[k] for k in ordered]
+
+
+def timeSeriesRDDFromObservations(targetIndex, keys, timestamps, values, device=None, numPartitions=1):
     """S/TimeSeriesRDD.scala:493-542.  targetIndex: sorted instants (int64 / datetime64);
-    keys: one string per observation; timestamps: one instant per observation.  Series come
-    out in sorted key order (the reference sorts by key within its partitions); timestamps
-    not in the index are dropped (locAtDateTime == -1); among observations of one cell the
-    last in input order wins."""
+    keys: one string per observation; timestamps: one instant per observation; numPartitions:
+    the input RDD's partition count (the reference shuffles into that many partitions).
+    Series come out in the reference's record order: by hash partition of the key, then by
+    String.compareTo within the partition (observation_key_order); timestamps not in the
+    index are dropped (locAtDateTime == -1); among observations of one cell the last in input
+    order wins.  The result's `partitions` lists each record's partition."""
     from .timeseriesrdd import TimeSeriesRDD
     torch = _torch()
     dev = _device(device)
+    if numPartitions < 1:
+        raise ValueError("numPartitions must be >= 1")
     idx = np.asarray(targetIndex)
     ts = np.asarray(timestamps)
     if idx.dtype.kind == "M":
@@ -115,11 +155,14 @@ def timeSeriesRDDFromObservations(targetIndex, keys, timestamps, values, device=
         ts = ts.astype("datetime64[ns]").astype(np.int64)
     idx = idx.astype(np.int64)
     ts = ts.astype(np.int64)
-    uniq, sid = np.unique(np.asarray(keys, dtype=object).astype(str), return_inverse=True)
+    key_list = [str(k) for k in keys]
+    order, parts = observation_key_order(key_list, numPartitions)
+    rank = {k: i for i, k in enumerate(order)}
+    sid = np.fromiter((rank[k] for k in key_list), dtype=np.int64, count=len(key_list))
     pos = np.searchsorted(idx, ts)
     pos_c = np.minimum(pos, max(len(idx) - 1, 0))
     loc = np.where((len(idx) > 0) & (idx[pos_c] == ts), pos_c, -1).astype(np.int64)
-    S, T = len(uniq), len(idx)
+    S, T = len(order), len(idx)
     panel = torch.empty((S, T), dtype=torch.float64, device=dev)
     n = len(ts)
     sid_d = torch.as_tensor(sid.astype(np.int32), device=dev)
@@ -127,7 +170,9 @@ def timeSeriesRDDFromObservations(targetIndex, keys, timestamps, values, device=
     val_d = torch.as_tensor(np.asarray(values, dtype=np.float64), device=dev)
     check(_native.lib().sts_observations_to_panel(ptr(sid_d), ptr(loc_d), ptr(val_d), n, ptr(panel), S, T, T,
                                                   _stream(dev)), "timeSeriesRDDFromObservations")
-    return TimeSeriesRDD(targetIndex, list(uniq), panel)
+    rdd = TimeSeriesRDD(targetIndex, list(order), panel)
+    rdd.partitions = parts
+    return rdd
 
 
 def csv_parse(text: bytes):

@@ -6,14 +6,23 @@
 // its documented status without touching memory it does not own -- and then with valid
 // arguments, which on a machine without a gfx950 device must fail cleanly with
 // STS_ERR_NO_DEVICE or STS_ERR_HIP.  Prints "ok" and exits 0 when every status matched.
+//
+// `host_args_san N` runs the whole sequence in N threads at once (the ThreadSanitizer build
+// of tests/test_sanitizers.py: Spark's N executor threads calling the ABI concurrently,
+// S/TimeSeriesRDD.scala:417-421), and checks that sts_last_error() stays per thread: each
+// thread's own failing call leaves its own message, whatever the other threads do meanwhile.
+#include <atomic>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <string>
+#include <thread>
 #include <vector>
 
 #include "sts.h"
 
-static int failures = 0;
+static std::atomic<int> failures{0};
 
 static void expect(int got, int want, const char* what) {
     if (got != want) {
@@ -29,7 +38,7 @@ static void expect_no_device(int got, const char* what) {
     }
 }
 
-int main() {
+static void run_checks(int tid) {
     const int64_t S = 3, T = 50;
     std::vector<double> in(S * T, 1.0), out(S * T), acf(S * 70), c(S), coef(S * 8), sm(S, 0.2), par(S * 3);
     std::vector<int32_t> err(S);
@@ -83,7 +92,36 @@ int main() {
     expect_no_device(sts_ar_fit_remove_host(in.data(), out.data(), S, T, T, 5, 0, c.data(), coef.data(), nullptr),
                      "ar_fit_remove");
     expect_no_device(sts_init(0), "init");
+    // staging pool controls
+    expect(sts_staging_set_limit(0), STS_ERR_BAD_ARG, "staging limit 0");
+    expect(sts_staging_set_limit(2 + tid % 3), STS_OK, "staging limit");
+    expect(sts_staging_pool_info(nullptr), STS_ERR_BAD_ARG, "pool info null");
+    // the thread-local error message: this thread's failing call, other threads' calls in
+    // between, still this thread's message
+    char want[64];
+    std::snprintf(want, sizeof want, "S=%d,", -(tid + 1));
+    expect(sts_fill_host(in.data(), out.data(), -(tid + 1), T, T, STS_FILL_LINEAR, nullptr), STS_ERR_BAD_ARG,
+           "fill S < 0 (per thread)");
+    for (int k = 0; k < 200; k++) std::this_thread::yield();
+    const std::string msg = sts_last_error();
+    if (msg.find(want) == std::string::npos) {
+        std::printf("FAIL thread %d: last error \"%s\" is not its own (%s)\n", tid, msg.c_str(), want);
+        failures++;
+    }
     sts_staging_release();
+}
+
+int main(int argc, char** argv) {
+    const int nthreads = argc > 1 ? std::atoi(argv[1]) : 0;
+    if (nthreads <= 0) {
+        run_checks(0);
+    } else {
+        for (int rep = 0; rep < 3; rep++) {
+            std::vector<std::thread> th;
+            for (int t = 0; t < nthreads; t++) th.emplace_back(run_checks, t);
+            for (auto& t : th) t.join();
+        }
+    }
     if (failures) return 1;
     std::puts("ok");
     return 0;

@@ -1,7 +1,9 @@
 /* Minimal STAND-IN for the JNI C++ interface -- only the types and JNIEnv / JavaVM members
  * spark-timeseries_amd/jni/sts_jni.cpp uses, with the JDK's signatures, so that
- * tests/test_jni_shim.py can type-check the shim in an image without a JDK.  It is never
- * linked or run; the shim is built against a real JDK's jni.h (Makefile target `jni`). */
+ * tests/test_jni_shim.py can type-check the shim in an image without a JDK, and link it
+ * against tests/native/jni_fake_env.cpp (an in-memory stand-in JVM heap that implements these
+ * members) to exercise the shim's gather / scatter and exception paths on the CPU.  The
+ * product shim is built against a real JDK's jni.h (Makefile target `jni`). */
 #pragma once
 #include <cstdarg>
 #include <cstdint>
@@ -53,6 +55,8 @@ struct JNIEnv {
     jobject NewObject(jclass clazz, jmethodID methodID, ...);
     jobjectArray NewObjectArray(jsize len, jclass clazz, jobject init);
     void SetObjectArrayElement(jobjectArray array, jsize index, jobject val);
+    jobject GetObjectArrayElement(jobjectArray array, jsize index);
+    jdoubleArray NewDoubleArray(jsize len);
     jsize GetArrayLength(jarray array);
     void GetDoubleArrayRegion(jdoubleArray array, jsize start, jsize len, jdouble* buf);
     void SetDoubleArrayRegion(jdoubleArray array, jsize start, jsize len, const jdouble* buf);

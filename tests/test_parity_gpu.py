@@ -900,17 +900,21 @@ def test_wire_decode_encode_round_trip(torch):
         assert sio.toWire(rdd) == data                       # KeyAndSeriesToBytes, byte for byte
 
 
-def test_observations_to_panel(torch):
+@pytest.mark.parametrize("parts", [1, 4, 13])
+def test_observations_to_panel(torch, parts):
+    # S/TimeSeriesRDD.scala:493-542 with the input RDD in `parts` partitions: records in the
+    # reference's order (hash partition of the key, then String.compareTo)
     from sparkts import io as sio
     rng = np.random.default_rng(8)
     idx = np.arange(0, 5000, 5, dtype=np.int64)             # 1000 instants
     n = 20000
     keys = ["s%03d" % k for k in rng.integers(0, 150, n)]
+    keys[::97] = ["\U0001F600x", "\uffffy", "\u00e9"] * (len(keys[::97]) // 3) + ["z"] * (len(keys[::97]) % 3)
     ts = rng.integers(0, 5100, n).astype(np.int64)          # some off-grid / past the end: dropped
     ts[::3] = ts[::3] // 5 * 5                              # many on the grid, duplicates included
     vals = rng.standard_normal(n)
-    rdd = sio.timeSeriesRDDFromObservations(idx, keys, ts, vals)
-    ref_keys, ref = oracle.observations_to_panel(idx, keys, ts, vals)
+    rdd = sio.timeSeriesRDDFromObservations(idx, keys, ts, vals, numPartitions=parts)
+    ref_keys, ref = oracle.observations_to_panel(idx, keys, ts, vals, num_partitions=parts)
     assert rdd.keys == ref_keys
     assert_bits(host(rdd.data), ref, "observations")
 

@@ -11,6 +11,11 @@
   documented status, valid calls fail cleanly without a device
   (tests/native/host_args_san.cpp).
 
+* ThreadSanitizer (round 3, VERDICT r2 "reentrancy"): the staging slot-set pool
+  (csrc/sts_stage_pool.hpp) with fake sets under 16 threads (tests/native/stage_pool_tsan.cpp),
+  and sts_api.cpp + sts_host.cpp driven through every argument path from 8 threads at once
+  (tests/native/host_args_san.cpp N), checking that sts_last_error() stays per thread.
+
 Every build uses -fno-sanitize-recover=all, so any report fails the run.
 """
 import os
@@ -105,3 +110,40 @@ def test_host_entry_points_under_asan_ubsan(tmp_path):
     env = dict(ENV, ASAN_OPTIONS="detect_leaks=0", HIP_VISIBLE_DEVICES="")
     r = subprocess.run([exe], capture_output=True, text=True, env=env, timeout=300)
     assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stdout[-3000:] + r.stderr[-4000:]
+
+
+TSAN = ["-fsanitize=thread", "-g", "-O1"]
+TSAN_ENV = dict(os.environ, TSAN_OPTIONS="halt_on_error=1:second_deadlock_stack=1")
+
+
+def test_stage_pool_under_tsan(tmp_path):
+    gxx = need("g++")
+    exe = str(tmp_path / "stage_pool_tsan")
+    subprocess.check_call([gxx, *TSAN, "-std=c++17", "-I", CSRC, os.path.join(NATIVE, "stage_pool_tsan.cpp"),
+                           "-o", exe, "-pthread"])
+    r = subprocess.run([exe, "16", "400"], capture_output=True, text=True, env=TSAN_ENV, timeout=600)
+    assert r.returncode == 0 and r.stdout.strip().startswith("ok"), r.stdout[-3000:] + r.stderr[-6000:]
+    assert "WARNING: ThreadSanitizer" not in r.stderr, r.stderr[-6000:]
+
+
+def test_host_entry_points_concurrent_under_tsan(tmp_path):
+    hipcc = need("/opt/rocm/bin/hipcc")
+    objdir = os.path.join(ROOT, "spark-timeseries_amd", "build", "obj")
+    dev_objs = sorted(os.path.join(objdir, f) for f in os.listdir(objdir) if f.endswith(".hip.o")) \
+        if os.path.isdir(objdir) else []
+    if not dev_objs:
+        pytest.skip("device objects not built (run __graft_entry__.build())")
+    flags = [*TSAN, "-std=c++17", "-fPIC", "-fno-gpu-sanitize", "-I", os.path.join(ROOT, "include"), "-I", CSRC]
+    objs = []
+    for src in (os.path.join(CSRC, "sts_api.cpp"), os.path.join(CSRC, "sts_host.cpp"),
+                os.path.join(NATIVE, "host_args_san.cpp")):
+        o = str(tmp_path / (os.path.basename(src) + ".tsan.o"))
+        subprocess.check_call([hipcc, *flags, "-c", src, "-o", o])
+        objs.append(o)
+    exe = str(tmp_path / "host_args_tsan")
+    subprocess.check_call([hipcc, "-fsanitize=thread", "-fno-gpu-sanitize", "--offload-arch=gfx950",
+                           *objs, *dev_objs, "-o", exe, "-pthread"])
+    env = dict(TSAN_ENV, HIP_VISIBLE_DEVICES="")
+    r = subprocess.run([exe, "8"], capture_output=True, text=True, env=env, timeout=600)
+    assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stdout[-3000:] + r.stderr[-6000:]
+    assert "WARNING: ThreadSanitizer" not in r.stderr, r.stderr[-6000:]

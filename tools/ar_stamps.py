@@ -13,6 +13,8 @@ os.environ.setdefault("STS_HIP_LIB", os.path.join(ROOT, "spark-timeseries_amd", 
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 from sparkts import _native  # noqa: E402
+if os.environ.get("STS_HIP_LIB"):   # a tools/variant.sh build
+    _native.use_library(os.environ["STS_HIP_LIB"])
 
 NAMES = ["load+mean", "passA lag products", "reductions", "gram+chol+solve", "passB residual",
          "refine solve", "passC remove"]

@@ -26,5 +26,7 @@ for s in ${STEPS:-c1 c2 c4 c5 prof fetch write}; do
     fp64_c3|fp64_c4) W=${s#fp64_}; step pmc_$s 300 rocprofv3 --pmc SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MFMA_MOPS_F64 SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE -d gpurun_out/pmc_$s -o bench --output-format csv -- python -u bench.py --workload $W --steps 2 --warmup 0 --no-cpu-baseline ;;
     tests) step pytest_gpu 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider ;;
     custom) step custom ${CUSTOM_SECS:-300} bash -c "$CUSTOM_CMD" ;;
+    pytest) step pytest_sel ${TEST_SECS:-900} python -u -m pytest $TEST_FILES -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider ;;
+    ab) step ab_libs ${AB_SECS:-600} bash tools/ab_libs.sh "$AB_CASES" $AB_LIBS ;;
   esac
 done

@@ -19,6 +19,8 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 from sparkts import _native  # noqa: E402
+if os.environ.get("STS_HIP_LIB"):   # a tools/variant.sh build
+    _native.use_library(os.environ["STS_HIP_LIB"])
 
 METHODS = {"linear": 0, "nearest": 1, "next": 2, "previous": 3, "none": -1}
 

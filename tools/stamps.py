@@ -18,6 +18,8 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 from sparkts import _native  # noqa: E402
+if os.environ.get("STS_HIP_LIB"):   # a tools/variant.sh build
+    _native.use_library(os.environ["STS_HIP_LIB"])
 
 NAMES = ["regs->LDS", "bar A", "ballots", "bar B", "scan+NaN list", "bar C", "NaN fill", "bar D",
          "store+y+prefetch", "bar E", "MFMA", "bar F"]
