@@ -130,6 +130,12 @@ __device__ __forceinline__ unsigned long long interleave2(unsigned ev, unsigned 
     return (bitrep(ev) & 0x5555555555555555ull) | (bitrep(od) & 0xAAAAAAAAAAAAAAAAull);
 }
 
+// v_writelane with a constant lane: lane L of v takes the wave-uniform x (no exec change)
+template <int L>
+__device__ __forceinline__ void wlane(int& v, unsigned x) {
+    asm("v_writelane_b32 %0, %1, %2" : "+v"(v) : "s"(x), "n"(L));
+}
+
 // Wave-wide scans of one int per lane for wave 0's word scan: DPP within rows of 16 lanes
 // (row_shr / row_shl 1, 2, 4, 8; lanes without a source keep the identity) and readlane
 // carries across the four rows -- VALU-latency steps instead of one ds_bpermute round trip
@@ -283,10 +289,14 @@ __global__ __launch_bounds__(NTH, (DB || DMA) ? 2 : STS_TILE_WGS) void tile_kern
         STS_LD1(5) STS_LD1(6) STS_LD1(7) STS_LD1(8)                                         \
     } while (0)
 // define R on the no-prefetch path too, so the registers are dead between their store to
-// LDS and the next issue (otherwise the loop-carried values stay live across the body)
+// LDS and the next issue (otherwise the loop-carried values stay live across the body).  An
+// empty asm that "writes" them defines them with no instruction (round 3: the zeroing moves
+// it replaced were hoisted above the prefetch branch, 18 VALU per wave and tile); the values
+// are never read (every read of R sits behind `have`).
 #define STS_CLEAR()                                                                         \
     do {                                                                                    \
-        R0 = R1 = R2 = R3 = R4 = R5 = R6 = R7 = R8 = make_double2(0.0, 0.0);                \
+        asm volatile("" : "=v"(R0), "=v"(R1), "=v"(R2), "=v"(R3), "=v"(R4));               \
+        asm volatile("" : "=v"(R5), "=v"(R6), "=v"(R7), "=v"(R8));                         \
     } while (0)
 // DMA: wave w issues the 1-KB pieces m = w, w + kWaves, ... of interior tile kk into the
 // staging image (pieces past the tile read its first piece into the image's tail)
@@ -309,10 +319,12 @@ __global__ __launch_bounds__(NTH, (DB || DMA) ? 2 : STS_TILE_WGS) void tile_kern
         const int q2_ = tid + j * kThreads;                                                 \
         R##j = g2_[q2_ < NP2 ? q2_ : NP2 - 1];                                              \
     }
+// (the bound test only where it can fail: a runtime test on every register kept a spilled
+// exec mask per register alive across the tile loop)
 #define STS_ST1(j)                                                                          \
     if constexpr (j < RPT) {                                                                \
         const int q2_ = tid + j * kThreads;                                                 \
-        if (q2_ < NP2) v2_[px2(q2_)] = R##j;                                                \
+        if ((j + 1) * kThreads <= NP2 || q2_ < NP2) v2_[px2(q2_)] = R##j;                   \
     }
 
     d4 U[NA];
@@ -540,18 +552,28 @@ __global__ __launch_bounds__(NTH, (DB || DMA) ? 2 : STS_TILE_WGS) void tile_kern
             }
             double2* v2_ = reinterpret_cast<double2*>(vals);
             STS_ST1(0) STS_ST1(1) STS_ST1(2) STS_ST1(3) STS_ST1(4) STS_ST1(5) STS_ST1(6) STS_ST1(7) STS_ST1(8)
+// The two words of register j go into lanes 4j .. 4j + 3 of one VGPR (v_writelane, no
+// branch), and one LDS store per wave writes them all (round 3: a lane-0 store per word
+// behind per-word bound tests cost ~20 SALU and 4 spilled-mask reloads per register).
 #define STS_BAL1(j)                                                                         \
     if constexpr (j < RPT) {                                                                \
         const unsigned long long bx_ = __ballot(!isnan_d(R##j.x));                          \
         const unsigned long long by_ = __ballot(!isnan_d(R##j.y));                          \
-        const int w_ = 2 * wave + 2 * kWaves * j;                                                  \
-        if (lane == 0) {                                                                    \
-            if (w_ < NW) mask[w_] = interleave2((unsigned)bx_, (unsigned)by_);              \
-            if (w_ + 1 < NW) mask[w_ + 1] = interleave2((unsigned)(bx_ >> 32), (unsigned)(by_ >> 32)); \
-        }                                                                                   \
+        const unsigned long long lo_ = interleave2((unsigned)bx_, (unsigned)by_);           \
+        const unsigned long long hi_ = interleave2((unsigned)(bx_ >> 32), (unsigned)(by_ >> 32)); \
+        wlane<4 * j + 0>(mv_, (unsigned)lo_);                                               \
+        wlane<4 * j + 1>(mv_, (unsigned)(lo_ >> 32));                                       \
+        wlane<4 * j + 2>(mv_, (unsigned)hi_);                                               \
+        wlane<4 * j + 3>(mv_, (unsigned)(hi_ >> 32));                                       \
     }
-            STS_BAL1(0) STS_BAL1(1) STS_BAL1(2) STS_BAL1(3) STS_BAL1(4) STS_BAL1(5) STS_BAL1(6) STS_BAL1(7)
-            STS_BAL1(8)
+            {
+                int mv_ = 0;
+                STS_BAL1(0) STS_BAL1(1) STS_BAL1(2) STS_BAL1(3) STS_BAL1(4) STS_BAL1(5) STS_BAL1(6)
+                STS_BAL1(7) STS_BAL1(8)
+                // lane i: dword (i & 1) of word 2 wave + 2 kWaves (i / 4) + ((i >> 1) & 1)
+                const int w_ = 2 * wave + 2 * kWaves * (lane >> 2) + ((lane >> 1) & 1);
+                if (lane < 4 * RPT && w_ < NW) reinterpret_cast<int*>(mask)[2 * w_ + (lane & 1)] = mv_;
+            }
 #undef STS_BAL1
         } else {
             for (int q = tid; q < EW; q += kThreads) {
@@ -837,7 +859,11 @@ __global__ __launch_bounds__(NTH, (DB || DMA) ? 2 : STS_TILE_WGS) void tile_kern
                 constexpr int FH = (FY + 1) / 2;     // two halves: fewer live registers
                 const int vq = (kHB >> 1) + tid;
                 const bool wr = dst != nullptr;   // wave-uniform (a null test of dp is per lane)
-                double2* dp = reinterpret_cast<double2*>(dst + t0) + tid;
+                // uniform tile base (SGPRs) + a 32-bit lane offset: the saddr store form, no
+                // 64-bit per-lane pointer kept live across the tile loop
+                char* const dpb = reinterpret_cast<char*>(dst + t0);
+                unsigned dpo = (unsigned)tid * 16u;
+                asm volatile("" : "+v"(dpo));   // per tile: else LICM keeps dst + dpo as a 64-bit VGPR pair
 #pragma unroll
                 for (int h = 0; h < 2; h++) {
                     double2 fv[FH];
@@ -855,8 +881,9 @@ __global__ __launch_bounds__(NTH, (DB || DMA) ? 2 : STS_TILE_WGS) void tile_kern
                         const bool in = jj * kThreads + kThreads <= NP2 - kHB / 2 ||
                                         tid + jj * kThreads < NP2 - kHB / 2;
                         if (jj < FS && wr) {   // non-temporal: A/B on C3 +1 %
-                            __builtin_nontemporal_store(fv[j].x, &dp[jj * kThreads].x);
-                            __builtin_nontemporal_store(fv[j].y, &dp[jj * kThreads].y);
+                            double2* dq = reinterpret_cast<double2*>(dpb + jj * kThreads * 16 + dpo);
+                            __builtin_nontemporal_store(fv[j].x, &dq->x);
+                            __builtin_nontemporal_store(fv[j].y, &dq->y);
                         }
                         if (NT > 0 && in) {
                             double2 y;
