@@ -58,11 +58,15 @@
 #endif
 
 #ifndef STS_TILE_WGS
-#define STS_TILE_WGS 3    // workgroups per CU the register budget is sized for
+#define STS_TILE_WGS 4    // workgroups per CU the register budget is sized for (128 VGPRs; LDS 40.5 KB x 4 fits)
 #endif
 
 #ifndef STS_TILE_DMA
 #define STS_TILE_DMA 0    // A/B: the next interior tile arrives by LDS-DMA into a staging buffer, issued at tile start
+#endif
+
+#ifndef STS_PF_POS
+#define STS_PF_POS 0      // A/B: 1 = the next tile's register prefetch is issued before the store pass
 #endif
 
 #ifndef STS_EARLY
@@ -128,6 +132,14 @@ __device__ __forceinline__ unsigned long long bitrep(unsigned x) {
 }
 __device__ __forceinline__ unsigned long long interleave2(unsigned ev, unsigned od) {
     return (bitrep(ev) & 0x5555555555555555ull) | (bitrep(od) & 0xAAAAAAAAAAAAAAAAull);
+}
+
+// An opaque copy of a per-lane value: computed where it is used, per tile, instead of being
+// hoisted out of the tile loop by LICM and kept live in a VGPR for the whole kernel (round 3:
+// ~50 VGPRs of hoisted per-lane LDS addresses that are one base plus immediate offsets)
+__device__ __forceinline__ int opq(int x) {
+    asm volatile("" : "+v"(x));
+    return x;
 }
 
 // v_writelane with a constant lane: lane L of v takes the wave-uniform x (no exec change)
@@ -209,6 +221,10 @@ __global__ __launch_bounds__(NTH, (DB || DMA) ? 2 : STS_TILE_WGS) void tile_kern
     constexpr int EWP = PAD ? EW + EW / 8 : EW;
     auto px = [](int q) { return px_<PAD>(q); };
     auto px2 = [](int q2) { return px2_<PAD>(q2); };
+    // px2(q2 + kThreads) - px2(q2) (kThreads is a multiple of 16) and px(q + 64) - px(q)
+    constexpr int PX2S = PAD ? kThreads + 2 * (kThreads / 16) : kThreads;
+    constexpr int PXW = PAD ? 72 : 64;
+    static_assert(kThreads % 16 == 0, "linear padded strides");
     constexpr int NW = EW / 64;
     constexpr int NP2 = EW / 2;                              // double2 per extended tile
     constexpr int RPT = (NP2 + kThreads - 1) / kThreads;     // prefetch registers per thread
@@ -324,7 +340,7 @@ __global__ __launch_bounds__(NTH, (DB || DMA) ? 2 : STS_TILE_WGS) void tile_kern
 #define STS_ST1(j)                                                                          \
     if constexpr (j < RPT) {                                                                \
         const int q2_ = tid + j * kThreads;                                                 \
-        if ((j + 1) * kThreads <= NP2 || q2_ < NP2) v2_[px2(q2_)] = R##j;                   \
+        if ((j + 1) * kThreads <= NP2 || q2_ < NP2) v2_[pst_ + j * PX2S] = R##j;            \
     }
 
     d4 U[NA];
@@ -416,8 +432,8 @@ __global__ __launch_bounds__(NTH, (DB || DMA) ? 2 : STS_TILE_WGS) void tile_kern
                     const int j = lane & 15;
                     const int ra = QS * t + lane;
                     const int rb = QS * t + 16 * (lane >> 4) + 16 * (j / QS) + (16 - QS) + (j % QS);
-                    oa[t] = px(ra);
-                    ob[t] = px(rb);
+                    oa[t] = opq(px(ra));
+                    ob[t] = opq(px(rb));
                 }
                 auto chunk_mfma = [&](const double* yb) {
                     double av[NTA], bv[NTA];
@@ -551,6 +567,7 @@ __global__ __launch_bounds__(NTH, (DB || DMA) ? 2 : STS_TILE_WGS) void tile_kern
                 STS_DMA_TAKE();
             }
             double2* v2_ = reinterpret_cast<double2*>(vals);
+            const int pst_ = opq(px2(tid));   // px2(tid + j kThreads) = px2(tid) + j PX2S
             STS_ST1(0) STS_ST1(1) STS_ST1(2) STS_ST1(3) STS_ST1(4) STS_ST1(5) STS_ST1(6) STS_ST1(7) STS_ST1(8)
 // The two words of register j go into lanes 4j .. 4j + 3 of one VGPR (v_writelane, no
 // branch), and one LDS store per wave writes them all (round 3: a lane-0 store per word
@@ -606,11 +623,12 @@ __global__ __launch_bounds__(NTH, (DB || DMA) ? 2 : STS_TILE_WGS) void tile_kern
 
         // ---- 2. validity ballots from LDS for the edge tiles (wave v owns words v, v+4, ...) ----
         if (!have) {
+            const int pb = opq(px(lane) + PXW * wave);   // px(64 w + lane) = px(lane) + PXW w
 #pragma unroll 2
             for (int i = 0; i < (NW + kWaves - 1) / kWaves; i++) {
                 const int w = wave + i * kWaves;
                 if (w < NW) {
-                    const unsigned long long m = __ballot(!isnan_d(vals[px(w * 64 + lane)]));
+                    const unsigned long long m = __ballot(!isnan_d(vals[pb + PXW * kWaves * i]));
                     if (lane == 0) mask[w] = m;
                 }
             }
@@ -842,6 +860,13 @@ __global__ __launch_bounds__(NTH, (DB || DMA) ? 2 : STS_TILE_WGS) void tile_kern
         lds_barrier();
         STAMP(7);
 
+#if STS_PF_POS == 1
+        // A/B: the next tile's loads before the store pass (in flight during stores + MFMA)
+        if constexpr (!DMA) {
+            if (have_next) STS_ISSUE(k + 1);
+            else STS_CLEAR();
+        }
+#endif
         // ---- 5. filled output + lag matrix (16-B stores), then y = F - F(0) in place
         //      (0 past the series end) for the MFMA phase; start the next tile's loads ----
         {
@@ -858,6 +883,7 @@ __global__ __launch_bounds__(NTH, (DB || DMA) ? 2 : STS_TILE_WGS) void tile_kern
                 constexpr int FY = NT > 0 ? (NP2 - kHB / 2 + kThreads - 1) / kThreads : FS;
                 constexpr int FH = (FY + 1) / 2;     // two halves: fewer live registers
                 const int vq = (kHB >> 1) + tid;
+                const int pvq = opq(px2(vq));   // px2(vq + jj kThreads) = pvq + jj PX2S
                 const bool wr = dst != nullptr;   // wave-uniform (a null test of dp is per lane)
                 // uniform tile base (SGPRs) + a 32-bit lane offset: the saddr store form, no
                 // 64-bit per-lane pointer kept live across the tile loop
@@ -872,7 +898,7 @@ __global__ __launch_bounds__(NTH, (DB || DMA) ? 2 : STS_TILE_WGS) void tile_kern
                         const int jj = h * FH + j;
                         if (jj < FY && (jj * kThreads + kThreads <= NP2 - kHB / 2 ||
                                         tid + jj * kThreads < NP2 - kHB / 2))
-                            fv[j] = v2[px2(vq + jj * kThreads)];
+                            fv[j] = v2[pvq + jj * PX2S];
                     }
 #pragma unroll
                     for (int j = 0; j < FH; j++) {
@@ -889,7 +915,7 @@ __global__ __launch_bounds__(NTH, (DB || DMA) ? 2 : STS_TILE_WGS) void tile_kern
                             double2 y;
                             y.x = fv[j].x - c0;
                             y.y = fv[j].y - c0;
-                            v2[px2(vq + jj * kThreads)] = y;
+                            v2[pvq + jj * PX2S] = y;
 #if STS_DIAG >= 3   // cost model: the middle sums move from the MFMA loop to this pass
                             acc_s += y.x + y.y;
                             acc_q = __builtin_fma(y.x, y.x, __builtin_fma(y.y, y.y, acc_q));
@@ -939,8 +965,10 @@ __global__ __launch_bounds__(NTH, (DB || DMA) ? 2 : STS_TILE_WGS) void tile_kern
 #endif
         {
             if constexpr (DMA) STS_CLEAR();
+#if STS_PF_POS == 0
             else if (have_next) STS_ISSUE(k + 1);   // in flight during the MFMA phase of tile k
             else STS_CLEAR();
+#endif
         }
         STAMP(8);
 
