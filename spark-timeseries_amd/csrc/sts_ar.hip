@@ -298,67 +298,22 @@ struct ArWaveLds {
 // registers, and the fused residuals go out through it again (16-B LDS writes at the lanes'
 // block offsets, then 1-KB coalesced stores).  Without DMA every load / store instruction
 // touches one 16-B piece per lane at a B * 8-byte stride: 64 cache lines per instruction.
-// PERS (round 3, A/B build only -- STS_AR_PERS; measured 7.0-7.2 ms against 5.3 ms for the
-// one-series-per-wave form on C4): persistent waves, two per SIMD, one LDS block
-// per wave.  As soon as series
-// k's block is in registers, series k + 1's block streams into the same LDS block by
-// LDS-DMA, so the load latency that bounded the one-series-per-wave form (~47 % of a series'
-// time waiting for its block) hides behind series k's passes.  The fit's scratch (head /
-// tail values, column sums, L) moves to the block's unused end [T, 64 B), which the DMA never
-// writes (it masks the lanes past the row), and the residuals leave straight from registers
-// as B / 2 16-B stores per lane.  The host launches it for aligned panels (16-B aligned rows,
-// T and both row strides even) with T + 3P + 1 + P (P + 1) / 2 <= 64 B and T >= 16.
-template <int N>
-__device__ __forceinline__ void dma_wait_n() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
-
-template <int P, int B, int NWV = kRegWaves, bool DMA = false, bool PERS = false>
+template <int P, int B, int NWV = kRegWaves, bool DMA = false>
 __global__ __launch_bounds__(64 * NWV, STS_AR_WAVES_PER_EU) void ar_fit_blk_kernel(ArArgs a) {
     constexpr int BUFD = 64 * B;              // doubles per wave block
     static_assert(!DMA || sizeof(ArWaveLds) <= BUFD * sizeof(double), "scratch fits the block");
-    static_assert(!PERS || DMA, "the persistent form streams by DMA");
-    static_assert(B / 2 <= 63, "vmcnt range");
-    constexpr int WLD = (int)((sizeof(ArWaveLds) + sizeof(double) - 1) / sizeof(double));
-    // DMA: the wave blocks (the fit's scratch aliases the current one); else one scratch per wave
-    __shared__ __attribute__((aligned(16))) double buf_mem[DMA ? NWV * BUFD : NWV * WLD];
+    __shared__ __attribute__((aligned(16))) double buf_mem[DMA ? NWV * BUFD : 2];
+    __shared__ ArWaveLds lds_mem[DMA ? 1 : NWV];
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int T = (int)a.T;
-    const bool intercept = !a.no_intercept;
-    const int64_t s_first = (int64_t)blockIdx.x * NWV + wave;
-    const int64_t s_step = PERS ? (int64_t)gridDim.x * NWV : a.S;
-    // one block = B / 2 DMA pieces of 1 KB: piece i holds positions [128 i, 128 i + 128)
-    auto issue_block = [&](int64_t ss, double* into) {
-        const double* src = a.in + ss * a.ld_in;
-        const unsigned lb = lds_addr(into);
-        unsigned vo = (unsigned)lane * 16u;
-        if (PERS) asm volatile("" : "+v"(vo));
-#pragma unroll
-        for (int i = 0; i < B / 2; i++) {
-            const int u = 2 * (i * 64 + lane);   // series position of this lane's 16-B piece
-            if (PERS) {
-                // saddr form (piece base in SGPRs); [T, 64 B) of the block stays the wave's
-                if (u < T) glds16_s(src + 128 * i, vo, lb + i * 1024);
-            } else {
-                glds16(src + (u < T ? u : 0), lb + i * 1024);
-            }
-        }
-    };
-    if (PERS && s_first < a.S) issue_block(s_first, buf_mem + wave * BUFD);
-    // one series (a lambda: the one-series-per-wave form runs it once, without a loop around it)
-    auto one = [&](const int64_t s, const int it) {
+    const int64_t s = (int64_t)blockIdx.x * NWV + wave;
+    if (s >= a.S) return;
     double* buf = buf_mem + (DMA ? wave * BUFD : 0);
-    // this lane's block [t0, t0 + B); opaque per series, so the per-lane masks derived from it
-    // are recomputed in the loop instead of being hoisted out of it as ~40 SGPR pairs
-    int t0 = lane * B;
-    if (PERS) asm volatile("" : "+v"(t0));
-    ArWaveLds& w = *reinterpret_cast<ArWaveLds*>(DMA ? buf : buf_mem + wave * WLD);
-    // PERS: the block's unused end [T, 64 B) is the fit's scratch (the next block streams into
-    // [0, T) meanwhile): head | tail | column sums | rows 1..P of L, lower triangle
-    double* const whead = PERS ? buf + T : w.head;
-    double* const wtail = PERS ? buf + T + P : w.tail;
-    double* const wcs = PERS ? buf + T + 2 * P : w.cs;
-    double* const wL = buf + T + 3 * P + 1;
+    ArWaveLds& w = DMA ? *reinterpret_cast<ArWaveLds*>(buf) : lds_mem[wave];
+    const int T = (int)a.T;
+    const int t0 = lane * B;                  // this lane's block [t0, t0 + B)
     const double* xg = a.in + s * a.ld_in;
+    const bool intercept = !a.no_intercept;
 #ifdef STS_STAMPS
     unsigned long long st_acc[8] = {0};
     unsigned long long st_prev = __builtin_amdgcn_s_memtime();
@@ -369,18 +324,15 @@ __global__ __launch_bounds__(64 * NWV, STS_AR_WAVES_PER_EU) void ar_fit_blk_kern
     const bool full = (t0 + B <= T);
     const bool al = ((reinterpret_cast<uintptr_t>(xg) & 15) == 0) && (B % 2 == 0);
     // DMA needs whole 16-B pieces inside the row: T even (and a 16-B aligned row)
-    const bool dma = PERS || (DMA && al && !(T & 1));
+    const bool dma = DMA && al && !(T & 1);
     if (dma) {
-        if (!PERS) {
-            issue_block(s, buf);
-            dma_wait();
-        } else if (it == 0 || !a.out) {
-            dma_wait();
-        } else {
-            // issued since this block: the previous series' c / coef / err stores and then
-            // exactly B / 2 residual stores (see the remove loop) -- wait for all but those
-            dma_wait_n<B / 2>();
+        const unsigned lb = lds_addr(buf);
+#pragma unroll
+        for (int i = 0; i < B / 2; i++) {
+            const int u = 2 * (i * 64 + lane);   // series position of this lane's 16-B piece
+            glds16(xg + (u < T ? u : 0), lb + i * 1024);
         }
+        dma_wait();
         wave_lds_sync();
 #pragma unroll
         for (int j = 0; j < B / 2; j++) {
@@ -389,7 +341,6 @@ __global__ __launch_bounds__(64 * NWV, STS_AR_WAVES_PER_EU) void ar_fit_blk_kern
             x[2 * j + 1] = (t0 + 2 * j + 1 < T) ? v.y : 0.0;
         }
         wave_lds_sync();   // the block is in registers: the LDS block becomes the fit's scratch
-        if (PERS && s + s_step < a.S) issue_block(s + s_step, buf);   // the next block streams in now
     } else if (full && al) {
         const double2* s2 = reinterpret_cast<const double2*>(xg + t0);
 #pragma unroll
@@ -450,9 +401,9 @@ __global__ __launch_bounds__(64 * NWV, STS_AR_WAVES_PER_EU) void ar_fit_blk_kern
 #pragma unroll
             for (int k = P; k >= 2; k--) win[k] = win[k - 1];
             win[1] = yj;
-            if (j < P && lane == 0) whead[j] = yj;
+            if (j < P && lane == 0) w.head[j] = yj;
             const int t = t0 + j;
-            if (t >= T - P && t < T) wtail[t - (T - P)] = yj;
+            if (t >= T - P && t < T) w.tail[t - (T - P)] = yj;
         }
     }
     AR_STAMP(1);
@@ -464,7 +415,7 @@ __global__ __launch_bounds__(64 * NWV, STS_AR_WAVES_PER_EU) void ar_fit_blk_kern
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
     AR_STAMP(2);
     // Y(u) for u in the head [0, P) or the tail [T - P, T) (T >= 2P + 1: disjoint)
-    auto Yh = [&](int u) -> double { return (u < P) ? whead[u] : wtail[u - (T - P)]; };
+    auto Yh = [&](int u) -> double { return (u < P) ? w.head[u] : w.tail[u - (T - P)]; };
 
     // ---- Gram of [Y | X_1..X_p], lane-parallel: lane j < P + 1 holds row j ----
     const int m = T - P;
@@ -508,21 +459,14 @@ __global__ __launch_bounds__(64 * NWV, STS_AR_WAVES_PER_EU) void ar_fit_blk_kern
         }
     }
     if (lane <= P) {
-        if (PERS) {
 #pragma unroll
-            for (int k = 1; k <= P; k++)
-                if (k <= lane) wL[lane * (lane - 1) / 2 + k - 1] = row[k];
-        } else {
-#pragma unroll
-            for (int k = 0; k <= P; k++) w.L[lane * (kRegPB + 1) + k] = row[k];
-        }
-        wcs[lane] = csj;
+        for (int k = 0; k <= P; k++) w.L[lane * (kRegPB + 1) + k] = row[k];
+        w.cs[lane] = csj;
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
-    auto Lu = [&](int i, int k) -> double { return PERS ? wL[i * (i - 1) / 2 + k - 1] : w.L[i * (kRegPB + 1) + k]; };
-    auto Cs = [&](int k) -> double { return wcs[k]; };
+    auto Lu = [&](int i, int k) -> double { return w.L[i * (kRegPB + 1) + k]; };
     auto solve = [&](double (&z)[P + 1]) {
 #pragma unroll
         for (int i = 1; i <= P; i++) {
@@ -547,9 +491,9 @@ __global__ __launch_bounds__(64 * NWV, STS_AR_WAVES_PER_EU) void ar_fit_blk_kern
     double cpr = 0.0;
     if (!bad && ok) {
         solve(phi);
-        double sc = Cs(0);
+        double sc = w.cs[0];
 #pragma unroll
-        for (int k = 1; k <= P; k++) sc -= phi[k] * Cs(k);
+        for (int k = 1; k <= P; k++) sc -= phi[k] * w.cs[k];
         cpr = intercept ? sc / fm : 0.0;
         AR_STAMP(3);
 
@@ -598,12 +542,12 @@ __global__ __launch_bounds__(64 * NWV, STS_AR_WAVES_PER_EU) void ar_fit_blk_kern
         double z[P + 1];
         const double g0 = g[0];
 #pragma unroll
-        for (int i = 1; i <= P; i++) z[i] = g[i] - (intercept ? Cs(i) * g0 / fm : 0.0);
+        for (int i = 1; i <= P; i++) z[i] = g[i] - (intercept ? w.cs[i] * g0 / fm : 0.0);
         z[0] = 0.0;
         solve(z);
         double dc = g0;
 #pragma unroll
-        for (int k = 1; k <= P; k++) dc -= z[k] * Cs(k);
+        for (int k = 1; k <= P; k++) dc -= z[k] * w.cs[k];
         double sphi = 0.0;
 #pragma unroll
         for (int k = 1; k <= P; k++) {
@@ -629,7 +573,7 @@ __global__ __launch_bounds__(64 * NWV, STS_AR_WAVES_PER_EU) void ar_fit_blk_kern
     // ---- fused removeTimeDependentEffects with the fitted model, in the reference's order
     //      (S/models/Autoregression.scala:60-73): d = x_t - c; d -= x_{t-j-1} * coef_j ----
     double* dst = a.out + s * a.ld_out;
-    const bool dma_out = !PERS && dma && ((reinterpret_cast<uintptr_t>(dst) & 15) == 0);
+    const bool dma_out = dma && ((reinterpret_cast<uintptr_t>(dst) & 15) == 0);
     const bool st16 = !dma_out && full && al && ((reinterpret_cast<uintptr_t>(dst) & 15) == 0);
     if (dma_out) wave_lds_sync();   // every read of the fit's scratch (w) is done before the block is rewritten
     double xw[P + 1];                          // xw[k] = x_{t-k}
@@ -646,12 +590,7 @@ __global__ __launch_bounds__(64 * NWV, STS_AR_WAVES_PER_EU) void ar_fit_blk_kern
 #pragma unroll
         for (int k = P; k >= 2; k--) xw[k] = xw[k - 1];
         xw[1] = x[j];
-        if (PERS) {
-            // one 16-B store per odd j in every lane (masked past the row, T even): exactly
-            // B / 2 store instructions per series, which the next iteration's wait counts on
-            if ((j & 1) && t < T) *reinterpret_cast<double2*>(dst + t - 1) = make_double2(rprev, d);
-            rprev = d;
-        } else if (dma_out) {
+        if (dma_out) {
             if (j & 1) *reinterpret_cast<double2*>(buf + t - 1) = make_double2(rprev, d);
             rprev = d;
         } else if (st16) {
@@ -666,9 +605,7 @@ __global__ __launch_bounds__(64 * NWV, STS_AR_WAVES_PER_EU) void ar_fit_blk_kern
 #pragma unroll
         for (int i = 0; i < B / 2; i++) {
             const int u = 2 * (i * 64 + lane);
-            if (u < T) {
-                *reinterpret_cast<double2*>(dst + u) = *reinterpret_cast<const double2*>(buf + u);
-            }
+            if (u < T) *reinterpret_cast<double2*>(dst + u) = *reinterpret_cast<const double2*>(buf + u);
         }
     }
 #ifdef STS_STAMPS
@@ -679,14 +616,6 @@ __global__ __launch_bounds__(64 * NWV, STS_AR_WAVES_PER_EU) void ar_fit_blk_kern
         atomicAdd(&g_ar_stamps[15], 1ull);
     }
 #endif
-    };   // one series
-    if constexpr (PERS) {
-        int it = 0;
-        for (int64_t s = s_first; s < a.S; s += s_step, it++) one(s, it);
-        dma_wait();   // nothing in flight at exit
-    } else {
-        if (s_first < a.S) one(s_first, 0);
-    }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -923,43 +852,9 @@ hipError_t launch_ar_fit(const ArArgs& a, hipStream_t st) {
     // register path: p <= 8, T <= 64 * 40 (lane blocks of B steps, B in {8, 16, 24, 32, 40})
     if (a.p <= kRegPB && a.T <= 64 * 40 && !ab_knob("STS_AR_STAGED")) {
         constexpr int NWV = kRegWaves;
-        // persistent double-buffered form for aligned panels with enough series to fill the
-        // chip (one 4-wave workgroup per CU, each wave walking every (CUs x 4)-th series)
-        const bool aligned = ((reinterpret_cast<uintptr_t>(a.in) & 15) == 0) && !(a.ld_in & 1) && !(a.T & 1) &&
-                             a.T >= 2 && (!a.out || (((reinterpret_cast<uintptr_t>(a.out) & 15) == 0) && !(a.ld_out & 1)));
-        static int cus = 0;
-        if (cus == 0) {
-            int dev = 0, n = 0;
-            if (hipGetDevice(&dev) == hipSuccess &&
-                hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0)
-                cus = n;
-            else
-                cus = 256;
-        }
+        dim3 g((unsigned)((a.S + NWV - 1) / NWV)), b(64 * NWV);
         const int64_t need = (a.T + 63) / 64;
         const int B = need <= 8 ? 8 : need <= 16 ? 16 : need <= 24 ? 24 : need <= 32 ? 32 : 40;
-        // (no scratch: a spilled VGPR would be a vector-memory op the vmcnt wait does not count)
-        if (STS_AR_DMA && aligned && a.p <= 5 && a.T >= 16 && a.T + 3 * a.p + 1 + a.p * (a.p + 1) / 2 <= 64 * B &&
-            a.S >= (int64_t)cus * NWV * 4 && ab_knob("STS_AR_PERS")) {   // A/B only: measured slower
-            dim3 g((unsigned)(2 * cus)), b(64 * NWV);   // 2 workgroups (8 waves) per CU
-#define STS_AR_PERS(PP)                                                                         \
-        case PP:                                                                                \
-            switch (B) {                                                                        \
-            case 8: hipLaunchKernelGGL((ar_fit_blk_kernel<PP, 8, NWV, true, true>), g, b, 0, st, a); break;   \
-            case 16: hipLaunchKernelGGL((ar_fit_blk_kernel<PP, 16, NWV, true, true>), g, b, 0, st, a); break; \
-            case 24: hipLaunchKernelGGL((ar_fit_blk_kernel<PP, 24, NWV, true, true>), g, b, 0, st, a); break; \
-            case 32: hipLaunchKernelGGL((ar_fit_blk_kernel<PP, 32, NWV, true, true>), g, b, 0, st, a); break; \
-            default: hipLaunchKernelGGL((ar_fit_blk_kernel<PP, 40, NWV, true, true>), g, b, 0, st, a); break; \
-            }                                                                                   \
-            break;
-            switch (a.p) {   // p <= 5: the instantiations that fit 256 VGPRs without scratch
-                STS_AR_PERS(1) STS_AR_PERS(2) STS_AR_PERS(3) STS_AR_PERS(4) STS_AR_PERS(5)
-            default: return hipErrorInvalidValue;
-            }
-#undef STS_AR_PERS
-            return hipGetLastError();
-        }
-        dim3 g((unsigned)((a.S + NWV - 1) / NWV)), b(64 * NWV);
 #define STS_AR_BLK(PP)                                                                          \
         case PP:                                                                                \
             switch (B) {                                                                        \

@@ -28,23 +28,6 @@ __device__ __forceinline__ void glds16(const double* gsrc, unsigned lds_byte_add
                  : "memory");
 }
 
-// The saddr form: a wave-uniform 64-bit base in SGPRs + this lane's 32-bit byte offset, so a
-// stream of DMA pieces costs one offset VGPR instead of a 64-bit address pair per piece.
-__device__ __forceinline__ void glds16_s(const double* sbase, unsigned voff_bytes, unsigned lds_byte_addr) {
-    unsigned keep;
-    lds_byte_addr = __builtin_amdgcn_readfirstlane(lds_byte_addr);
-    const unsigned long long b = reinterpret_cast<unsigned long long>(sbase);
-    // (the builtin returns int: widen through unsigned, or a low word >= 2^31 sign-extends
-    // over the high word and the base points nowhere)
-    const unsigned lo = (unsigned)__builtin_amdgcn_readfirstlane((unsigned)b);
-    const unsigned hi = (unsigned)__builtin_amdgcn_readfirstlane((unsigned)(b >> 32));
-    const unsigned long long bu = ((unsigned long long)hi << 32) | (unsigned long long)lo;
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
-                 : "=&s"(keep)
-                 : "v"(voff_bytes), "s"(bu), "s"(lds_byte_addr)
-                 : "memory");
-}
-
 __device__ __forceinline__ void dma_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
 // order this wave's LDS accesses (no workgroup barrier: the buffers are per wave)
