@@ -362,6 +362,11 @@ __global__ __launch_bounds__(64 * NWV, STS_AR_WAVES_PER_EU) void ar_fit_blk_kern
     for (int j = 0; j < B; j++) part += x[j];
     part = wave_sum_dpp(part);
     const double mu = intercept ? part / (double)T : 0.0;
+    // positions past the row take the value mu, so y = x - mu is exactly 0 there and no pass
+    // needs a per-step mask (round 3: 3 VALU per step in two passes); the remove pass never
+    // stores them
+#pragma unroll
+    for (int j = 0; j < B; j++) x[j] = (t0 + j < T) ? x[j] : mu;
     AR_STAMP(0);
     // the previous lane's last P raw values (0 before the series)
     double xp[P + 1];
@@ -371,7 +376,7 @@ __global__ __launch_bounds__(64 * NWV, STS_AR_WAVES_PER_EU) void ar_fit_blk_kern
         xp[k] = (lane > 0) ? v : 0.0;
     }
     // y at block offset j - k (k >= 1 may reach into the previous lane's block)
-    auto Y = [&](int j) -> double { return (t0 + j < T) ? x[j] - mu : 0.0; };
+    auto Y = [&](int j) -> double { return x[j] - mu; };
     auto Yprev = [&](int k) -> double { return (lane > 0) ? xp[k] - mu : 0.0; };
 
     // ---- lag products P_d = sum_t y_t y_{t-d}; head / tail of the series to LDS ----
@@ -420,6 +425,7 @@ __global__ __launch_bounds__(64 * NWV, STS_AR_WAVES_PER_EU) void ar_fit_blk_kern
     // ---- Gram of [Y | X_1..X_p], lane-parallel: lane j < P + 1 holds row j ----
     const int m = T - P;
     const double fm = (double)m;
+    const double ifm = 1.0 / fm;   // the fit is a 1e-10-tolerance path: multiply, no division chains
     const int jr = (lane <= P) ? lane : P;
     double row[P + 1];
 #pragma unroll
@@ -441,7 +447,7 @@ __global__ __launch_bounds__(64 * NWV, STS_AR_WAVES_PER_EU) void ar_fit_blk_kern
     // ---- centred normal equations (intercept eliminated); rhs_j = row[0] ----
     if (intercept) {
 #pragma unroll
-        for (int k = 0; k <= P; k++) row[k] -= csj * lane_bcast(csj, k) / fm;
+        for (int k = 0; k <= P; k++) row[k] -= csj * lane_bcast(csj, k) * ifm;
     }
     // ---- Cholesky of the 1..P block, lane-parallel (lane i owns row i of L) ----
     bool ok = true;
@@ -467,20 +473,26 @@ __global__ __launch_bounds__(64 * NWV, STS_AR_WAVES_PER_EU) void ar_fit_blk_kern
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
     auto Lu = [&](int i, int k) -> double { return w.L[i * (kRegPB + 1) + k]; };
+    // reciprocals of L's diagonal once: the two solves' substitutions are chains of P steps,
+    // and a division per step was ~10 instructions of dependent latency
+    double rdg[P + 1];
+    rdg[0] = 0.0;
+#pragma unroll
+    for (int i = 1; i <= P; i++) rdg[i] = 1.0 / Lu(i, i);
     auto solve = [&](double (&z)[P + 1]) {
 #pragma unroll
         for (int i = 1; i <= P; i++) {
             double v = z[i];
 #pragma unroll
             for (int k = 1; k < i; k++) v -= Lu(i, k) * z[k];
-            z[i] = v / Lu(i, i);
+            z[i] = v * rdg[i];
         }
 #pragma unroll
         for (int i = P; i >= 1; i--) {
             double v = z[i];
 #pragma unroll
             for (int k = i + 1; k <= P; k++) v -= Lu(k, i) * z[k];
-            z[i] = v / Lu(i, i);
+            z[i] = v * rdg[i];
         }
     };
     double phi[P + 1];
@@ -494,7 +506,7 @@ __global__ __launch_bounds__(64 * NWV, STS_AR_WAVES_PER_EU) void ar_fit_blk_kern
         double sc = w.cs[0];
 #pragma unroll
         for (int k = 1; k <= P; k++) sc -= phi[k] * w.cs[k];
-        cpr = intercept ? sc / fm : 0.0;
+        cpr = intercept ? sc * ifm : 0.0;
         AR_STAMP(3);
 
         // ---- refinement: exact residual pass e_t = Y_t - c' - sum_k phi_k Y_{t-k},
@@ -542,7 +554,7 @@ __global__ __launch_bounds__(64 * NWV, STS_AR_WAVES_PER_EU) void ar_fit_blk_kern
         double z[P + 1];
         const double g0 = g[0];
 #pragma unroll
-        for (int i = 1; i <= P; i++) z[i] = g[i] - (intercept ? w.cs[i] * g0 / fm : 0.0);
+        for (int i = 1; i <= P; i++) z[i] = g[i] - (intercept ? w.cs[i] * g0 * ifm : 0.0);
         z[0] = 0.0;
         solve(z);
         double dc = g0;
@@ -555,7 +567,7 @@ __global__ __launch_bounds__(64 * NWV, STS_AR_WAVES_PER_EU) void ar_fit_blk_kern
             sphi += phi[k];
         }
         // un-shift: y = x - mu  =>  c = c' + mu * (1 - sum phi)
-        cpr = intercept ? (cpr + dc / fm) + mu * (1.0 - sphi) : 0.0;
+        cpr = intercept ? (cpr + dc * ifm) + mu * (1.0 - sphi) : 0.0;
         AR_STAMP(5);
     } else {
         cpr = __builtin_nan("");

@@ -867,6 +867,9 @@ __global__ __launch_bounds__(NTH, (DB || DMA) ? 2 : STS_TILE_WGS) void tile_kern
             else STS_CLEAR();
         }
 #endif
+#if STS_PF_POS == 2
+        bool pf_lo = false;   // registers 0-3 of the next tile issued inside the store pass
+#endif
         // ---- 5. filled output + lag matrix (16-B stores), then y = F - F(0) in place
         //      (0 past the series end) for the MFMA phase; start the next tile's loads ----
         {
@@ -892,6 +895,14 @@ __global__ __launch_bounds__(NTH, (DB || DMA) ? 2 : STS_TILE_WGS) void tile_kern
                 asm volatile("" : "+v"(dpo));   // per tile: else LICM keeps dst + dpo as a 64-bit VGPR pair
 #pragma unroll
                 for (int h = 0; h < 2; h++) {
+#if STS_PF_POS == 2
+                    // A/B: the first half of the next tile's loads between the two store halves
+                    if (h == 1 && have_next) {
+                        const double2* s2_ = reinterpret_cast<const double2*>(src + ((k + 1) * TW - kHB));
+                        STS_LD1(0) STS_LD1(1) STS_LD1(2) STS_LD1(3)
+                        pf_lo = true;
+                    }
+#endif
                     double2 fv[FH];
 #pragma unroll
                     for (int j = 0; j < FH; j++) {
@@ -968,6 +979,14 @@ __global__ __launch_bounds__(NTH, (DB || DMA) ? 2 : STS_TILE_WGS) void tile_kern
 #if STS_PF_POS == 0
             else if (have_next) STS_ISSUE(k + 1);   // in flight during the MFMA phase of tile k
             else STS_CLEAR();
+#elif STS_PF_POS == 2
+            else if (have_next) {
+                if (!pf_lo) STS_ISSUE(k + 1);
+                else {
+                    const double2* s2_ = reinterpret_cast<const double2*>(src + ((k + 1) * TW - kHB));
+                    STS_LD1(4) STS_LD1(5) STS_LD1(6) STS_LD1(7) STS_LD1(8)
+                }
+            } else STS_CLEAR();
 #endif
         }
         STAMP(8);
