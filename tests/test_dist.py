@@ -1,4 +1,4 @@
-"""The N > 1 path on CPU: two gloo ranks on 127.0.0.1.
+"""The N > 1 path on CPU: two (and four) gloo ranks on 127.0.0.1.
 
 * shard_range reproduces Spark's ParallelCollectionRDD slicing (contiguous key ranges,
   the partitioning the reference's parallelize-built TimeSeriesRDDs use);
@@ -54,12 +54,13 @@ def _worker(rank, world, port, n, q):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("n", [10, 7])
-def test_all_gather_results_two_ranks(n):
+@pytest.mark.parametrize("n,world", [(10, 2), (7, 2), (9, 4), (3, 4)])
+def test_all_gather_results_ranks(n, world):
+    # world 4 rehearses more ranks than the CPU pair (ragged shards, an empty one at n = 3)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, n, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n, q)) for r in range(world)]
     for p in procs:
         p.start()
     res = dict(q.get(timeout=120) for _ in procs)
@@ -67,7 +68,7 @@ def test_all_gather_results_two_ranks(n):
         p.join(timeout=60)
         assert p.exitcode == 0
     want = [[float(i)] * 3 for i in range(n)]
-    assert res[0] == want and res[1] == want
+    assert all(res[r] == want for r in range(world))
 
 
 def _worker_instants(rank, world, port, S, T, q):
