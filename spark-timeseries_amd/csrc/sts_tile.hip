@@ -69,6 +69,10 @@
 #define STS_PF_POS 0      // A/B: 1 = the next tile's register prefetch is issued before the store pass
 #endif
 
+#ifndef STS_SUMS_Y
+#define STS_SUMS_Y 0      // A/B: fast-path tiles take the middle sums in the y pass, not under the MFMAs
+#endif
+
 #ifndef STS_EARLY
 #define STS_EARLY 0       // A/B: 1 = fill-only tiles issue the next loads at tile start, 2 = all tiles
 #endif
@@ -283,6 +287,7 @@ __global__ __launch_bounds__(NTH, (DB || DMA) ? 2 : STS_TILE_WGS) void tile_kern
         sh_c[2] = -1;
     }
     double acc_s = 0.0, acc_q = 0.0;   // sum y, sum y^2 over this thread's middle positions
+    bool ysums = false;                // STS_SUMS_Y: this tile's middle sums were taken in the y pass
 
     // register prefetch of one INTERIOR extended tile [e0, e0 + EW); the first and last tile
     // of a series (which touch its ends) are loaded synchronously with bounds checks
@@ -516,8 +521,10 @@ __global__ __launch_bounds__(NTH, (DB || DMA) ? 2 : STS_TILE_WGS) void tile_kern
 #else
                             U[t % NA] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[t], bv[t], U[t % NA], 0, 0, 0);
 #endif
-                        acc_s += av[0];   // middle sums: VALU under the MFMA pipe
-                        acc_q = __builtin_fma(av[0], av[0], acc_q);
+                        if (!STS_SUMS_Y || !ysums) {
+                            acc_s += av[0];   // middle sums: VALU under the MFMA pipe
+                            acc_q = __builtin_fma(av[0], av[0], acc_q);
+                        }
                         __builtin_amdgcn_sched_barrier(0);   // one chunk's operands live at a time
 #endif
                     }
@@ -881,7 +888,9 @@ __global__ __launch_bounds__(NTH, (DB || DMA) ? 2 : STS_TILE_WGS) void tile_kern
             // every index and guard below is a compile-time constant
             const bool fast = (dst == nullptr || al) && !a.lagmat && (t1 - t0 == TW) &&
                               (NT == 0 || e0 + qW + REACH <= T);
+            ysums = false;
             if (fast) {
+                if constexpr (STS_SUMS_Y && NT > 0 && !DB) ysums = true;
                 constexpr int FS = TW / 2 / kThreads;                          // stored double2
                 constexpr int FY = NT > 0 ? (NP2 - kHB / 2 + kThreads - 1) / kThreads : FS;
                 constexpr int FH = (FY + 1) / 2;     // two halves: fewer live registers
@@ -930,6 +939,11 @@ __global__ __launch_bounds__(NTH, (DB || DMA) ? 2 : STS_TILE_WGS) void tile_kern
 #if STS_DIAG >= 3   // cost model: the middle sums move from the MFMA loop to this pass
                             acc_s += y.x + y.y;
                             acc_q = __builtin_fma(y.x, y.x, __builtin_fma(y.y, y.y, acc_q));
+#elif STS_SUMS_Y
+                            if (jj < FS) {   // the tile's own positions (a fast tile is a middle tile)
+                                acc_s = (acc_s + y.x) + y.y;
+                                acc_q = __builtin_fma(y.y, y.y, __builtin_fma(y.x, y.x, acc_q));
+                            }
 #endif
 #if STS_DIAG == 4
                             tmax = __builtin_fmax(tmax, __builtin_fmax(__builtin_fabs(y.x), __builtin_fabs(y.y)));
