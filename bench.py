@@ -255,7 +255,7 @@ def main():
               "c5": "sts::tile_kernel<4096,0> (fill nearest + lag-matrix columns)",
               "c2": "sts::recur_kernel<kFillDiffEwma> (fillPrevious -> differencesAtLag(1) -> EWMA add, lane per series)",
               "stage_c2": "sts::recur_kernel<kFillDiffEwma> (fillPrevious -> differencesAtLag(1) -> EWMA add, lane per series)",
-              "c4": "sts::ar_fit_blk_kernel<5,40,4,dma> (AR(5): series in by LDS-DMA, lane-blocked register lag products, lane-parallel Gram / Cholesky + refinement, fused remove out through LDS)",
+              "c4": "sts::ar_fit_blk_kernel<5,40,4,dma> (AR(5): series in by LDS-DMA, lane-blocked register lag products, normal equations / Cholesky uniform in every lane + refinement, fused remove out through LDS)",
               "stats": "sts::stats_fast_kernel<64,16> (StatCounter.merge per lane, LDS-staged series block, division off the step chain)",
               "nan_instants": "sts::nan_instants16_kernel + sts::gather_instants_kernel (wave per row)",
               "to_instants": "sts::transpose16_kernel (64x64 LDS tiles, 16-B accesses)",

@@ -253,7 +253,7 @@ __global__ __launch_bounds__(64) void ar_fit_kernel(ArArgs a, int NT) {
 // The lag products P_0..P_p are lane-local FP64 FMAs: for p <= 8 the 16 x 16 MFMA tile
 // would compute >= 24 lags to use p + 1 of them, and on MI355X the FP64 VALU and FP64
 // MFMA peaks are equal (profiles/r01_ubench_fp64.jsonl).  The (p+1) x (p+1) Gram and the
-// Cholesky are lane-parallel (lane j owns row j).  Same algebra as ar_fit_kernel: centred
+// Cholesky run uniformly in every lane (ar_normal_chol).  Same algebra as ar_fit_kernel: centred
 // data, Gram from lag products minus head/tail terms, Cholesky + one step of refinement
 // against an exact residual pass (corrected semi-normal equations: Householder-QR accuracy).
 constexpr int kRegPB = 8;             // p <= kRegPB
@@ -274,8 +274,6 @@ __device__ unsigned long long g_ar_stamps[16];
 #endif
 
 struct ArWaveLds {
-    double L[(kRegPB + 1) * (kRegPB + 1)];   // Cholesky factor rows (1-based block)
-    double cs[kRegPB + 1];                   // column sums of the design
     double head[kRegPB];                     // Y(0 .. p-1)
     double tail[kRegPB];                     // Y(T-p .. T-1)
 };
@@ -298,6 +296,72 @@ struct ArWaveLds {
 // registers, and the fused residuals go out through it again (16-B LDS writes at the lanes'
 // block offsets, then 1-KB coalesced stores).  Without DMA every load / store instruction
 // touches one 16-B piece per lane at a B * 8-byte stride: 64 cache lines per instruction.
+// The (p+1)^2 normal equations of the register kernels, solved UNIFORMLY: every lane of the
+// wave computes the same Gram, centring and Cholesky in its own registers (round 3).  The
+// round-2 form gave lane j row j and moved every column through v_readlane, LDS and a wave
+// barrier: ~13 k cycles per series of dependent broadcasts and LDS round trips, the largest
+// single phase after the block wait (tools/ar_stamps.py, profiles/r03_v7_ar_stamps.jsonl).
+// Same operations in the same order as the lane-parallel form (identical bits):
+//   A[i][k] (k <= i) = P_{i-k} - sum_{u < P-i} y_u y_{u+i-k} - sum_{v = P-i}^{P-1-(i-k)} t_v t_{v+i-k}
+// with y_u the head y(0..p-1) and t_v the tail y(T-p..T-1) (T >= 2p + 1: disjoint); column 0
+// is Y, rows / columns 1..p the lags; cs = the design's column sums; centring eliminates the
+// intercept; the Cholesky factor of the 1..p block overwrites A's lower triangle; phi = the
+// centred right-hand side A[1..p][0].  Returns false when a pivot is not positive (or NaN).
+template <int P>
+__device__ __forceinline__ bool ar_normal_chol(const double (&Pd)[P + 1], double sy, const double (&hd)[P],
+                                               const double (&tl)[P], bool intercept, double ifm,
+                                               double (&A)[P + 1][P + 1], double (&cs)[P + 1],
+                                               double (&phi)[P + 1]) {
+#pragma unroll
+    for (int i = 1; i <= P; i++) {
+#pragma unroll
+        for (int k = 0; k <= i; k++) {
+            const int d = i - k;
+            double g = Pd[d];
+#pragma unroll
+            for (int u = 0; u < P - i; u++) g -= hd[u] * hd[u + d];
+#pragma unroll
+            for (int v = P - i; v <= P - 1 - d; v++) g -= tl[v] * tl[v + d];
+            A[i][k] = g;
+        }
+    }
+#pragma unroll
+    for (int j = 0; j <= P; j++) {
+        double c = sy;
+#pragma unroll
+        for (int u = 0; u < P - j; u++) c -= hd[u];
+#pragma unroll
+        for (int v = P - j; v < P; v++) c -= tl[v];
+        cs[j] = c;
+    }
+    if (intercept) {
+#pragma unroll
+        for (int i = 1; i <= P; i++)
+#pragma unroll
+            for (int k = 0; k <= i; k++) A[i][k] -= cs[i] * cs[k] * ifm;
+    }
+    bool ok = true;
+#pragma unroll
+    for (int j = 1; j <= P; j++) {
+        const double djj = A[j][j];
+        ok = ok && (djj > 0.0);
+        const double l = __builtin_sqrt(djj);
+        A[j][j] = l;
+#pragma unroll
+        for (int i = j + 1; i <= P; i++) A[i][j] = A[i][j] / l;
+#pragma unroll
+        for (int k = j + 1; k <= P; k++) {
+            const double lkj = A[k][j];
+#pragma unroll
+            for (int i = k; i <= P; i++) A[i][k] -= A[i][j] * lkj;
+        }
+    }
+    phi[0] = 0.0;
+#pragma unroll
+    for (int i = 1; i <= P; i++) phi[i] = A[i][0];
+    return ok;
+}
+
 template <int P, int B, int NWV = kRegWaves, bool DMA = false>
 __global__ __launch_bounds__(64 * NWV, STS_AR_WAVES_PER_EU) void ar_fit_blk_kernel(ArArgs a) {
     constexpr int BUFD = 64 * B;              // doubles per wave block
@@ -419,60 +483,20 @@ __global__ __launch_bounds__(64 * NWV, STS_AR_WAVES_PER_EU) void ar_fit_blk_kern
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
     AR_STAMP(2);
-    // Y(u) for u in the head [0, P) or the tail [T - P, T) (T >= 2P + 1: disjoint)
-    auto Yh = [&](int u) -> double { return (u < P) ? w.head[u] : w.tail[u - (T - P)]; };
-
-    // ---- Gram of [Y | X_1..X_p], lane-parallel: lane j < P + 1 holds row j ----
+    // ---- normal equations, centring, Cholesky: uniform in every lane (ar_normal_chol) ----
+    double hd[P], tl[P];
+#pragma unroll
+    for (int u = 0; u < P; u++) {
+        hd[u] = w.head[u];
+        tl[u] = w.tail[u];
+    }
     const int m = T - P;
     const double fm = (double)m;
     const double ifm = 1.0 / fm;   // the fit is a 1e-10-tolerance path: multiply, no division chains
-    const int jr = (lane <= P) ? lane : P;
-    double row[P + 1];
-#pragma unroll
-    for (int k = 0; k <= P; k++) {
-        const int lo = jr < k ? jr : k, hi = jr < k ? k : jr, d = hi - lo;
-        double g = 0.0;
-#pragma unroll
-        for (int dd = 0; dd <= P; dd++)
-            if (dd == d) g = Pd[dd];
-        for (int u = 0; u < P - hi; u++) g -= Yh(u) * Yh(u + d);           // head rows
-        for (int u = T - hi; u <= T - 1 - d; u++) g -= Yh(u) * Yh(u + d);  // tail rows
-        row[k] = g;
-    }
-    double csj = sy;                                                        // column sums
-    for (int u = 0; u < P - jr; u++) csj -= Yh(u);
-    for (int u = T - jr; u < T; u++) csj -= Yh(u);
     const bool bad = __builtin_isnan(sy) || __builtin_isnan(part);
-
-    // ---- centred normal equations (intercept eliminated); rhs_j = row[0] ----
-    if (intercept) {
-#pragma unroll
-        for (int k = 0; k <= P; k++) row[k] -= csj * lane_bcast(csj, k) * ifm;
-    }
-    // ---- Cholesky of the 1..P block, lane-parallel (lane i owns row i of L) ----
-    bool ok = true;
-#pragma unroll
-    for (int j = 1; j <= P; j++) {
-        const double djj = lane_bcast(row[j], j);
-        ok = ok && (djj > 0.0);
-        const double l = __builtin_sqrt(djj);
-        if (lane == j) row[j] = l;
-        else if (lane > j) row[j] = row[j] / l;
-#pragma unroll
-        for (int k = j + 1; k <= P; k++) {
-            const double lkj = lane_bcast(row[j], k);
-            if (lane >= k) row[k] -= row[j] * lkj;
-        }
-    }
-    if (lane <= P) {
-#pragma unroll
-        for (int k = 0; k <= P; k++) w.L[lane * (kRegPB + 1) + k] = row[k];
-        w.cs[lane] = csj;
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
-    auto Lu = [&](int i, int k) -> double { return w.L[i * (kRegPB + 1) + k]; };
+    double A[P + 1][P + 1], cs[P + 1], phi[P + 1];
+    const bool ok = ar_normal_chol<P>(Pd, sy, hd, tl, intercept, ifm, A, cs, phi);
+    auto Lu = [&](int i, int k) -> double { return A[i][k]; };
     // reciprocals of L's diagonal once: the two solves' substitutions are chains of P steps,
     // and a division per step was ~10 instructions of dependent latency
     double rdg[P + 1];
@@ -495,17 +519,13 @@ __global__ __launch_bounds__(64 * NWV, STS_AR_WAVES_PER_EU) void ar_fit_blk_kern
             z[i] = v * rdg[i];
         }
     };
-    double phi[P + 1];
-    phi[0] = 0.0;
-#pragma unroll
-    for (int i = 1; i <= P; i++) phi[i] = lane_bcast(row[0], i);
     const int status = (!bad && !ok) ? STS_ERR_SINGULAR : STS_OK;
     double cpr = 0.0;
     if (!bad && ok) {
         solve(phi);
-        double sc = w.cs[0];
+        double sc = cs[0];
 #pragma unroll
-        for (int k = 1; k <= P; k++) sc -= phi[k] * w.cs[k];
+        for (int k = 1; k <= P; k++) sc -= phi[k] * cs[k];
         cpr = intercept ? sc * ifm : 0.0;
         AR_STAMP(3);
 
@@ -554,12 +574,12 @@ __global__ __launch_bounds__(64 * NWV, STS_AR_WAVES_PER_EU) void ar_fit_blk_kern
         double z[P + 1];
         const double g0 = g[0];
 #pragma unroll
-        for (int i = 1; i <= P; i++) z[i] = g[i] - (intercept ? w.cs[i] * g0 * ifm : 0.0);
+        for (int i = 1; i <= P; i++) z[i] = g[i] - (intercept ? cs[i] * g0 * ifm : 0.0);
         z[0] = 0.0;
         solve(z);
         double dc = g0;
 #pragma unroll
-        for (int k = 1; k <= P; k++) dc -= z[k] * w.cs[k];
+        for (int k = 1; k <= P; k++) dc -= z[k] * cs[k];
         double sphi = 0.0;
 #pragma unroll
         for (int k = 1; k <= P; k++) {

@@ -659,6 +659,30 @@ def test_ar_fit_register_path_shapes(torch, p):
                     "fused remove T=%d p=%d" % (T, p))
 
 
+@pytest.mark.parametrize("p", [1, 5, 8])
+def test_ar_fit_register_path_edges(torch, p):
+    # the register kernel at lane-block edges (B = 8 .. 40), an odd series count, NaN in
+    # the first and the last lane blocks (NaN model, the others unaffected), the fused remove
+    # bit-exact given the fitted model
+    from sparkts.models import Autoregression
+    S = 7
+    for T in (514, 1024, 1026, 1536, 1538, 2048, 2050, 2520, 2558, 2560):
+        x = oracle.gen_ar_panel(12, S, T, min(p, 5)) + 0.01 * np.sin(np.arange(T))[None, :]
+        x[2, T - 3] = NaN
+        x[4, 5] = NaN
+        m, resid = Autoregression.fitModelAndRemove(dev(torch, x), p)
+        c, coef = host(m.c), host(m.coefficients)
+        ok = [0, 1, 3, 5, 6]
+        rc = np.empty(S); rcoef = np.empty((S, p))
+        for s in ok:
+            rc[s], rcoef[s] = oracle.ar_fit(x[s], p)
+        assert_rel(coef[ok], rcoef[ok], what="coef T=%d p=%d" % (T, p))
+        assert_rel(c[ok], rc[ok], what="c T=%d p=%d" % (T, p))
+        assert np.all(np.isnan(c[[2, 4]])) and np.all(np.isnan(coef[[2, 4]]))
+        assert_bits(host(resid)[ok], np.array([oracle.ar_remove(x[s], c[s], coef[s]) for s in ok]),
+                    "fused remove T=%d p=%d" % (T, p))
+
+
 def test_ar_fit_register_path_matches_staged_on_nan(torch, monkeypatch):
     # NaN anywhere -> NaN model, same as the LDS-staged kernel (forced on the A/B build)
     from sparkts import _native
