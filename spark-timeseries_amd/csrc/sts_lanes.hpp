@@ -30,6 +30,13 @@ __device__ __forceinline__ double wave_sum_dpp(double v) {
     v = v + dpp_d<0x128>(v);
     return (lane_bcast(v, 0) + lane_bcast(v, 16)) + (lane_bcast(v, 32) + lane_bcast(v, 48));
 }
+// sum over the lane's row of 16, the same bits in every lane of the row (wave_sum_dpp's first steps)
+__device__ __forceinline__ double row_sum_dpp(double v) {
+    v = v + dpp_d<0xB1>(v);
+    v = v + dpp_d<0x4E>(v);
+    v = v + dpp_d<0x124>(v);
+    return v + dpp_d<0x128>(v);
+}
 // lane l - 1's value (wave_shr:1; lane 0 gets 0)
 __device__ __forceinline__ double lane_prev(double v) { return dpp_d<0x138>(v); }
 

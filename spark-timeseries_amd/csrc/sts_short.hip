@@ -1,0 +1,272 @@
+// sts_short.hip -- fill('linear') + autocorr(numLags <= 24) for short series held whole in one
+// wave's registers (round 3: C1, the 10-year daily panels, T <= 2 560).
+//
+// Reference path: TimeSeriesRDD.fill("linear") then mapSeries(autocorr(_, K))
+// (S/TimeSeriesRDD.scala:180-182, S/UnivariateTimeSeries.scala:247-266 fillLinear,
+// :68-93 autocorr).  The segment kernel (sts_seg.hip) walks a short series in 512-step tiles
+// with its lag products on FP64 MFMA; at T = 2 520 that is five tiles of ~1 500 instructions
+// per wave, and the SIMDs' issue ports bound it.  Here one wave owns one series
+// the way the AR fit does (§5.6): the series arrives by LDS-DMA into a per-wave LDS block,
+// lane l takes the contiguous steps [l B, l B + B) into registers, and
+//   * the linear fill runs in registers: every lane learns the last valid step before its
+//     block and the first one after it (one ballot and two lane reads), then fills its NaN
+//     runs by the reference's SEQUENTIAL accumulation r[j] = r[j-1] + increment, a run that
+//     enters the block from the left being replayed from its start (bit-exact; a long run
+//     costs its length in adds per lane it crosses).  Filled steps are written back into the
+//     LDS block, which thus holds the filled series (unfillable NaNs keep their raw bits);
+//   * the lag products P_1..P_KM of y = F - c (c: the robust shift, sts_acf.hpp) are
+//     lane-local FP64 FMAs over a rolling window whose first KM values come from the previous
+//     lane (DPP shifts); the middle sums, the wave sums and the per-lag finalize
+//     (acf_combine: the head and tail read from the LDS block) follow sts_acf.hpp exactly;
+//   * the filled series leaves from the LDS block as coalesced 1-KB stores.
+// Tolerance as every ACF path: 1e-10 relative to the oracle; the fill is bit-exact.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "sts.h"
+#include "sts_acf.hpp"
+#include "sts_dma.hpp"
+#include "sts_internal.hpp"
+#include "sts_lanes.hpp"
+
+namespace sts {
+namespace {
+
+constexpr int kShortWaves = 4;
+
+#ifndef STS_SHORT_DIAG
+#define STS_SHORT_DIAG 0   // timing-only cost models (tools/variant.sh): 1 no ACF, 2 no fill,
+                           // 3 no per-lag finalize, 4 no robust shift; wrong results
+#endif
+
+template <int B, int KM>
+__global__ __launch_bounds__(64 * kShortWaves, 2) void short_fill_acf_kernel(TileArgs a) {
+    constexpr int BUFD = 64 * B;   // doubles per wave block: the whole series
+    __shared__ __attribute__((aligned(16))) double buf_mem[kShortWaves * BUFD];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int64_t s = (int64_t)blockIdx.x * kShortWaves + wave;
+    if (s >= a.S) return;
+    double* buf = buf_mem + wave * BUFD;
+    const int T = (int)a.T;
+    const int t0 = lane * B;
+    const double* src = a.in + s * a.ld_in;
+
+    // ---- the series into the LDS block (T even, 16-B aligned rows: whole 16-B pieces) ----
+    {
+        const unsigned lb = lds_addr(buf);
+#pragma unroll
+        for (int i = 0; i < B / 2; i++) {
+            const int u = 2 * (i * 64 + lane);
+            glds16(src + (u < T ? u : 0), lb + i * 1024);
+        }
+        dma_wait();
+        wave_lds_sync();
+    }
+    // the ACF shift from the RAW series, like the tile / segment kernels (sts_acf.hpp: the same
+    // pure function of the values, so the same bits)
+    const double c0 = (a.K > 0 && STS_SHORT_DIAG != 4) ? robust_shift(buf, T, lane) : buf[0];
+    unsigned long long vm = 0ull;   // bit j: step t0 + j is inside the series and valid
+#pragma unroll
+    for (int j = 0; j < B / 2; j++) {
+        const double2 v = *reinterpret_cast<const double2*>(buf + t0 + 2 * j);
+        if (t0 + 2 * j < T && !__builtin_isnan(v.x)) vm |= 1ull << (2 * j);
+        if (t0 + 2 * j + 1 < T && !__builtin_isnan(v.y)) vm |= 1ull << (2 * j + 1);
+    }
+
+    // ---- linear fill (S/UnivariateTimeSeries.scala:247-266): a maximal NaN run with a valid
+    //      step L on its left and R on its right takes r[j] = r[j-1] + (x_R - x_L) / (R - L),
+    //      written into the LDS block run by run (a lane walks only its own runs) ----
+    const int fv = vm ? t0 + __builtin_ctzll(vm) : T;          // first valid step of the block
+    const int lv = vm ? t0 + 63 - __builtin_clzll(vm) : -1;    // last valid step of the block
+    const unsigned long long hv = __ballot(vm != 0ull);
+    const unsigned long long below = hv & ((1ull << lane) - 1ull);
+    const unsigned long long above = hv & ~((2ull << lane) - 1ull);   // lane 63: none
+    const int Lsrc = below ? 63 - __builtin_clzll(below) : lane;
+    const int Rsrc = above ? __builtin_ctzll(above) : lane;
+    const int lvs = __shfl(lv, Lsrc), fvs = __shfl(fv, Rsrc);
+    const int Lc = below ? lvs : -1;   // last valid step before the block (-1: none)
+    const int Rc = above ? fvs : T;    // first valid step after the block (T: none)
+    const int tend = (t0 + B < T) ? t0 + B : T;   // end of this block inside the series
+    if (STS_SHORT_DIAG != 2) {
+        // the block opens inside a run (or at a NaN at t = 0): its left end is Lc, its right
+        // end the block's first valid step or Rc; the run's earlier steps are replayed
+        if (!(vm & 1ull) && t0 < T) {
+            const int R = vm ? fv : Rc;
+            if (Lc >= 0 && R < T) {
+                const double xL = buf[Lc];
+                const double inc = (buf[R] - xL) / (double)(R - Lc);
+                double cur = xL;
+                for (int q = Lc + 1; q < t0; q++) cur = cur + inc;
+                const int e = R < tend ? R : tend;
+                for (int q = t0; q < e; q++) {
+                    cur = cur + inc;
+                    buf[q] = cur;
+                }
+            }
+        }
+        // runs that start inside the block: step t NaN, t - 1 valid
+        const unsigned long long inT = (tend - t0 >= 64) ? ~0ull : ((1ull << (tend > t0 ? tend - t0 : 0)) - 1ull);
+        unsigned long long rs = ~vm & (vm << 1) & inT;
+        while (rs) {
+            const int j = __builtin_ctzll(rs);
+            rs &= rs - 1ull;
+            const int t = t0 + j;
+            const unsigned long long hi = (j + 1 < 64) ? vm >> (j + 1) : 0ull;
+            const int R = hi ? t + 1 + __builtin_ctzll(hi) : Rc;
+            if (R < T) {
+                const double xL = buf[t - 1];
+                const double inc = (buf[R] - xL) / (double)(R - (t - 1));
+                double cur = xL;
+                const int e = R < tend ? R : tend;
+                for (int q = t; q < e; q++) {
+                    cur = cur + inc;
+                    buf[q] = cur;
+                }
+            }
+        }
+    }
+    wave_lds_sync();   // the LDS block now holds the filled series
+
+    // ---- filled series out: coalesced 1-KB stores from the block ----
+    if (a.out) {
+        double* dst = a.out + s * a.ld_out;
+#pragma unroll
+        for (int i = 0; i < B / 2; i++) {
+            const int u = 2 * (i * 64 + lane);
+            if (u < T) *reinterpret_cast<double2*>(dst + u) = *reinterpret_cast<const double2*>(buf + u);
+        }
+    }
+    if (a.err && lane == 0) a.err[s] = STS_OK;   // fillLinear never throws
+    const int K = a.K;
+    if (K <= 0 || a.acf_fused == nullptr || STS_SHORT_DIAG == 1) return;
+
+    // ---- ACF: y = F - c, lag products P_d = sum_t y_t y_{t-d}, middle sums ----
+    double x[B];
+#pragma unroll
+    for (int j = 0; j < B / 2; j++) {
+        const double2 v = *reinterpret_cast<const double2*>(buf + t0 + 2 * j);
+        x[2 * j] = (t0 + 2 * j < T) ? v.x - c0 : 0.0;
+        x[2 * j + 1] = (t0 + 2 * j + 1 < T) ? v.y - c0 : 0.0;
+    }
+    // the head y(0..63) and the tail y(T-1-j), one per lane (T >= 128: disjoint)
+    const double yh = buf[lane] - c0, zt = buf[T - 1 - lane] - c0;
+    static_assert(KM <= B, "the window reaches one lane back only");
+    double win[KM + 1];
+#pragma unroll
+    for (int k = 1; k <= KM; k++) win[k] = lane_prev(x[B - k]);
+    double P[KM + 1];
+#pragma unroll
+    for (int d = 0; d <= KM; d++) P[d] = 0.0;
+    double sm = 0.0, qm = 0.0;
+#pragma unroll
+    for (int j = 0; j < B; j++) {
+        const double yj = x[j];
+        if (acf_mid(t0 + j, T)) {
+            sm += yj;
+            qm = __builtin_fma(yj, yj, qm);
+        }
+#pragma unroll
+        for (int d = 1; d <= KM; d++) P[d] = __builtin_fma(yj, win[d], P[d]);
+#pragma unroll
+        for (int k = KM; k >= 2; k--) win[k] = win[k - 1];
+        win[1] = yj;
+    }
+    // ---- wave sums: rows by DPP, the four row sums of each quantity through the block
+    //      (lane d - 1 collects lag d), added in wave_sum_dpp's order ----
+    wave_lds_sync();   // every read of the filled block is done: it becomes scratch
+    double* scr = buf;
+    const int row = lane >> 4;
+    const bool row_lead = (lane & 15) == 0;
+#pragma unroll
+    for (int d = 1; d <= KM; d++) {
+        const double v = row_sum_dpp(P[d]);
+        if (row_lead) scr[4 * d + row] = v;
+    }
+    {
+        const double v0 = row_sum_dpp(sm), v1 = row_sum_dpp(qm);
+        if (row_lead) {
+            scr[row] = v0;
+            scr[4 * (KM + 1) + row] = v1;
+        }
+    }
+    wave_lds_sync();
+    const int li = (lane < KM) ? lane + 1 : KM;
+    const double4 pr = *reinterpret_cast<const double4*>(scr + 4 * li);
+    const double Pi = (pr.x + pr.y) + (pr.z + pr.w);
+    const double4 sr = *reinterpret_cast<const double4*>(scr);
+    const double4 qr = *reinterpret_cast<const double4*>(scr + 4 * (KM + 1));
+    const double Sm = (sr.x + sr.y) + (sr.z + sr.w), Qm = (qr.x + qr.y) + (qr.z + qr.w);
+    if (STS_SHORT_DIAG == 3) {
+        if (lane < K) a.acf_fused[s * K + lane] = Pi + Sm + Qm;
+        return;
+    }
+    // ---- finalize per lag i = lane + 1 (sts_acf.hpp acf_combine's sums, regrouped): slice 1
+    //      = y[i..64) of the head + the whole tail + the middle, slice 2 = the whole head +
+    //      z[i..64) of the tail + the middle; every partial is a sum of its own terms (suffix
+    //      scans over the lanes, no "total minus head") ----
+    double ys = yh, yq = yh * yh, zs = zt, zq = zt * zt;   // suffix sums from lane .. 63
+#pragma unroll
+    for (int k = 1; k < 64; k <<= 1) {
+        const double a0 = __shfl_down(ys, k), a1 = __shfl_down(yq, k), a2 = __shfl_down(zs, k),
+                     a3 = __shfl_down(zq, k);
+        if (lane + k < 64) {
+            ys += a0;
+            yq += a1;
+            zs += a2;
+            zq += a3;
+        }
+    }
+    const double Yall = lane_bcast(ys, 0), YQall = lane_bcast(yq, 0), Zall = lane_bcast(zs, 0),
+                 ZQall = lane_bcast(zq, 0);
+    // lag i = lane + 1 wants the suffixes from position i: lane i's (none for i = 64)
+    double ysi = __shfl_down(ys, 1), yqi = __shfl_down(yq, 1), zsi = __shfl_down(zs, 1), zqi = __shfl_down(zq, 1);
+    if (lane == 63) ysi = yqi = zsi = zqi = 0.0;
+    const double sum1 = (Sm + Zall) + ysi, sq1 = (Qm + ZQall) + yqi;
+    const double sum2 = (Sm + Yall) + zsi, sq2 = (Qm + YQall) + zqi;
+    const double N = (double)(T - (lane + 1));
+    const double v1 = sq1 - sum1 * sum1 / N;
+    const double v2 = sq2 - sum2 * sum2 / N;
+    const double cv = Pi - sum1 * sum2 / N;
+    if (lane < K) a.acf_fused[s * K + lane] = cv / (__builtin_sqrt(v1) * __builtin_sqrt(v2));   // :89
+}
+
+}  // namespace
+
+// fill('linear') + fused ACF for 128 <= T <= 2 560, T even, K <= 24, 16-B aligned rows
+bool short_ok(int method, int64_t T, int K) {
+    return method == STS_FILL_LINEAR && T >= 2 * kAcfEdge && T <= 64 * 40 && !(T & 1) && K > 0 && K <= 24 &&
+           T > 2 * (int64_t)K;
+}
+
+hipError_t launch_short(const TileArgs& a, hipStream_t st) {
+    if (a.S <= 0) return hipSuccess;
+    const int64_t nblk = (a.S + kShortWaves - 1) / kShortWaves;
+    if (nblk > 0x7fffffffLL) return hipErrorInvalidValue;
+    dim3 g((unsigned)nblk), b(64 * kShortWaves);
+    const int64_t need = (a.T + 63) / 64;
+    // the lag window (KM >= K, a multiple of 4) reaches back KM steps: blocks of >= KM steps
+    const int KM = (a.K + 3) / 4 * 4 < 8 ? 8 : (a.K + 3) / 4 * 4;
+    const int64_t nb = need < KM ? KM : need;
+    const int B = nb <= 8 ? 8 : nb <= 16 ? 16 : nb <= 24 ? 24 : nb <= 32 ? 32 : 40;
+#define STS_SHORT_K(BB, KK) \
+    case KK: hipLaunchKernelGGL((short_fill_acf_kernel<BB, (KK <= BB ? KK : BB)>), g, b, 0, st, a); break;
+#define STS_SHORT(BB)                                                                              \
+    case BB:                                                                                       \
+        switch (KM) {                                                                              \
+            STS_SHORT_K(BB, 8) STS_SHORT_K(BB, 12) STS_SHORT_K(BB, 16) STS_SHORT_K(BB, 20)         \
+            STS_SHORT_K(BB, 24)                                                                    \
+        default: return hipErrorInvalidValue;                                                      \
+        }                                                                                          \
+        break;
+    switch (B) {
+        STS_SHORT(8) STS_SHORT(16) STS_SHORT(24) STS_SHORT(32) STS_SHORT(40)
+    default: return hipErrorInvalidValue;
+    }
+#undef STS_SHORT
+#undef STS_SHORT_K
+    return hipGetLastError();
+}
+
+}  // namespace sts

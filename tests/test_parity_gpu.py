@@ -318,7 +318,8 @@ def test_fill_autocorr_fused(torch, method):
 # (libsts_hip_ab.so); each must stay parity-green.
 KNOB_VARIANTS = {
     "tile": {"STS_TILE_KERNEL": "tile"},
-    "seg": {"STS_TILE_KERNEL": "seg"},
+    "seg": {"STS_TILE_KERNEL": "seg", "STS_NO_SHORT": "1"},
+    "short": {"STS_TILE_KERNEL": "seg"},                              # linear, K <= 24, T <= 2560: sts_short.hip
     "tile2048": {"STS_TILE_KERNEL": "tile", "STS_TILE_W": "2048"},    # 2-wave workgroups, 2048-step tiles
     "tilec4": {"STS_TILE_KERNEL": "tile", "STS_TILES_PER_CHUNK": "4"},  # 4 tiles per workgroup
     "seg3": {"STS_TILE_KERNEL": "seg", "STS_SEG_TILES": "3"},          # multi-segment partials + finalize
@@ -353,15 +354,19 @@ def test_fused_acf_finalize_matches_two_kernel_path(torch, monkeypatch, T):
     # one segment per series: the segment kernel finalizes the ACF itself (no partials, no
     # second launch) when T > 2K, T >= 128 and its last tile holds >= 64 steps; bit-identical
     # to the separate acf_finalize_kernel (forced with STS_NO_FUSED_ACF on the A/B build), and
-    # err is written for every series without a memset
+    # err is written for every series without a memset.  Both sides on the A/B build with the
+    # short-series kernel off (STS_NO_SHORT), which the product takes for linear fills with
+    # K <= 24 and even T <= 2560 (test_short_fill_acf covers it)
     from sparkts import TimeSeriesRDD
     from sparkts import _native
     rng = np.random.default_rng(T)
+    monkeypatch.setenv("STS_NO_SHORT", "1")
     x = random_panel(rng, 9, T, 0.05, runs=True)
     x[4] = 7.0                                            # constant: 0/0 = NaN
     x[5, 0] = NaN                                         # head NaN -> all-NaN ACF
-    prod = _native.lib()
-    ab = _native.load_variant(_native.AB_LIB_PATH)
+    prod = _native.load_variant(_native.AB_LIB_PATH)
+    ab = prod
+    monkeypatch.setattr(_native, "_lib", prod)
     for K in (1, 20, 60):
         if T <= 2 * K:
             continue
@@ -388,6 +393,53 @@ def test_fused_acf_finalize_matches_two_kernel_path(torch, monkeypatch, T):
     want = np.zeros(9, np.int32)
     want[2] = 2                                            # nearest on [x0, NaN, ...]: "Input is all NaNs!"
     assert np.array_equal(host(err), want)
+
+
+@pytest.mark.parametrize("K", [1, 8, 9, 20, 24])
+def test_short_fill_acf(torch, monkeypatch, K):
+    # sts_short.hip: fill('linear') + ACF with the whole series in one wave (K <= 24, even
+    # T in [128, 2560], aligned rows).  Fill bit-exact and ACF 1e-10 against the oracle, on NaN
+    # patterns that cross lane blocks (B = 8..40 steps): runs entering a block from the left,
+    # runs spanning many blocks, leading / trailing / t = 0 / t = T-1 NaNs, all-NaN, constant,
+    # one valid step, alternating; err written for every series; the segment kernel
+    # (STS_NO_SHORT on the A/B build) agrees to 1e-10
+    from sparkts import TimeSeriesRDD
+    from sparkts import _native
+    rng = np.random.default_rng(1000 + K)
+    for T in (128, 130, 512, 514, 1000, 1024, 1536, 2048, 2520, 2560):
+        if T <= 2 * K:
+            continue
+        x = random_panel(rng, 16, T, 0.05, runs=True)
+        x[1, : T // 3] = NaN                                  # leading run over many blocks
+        x[2, T // 4: 3 * T // 4] = NaN                        # interior run over many blocks
+        x[3, -(T // 5):] = NaN                                # trailing run
+        x[4, 0] = NaN; x[4, T - 1] = NaN                      # the ends
+        x[5] = NaN                                            # all NaN
+        x[6] = 3.25                                           # constant: 0/0
+        x[7] = NaN; x[7, T // 2] = 1.0                        # one valid step
+        x[8, 1::2] = NaN                                      # alternating
+        x[9, 7:9] = NaN; x[9, 39:41] = NaN; x[9, 79:81] = NaN  # runs across 8 / 40-step block edges
+        x[10, 1:T - 1] = NaN                                  # one run from 1 to T-2
+        x[11] = 1e6 + rng.standard_normal(T)                  # high level, no NaN
+        x[12, 22:200] = NaN                                   # run across several small blocks
+        rf, racf, err = oracle.panel_fill_autocorr(x, "linear", K)
+        xd = dev(torch, x)
+        out = torch.empty_like(xd)
+        acf = torch.empty((16, K), dtype=torch.float64, device="cuda:0")
+        e = torch.full((16,), 99, dtype=torch.int32, device="cuda:0")
+        lib = _native.lib()
+        assert lib.sts_fill_autocorr(xd.data_ptr(), out.data_ptr(), 16, T, T, T, 0, K, acf.data_ptr(),
+                                     e.data_ptr(), torch.cuda.current_stream().cuda_stream) == 0
+        torch.cuda.synchronize()
+        assert np.array_equal(host(e), np.zeros(16, np.int32))
+        assert_bits(host(out), rf, "fill T=%d K=%d" % (T, K))
+        assert_rel(host(acf), racf, what="acf T=%d K=%d" % (T, K))
+        with monkeypatch.context() as mp:
+            mp.setattr(_native, "_lib", _native.load_variant(_native.AB_LIB_PATH))
+            mp.setenv("STS_NO_SHORT", "1")
+            f2, a2 = TimeSeriesRDD(None, None, dev(torch, x)).fillAndAutocorr("linear", K)
+        assert_bits(host(f2.data), rf, "seg fill T=%d" % T)
+        assert_rel(host(acf), host(a2), what="short vs seg T=%d K=%d" % (T, K))
 
 
 def test_fill_autocorr_c3_length(torch):
