@@ -37,8 +37,35 @@ constexpr int kShortWaves = 4;
 
 #ifndef STS_SHORT_DIAG
 #define STS_SHORT_DIAG 0   // timing-only cost models (tools/variant.sh): 1 no ACF, 2 no fill,
-                           // 3 no per-lag finalize, 4 no robust shift; wrong results
+                           // 3 no per-lag finalize, 4 no robust shift, 5 no lag products;
+                           // wrong results
 #endif
+
+// robust_shift (sts_acf.hpp) from the lanes' validity masks: lane l's sample is the first
+// valid RAW step of [l T / 64, (l + 1) T / 64) -- a range of < B steps, so inside the blocks
+// of at most two lanes -- read from the LDS block (the fill never rewrites a valid step).
+// The same samples, fallbacks and median as robust_shift: the same bits.
+template <int B>
+__device__ __forceinline__ double shift_from_masks(const double* buf, unsigned long long vm, int T, int lane) {
+    const int a = (int)((int64_t)lane * T / 64), b = (int)((int64_t)(lane + 1) * T / 64);
+    const int ba = a / B;
+    const unsigned long long m0 = __shfl(vm, ba), m1 = __shfl(vm, ba + 1 < 64 ? ba + 1 : 63);
+    const int o = a - ba * B;                                  // offset of a in block ba
+    const int e0 = (b - ba * B < B) ? b - ba * B : B;          // end of the range in block ba
+    const unsigned long long w0 = (m0 >> o) & ((e0 - o >= 64) ? ~0ull : ((1ull << (e0 - o)) - 1ull));
+    const int e1 = b - (ba + 1) * B;                           // range steps in block ba + 1
+    const unsigned long long w1 = (e1 > 0) ? (m1 & ((1ull << e1) - 1ull)) : 0ull;
+    const bool found = a < b && (w0 || w1);
+    const int idx = w0 ? a + __builtin_ctzll(w0) : (ba + 1) * B + (w1 ? __builtin_ctzll(w1) : 0);
+    double v = found ? buf[idx] : 0.0;
+    const unsigned long long vmk = __ballot(found);
+    if (vmk == 0ull) return 0.0;
+    const unsigned long long above = vmk & ~((2ull << lane) - 1ull);
+    const unsigned long long below = vmk & ((1ull << lane) - 1ull);
+    const int from = found ? lane : (above ? __ffsll((long long)above) - 1 : 63 - __clzll(below));
+    v = __shfl(v, from);
+    return median_of_lanes(v, true, lane);
+}
 
 template <int B, int KM>
 __global__ __launch_bounds__(64 * kShortWaves, 2) void short_fill_acf_kernel(TileArgs a) {
@@ -64,9 +91,6 @@ __global__ __launch_bounds__(64 * kShortWaves, 2) void short_fill_acf_kernel(Til
         dma_wait();
         wave_lds_sync();
     }
-    // the ACF shift from the RAW series, like the tile / segment kernels (sts_acf.hpp: the same
-    // pure function of the values, so the same bits)
-    const double c0 = (a.K > 0 && STS_SHORT_DIAG != 4) ? robust_shift(buf, T, lane) : buf[0];
     unsigned long long vm = 0ull;   // bit j: step t0 + j is inside the series and valid
 #pragma unroll
     for (int j = 0; j < B / 2; j++) {
@@ -141,6 +165,8 @@ __global__ __launch_bounds__(64 * kShortWaves, 2) void short_fill_acf_kernel(Til
     if (a.err && lane == 0) a.err[s] = STS_OK;   // fillLinear never throws
     const int K = a.K;
     if (K <= 0 || a.acf_fused == nullptr || STS_SHORT_DIAG == 1) return;
+    // the ACF shift of the RAW series (sts_acf.hpp robust_shift) while the stores drain
+    const double c0 = (STS_SHORT_DIAG != 4) ? shift_from_masks<B>(buf, vm, T, lane) : buf[0];
 
     // ---- ACF: y = F - c, lag products P_d = sum_t y_t y_{t-d}, middle sums ----
     double x[B];
@@ -168,7 +194,8 @@ __global__ __launch_bounds__(64 * kShortWaves, 2) void short_fill_acf_kernel(Til
             qm = __builtin_fma(yj, yj, qm);
         }
 #pragma unroll
-        for (int d = 1; d <= KM; d++) P[d] = __builtin_fma(yj, win[d], P[d]);
+        for (int d = 1; d <= KM; d++)
+            if (STS_SHORT_DIAG != 5) P[d] = __builtin_fma(yj, win[d], P[d]);
 #pragma unroll
         for (int k = KM; k >= 2; k--) win[k] = win[k - 1];
         win[1] = yj;
