@@ -257,7 +257,10 @@ __global__ __launch_bounds__(64) void ar_fit_kernel(ArArgs a, int NT) {
 // data, Gram from lag products minus head/tail terms, Cholesky + one step of refinement
 // against an exact residual pass (corrected semi-normal equations: Householder-QR accuracy).
 constexpr int kRegPB = 8;             // p <= kRegPB
-constexpr int kRegWaves = 4;
+#ifndef STS_AR_NWV
+#define STS_AR_NWV 4   // waves (= series) per workgroup of the register kernel
+#endif
+constexpr int kRegWaves = STS_AR_NWV;
 
 #ifdef STS_STAMPS
 __device__ unsigned long long g_ar_stamps[16];

@@ -33,7 +33,12 @@
 namespace sts {
 namespace {
 
-constexpr int kShortWaves = 4;
+#ifndef STS_SHORT_WAVES
+#define STS_SHORT_WAVES 1   // waves (= series) per workgroup: the waves never synchronise, and
+                            // one-wave workgroups free each 20-KB block as soon as its wave
+                            // ends (C1: 0.1003-0.1012 ms vs 0.1036-0.1051 for 2, 0.108 for 4)
+#endif
+constexpr int kShortWaves = STS_SHORT_WAVES;
 
 #ifndef STS_SHORT_DIAG
 #define STS_SHORT_DIAG 0   // timing-only cost models (tools/variant.sh): 1 no ACF, 2 no fill,
