@@ -251,7 +251,7 @@ def main():
     if args.workload == "nan_instants":  # flag pass reads everything; the gather reads + writes kept values
         bytes_per_step = 8.0 * S * T + 16.0 * S * n_keep
     kernel = {"c3": "sts::tile_kernel<4096,4,shifted> (fill linear + ACF partials, FP64 MFMA)",
-              "c1": "sts::seg_kernel<2> (wave-private series segments: fill linear + ACF partials, FP64 MFMA)",
+              "c1": "sts::short_fill_acf_kernel<40,20> (one wave per series in one-wave workgroups: series in by LDS-DMA, linear fill run by run in LDS, lag products as register FMAs, fused ACF finalize)",
               "c5": "sts::tile_kernel<4096,0> (fill nearest + lag-matrix columns)",
               "c2": "sts::recur_kernel<kFillDiffEwma> (fillPrevious -> differencesAtLag(1) -> EWMA add, lane per series)",
               "stage_c2": "sts::recur_kernel<kFillDiffEwma> (fillPrevious -> differencesAtLag(1) -> EWMA add, lane per series)",
