@@ -223,7 +223,7 @@ int run_tile(const double* in, double* out, double* lagmat, int64_t S, int64_t T
                       !sts::ab_knob("STS_NO_FUSED_ACF");
     a.err_all = one_seg ? 1 : 0;
     a.acf_fused = fuse ? acf : nullptr;
-    // fill('linear') + ACF with K <= 24 on T <= 2560 (C1): one wave holds the whole series
+    // fill('linear' / 'previous' / 'next') + ACF with K <= 24 on T <= 2560 (C1): one wave holds the whole series
     // (sts_short.hip); STS_NO_SHORT keeps the segment kernel (A/B build)
     const bool short_k = fuse && sts::short_ok(method, T, K) && !sts::ab_knob("STS_NO_SHORT");
     if (err && !one_seg) HIP_TRY(hipMemsetAsync(err, 0, (size_t)S * sizeof(int32_t), st), "hipMemsetAsync(err)");
@@ -242,7 +242,7 @@ int run_tile(const double* in, double* out, double* lagmat, int64_t S, int64_t T
         }
     }
     prof_mark(st);
-    hipError_t e = short_k ? sts::launch_short(a, st)
+    hipError_t e = short_k ? sts::launch_short(method, a, st)
                    : seg   ? sts::launch_segment(method, a, st)
                            : sts::launch_tile(method, tw, a, st);
     prof_mark(st);

@@ -93,7 +93,7 @@ hipError_t launch_segment(int method, const TileArgs& a, hipStream_t st);
 // fill('linear') + fused ACF with the whole series in one wave's registers (sts_short.hip):
 // short_ok() says whether a one-segment, fused-ACF seg call may take it instead
 bool short_ok(int method, int64_t T, int K);
-hipError_t launch_short(const TileArgs& a, hipStream_t st);
+hipError_t launch_short(int method, const TileArgs& a, hipStream_t st);
 
 hipError_t launch_diff(const double* in, double* out, int64_t S, int64_t T, int64_t ld_in,
                        int64_t ld_out, int lag, int start, hipStream_t st);

@@ -1,5 +1,5 @@
-// sts_short.hip -- fill('linear') + autocorr(numLags <= 24) for short series held whole in one
-// wave's registers (round 3: C1, the 10-year daily panels, T <= 2 560).
+// sts_short.hip -- fill('linear' / 'previous' / 'next') + autocorr(numLags <= 24) for short
+// series held whole in one wave's registers (round 3: C1, the 10-year daily panels, T <= 2 560).
 //
 // Reference path: TimeSeriesRDD.fill("linear") then mapSeries(autocorr(_, K))
 // (S/TimeSeriesRDD.scala:180-182, S/UnivariateTimeSeries.scala:247-266 fillLinear,
@@ -72,8 +72,9 @@ __device__ __forceinline__ double shift_from_masks(const double* buf, unsigned l
     return median_of_lanes(v, true, lane);
 }
 
-template <int B, int KM>
+template <int B, int KM, int M>
 __global__ __launch_bounds__(64 * kShortWaves, 2) void short_fill_acf_kernel(TileArgs a) {
+    static_assert(M == STS_FILL_LINEAR || M == STS_FILL_PREVIOUS || M == STS_FILL_NEXT, "fill method");
     constexpr int BUFD = 64 * B;   // doubles per wave block: the whole series
     __shared__ __attribute__((aligned(16))) double buf_mem[kShortWaves * BUFD];
     const int lane = threadIdx.x & 63;
@@ -121,7 +122,15 @@ __global__ __launch_bounds__(64 * kShortWaves, 2) void short_fill_acf_kernel(Til
     if (STS_SHORT_DIAG != 2) {
         // the block opens inside a run (or at a NaN at t = 0): its left end is Lc, its right
         // end the block's first valid step or Rc; the run's earlier steps are replayed
-        if (!(vm & 1ull) && t0 < T) {
+        if (!(vm & 1ull) && t0 < T && M != STS_FILL_LINEAR) {
+            // fillPrevious / fillNext (:194-204, :214-224): the run's steps take x_L / x_R
+            const int R = vm ? fv : Rc;
+            if (M == STS_FILL_PREVIOUS ? Lc >= 0 : R < T) {
+                const double v = buf[M == STS_FILL_PREVIOUS ? Lc : R];
+                const int e = R < tend ? R : tend;
+                for (int q = t0; q < e; q++) buf[q] = v;
+            }
+        } else if (!(vm & 1ull) && t0 < T) {
             const int R = vm ? fv : Rc;
             if (Lc >= 0 && R < T) {
                 const double xL = buf[Lc];
@@ -144,7 +153,13 @@ __global__ __launch_bounds__(64 * kShortWaves, 2) void short_fill_acf_kernel(Til
             const int t = t0 + j;
             const unsigned long long hi = (j + 1 < 64) ? vm >> (j + 1) : 0ull;
             const int R = hi ? t + 1 + __builtin_ctzll(hi) : Rc;
-            if (R < T) {
+            if (M != STS_FILL_LINEAR) {
+                if (M == STS_FILL_PREVIOUS || R < T) {
+                    const double v = buf[M == STS_FILL_PREVIOUS ? t - 1 : R];
+                    const int e = R < tend ? R : tend;
+                    for (int q = t; q < e; q++) buf[q] = v;
+                }
+            } else if (R < T) {
                 const double xL = buf[t - 1];
                 const double inc = (buf[R] - xL) / (double)(R - (t - 1));
                 double cur = xL;
@@ -167,7 +182,7 @@ __global__ __launch_bounds__(64 * kShortWaves, 2) void short_fill_acf_kernel(Til
             if (u < T) *reinterpret_cast<double2*>(dst + u) = *reinterpret_cast<const double2*>(buf + u);
         }
     }
-    if (a.err && lane == 0) a.err[s] = STS_OK;   // fillLinear never throws
+    if (a.err && lane == 0) a.err[s] = STS_OK;   // fillLinear / Previous / Next never throw
     const int K = a.K;
     if (K <= 0 || a.acf_fused == nullptr || STS_SHORT_DIAG == 1) return;
     // the ACF shift of the RAW series (sts_acf.hpp robust_shift) while the stores drain
@@ -268,11 +283,13 @@ __global__ __launch_bounds__(64 * kShortWaves, 2) void short_fill_acf_kernel(Til
 
 // fill('linear') + fused ACF for 128 <= T <= 2 560, T even, K <= 24, 16-B aligned rows
 bool short_ok(int method, int64_t T, int K) {
-    return method == STS_FILL_LINEAR && T >= 2 * kAcfEdge && T <= 64 * 40 && !(T & 1) && K > 0 && K <= 24 &&
+    return (method == STS_FILL_LINEAR || method == STS_FILL_PREVIOUS || method == STS_FILL_NEXT) &&
+           T >= 2 * kAcfEdge && T <= 64 * 40 && !(T & 1) && K > 0 && K <= 24 &&
            T > 2 * (int64_t)K;
 }
 
-hipError_t launch_short(const TileArgs& a, hipStream_t st) {
+template <int M>
+hipError_t launch_short_m(const TileArgs& a, hipStream_t st) {
     if (a.S <= 0) return hipSuccess;
     const int64_t nblk = (a.S + kShortWaves - 1) / kShortWaves;
     if (nblk > 0x7fffffffLL) return hipErrorInvalidValue;
@@ -283,7 +300,7 @@ hipError_t launch_short(const TileArgs& a, hipStream_t st) {
     const int64_t nb = need < KM ? KM : need;
     const int B = nb <= 8 ? 8 : nb <= 16 ? 16 : nb <= 24 ? 24 : nb <= 32 ? 32 : 40;
 #define STS_SHORT_K(BB, KK) \
-    case KK: hipLaunchKernelGGL((short_fill_acf_kernel<BB, (KK <= BB ? KK : BB)>), g, b, 0, st, a); break;
+    case KK: hipLaunchKernelGGL((short_fill_acf_kernel<BB, (KK <= BB ? KK : BB), M>), g, b, 0, st, a); break;
 #define STS_SHORT(BB)                                                                              \
     case BB:                                                                                       \
         switch (KM) {                                                                              \
@@ -299,6 +316,15 @@ hipError_t launch_short(const TileArgs& a, hipStream_t st) {
 #undef STS_SHORT
 #undef STS_SHORT_K
     return hipGetLastError();
+}
+
+hipError_t launch_short(int method, const TileArgs& a, hipStream_t st) {
+    switch (method) {
+    case STS_FILL_LINEAR: return launch_short_m<STS_FILL_LINEAR>(a, st);
+    case STS_FILL_PREVIOUS: return launch_short_m<STS_FILL_PREVIOUS>(a, st);
+    case STS_FILL_NEXT: return launch_short_m<STS_FILL_NEXT>(a, st);
+    default: return hipErrorInvalidValue;
+    }
 }
 
 }  // namespace sts

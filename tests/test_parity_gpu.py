@@ -395,9 +395,10 @@ def test_fused_acf_finalize_matches_two_kernel_path(torch, monkeypatch, T):
     assert np.array_equal(host(err), want)
 
 
-@pytest.mark.parametrize("K", [1, 8, 9, 20, 24])
-def test_short_fill_acf(torch, monkeypatch, K):
-    # sts_short.hip: fill('linear') + ACF with the whole series in one wave (K <= 24, even
+@pytest.mark.parametrize("method,K", [("linear", 1), ("linear", 8), ("linear", 9), ("linear", 20), ("linear", 24),
+                                      ("previous", 20), ("previous", 5), ("next", 20), ("next", 13)])
+def test_short_fill_acf(torch, monkeypatch, method, K):
+    # sts_short.hip: fill('linear' / 'previous' / 'next') + ACF with the whole series in one wave (K <= 24, even
     # T in [128, 2560], aligned rows).  Fill bit-exact and ACF 1e-10 against the oracle, on NaN
     # patterns that cross lane blocks (B = 8..40 steps): runs entering a block from the left,
     # runs spanning many blocks, leading / trailing / t = 0 / t = T-1 NaNs, all-NaN, constant,
@@ -405,7 +406,9 @@ def test_short_fill_acf(torch, monkeypatch, K):
     # (STS_NO_SHORT on the A/B build) agrees to 1e-10
     from sparkts import TimeSeriesRDD
     from sparkts import _native
-    rng = np.random.default_rng(1000 + K)
+    from sparkts import UnivariateTimeSeries as uts
+    code = uts.fill_method_code(method)
+    rng = np.random.default_rng(1000 + K + 100 * code)
     for T in (128, 130, 512, 514, 1000, 1024, 1536, 2048, 2520, 2560):
         if T <= 2 * K:
             continue
@@ -422,13 +425,13 @@ def test_short_fill_acf(torch, monkeypatch, K):
         x[10, 1:T - 1] = NaN                                  # one run from 1 to T-2
         x[11] = 1e6 + rng.standard_normal(T)                  # high level, no NaN
         x[12, 22:200] = NaN                                   # run across several small blocks
-        rf, racf, err = oracle.panel_fill_autocorr(x, "linear", K)
+        rf, racf, err = oracle.panel_fill_autocorr(x, method, K)
         xd = dev(torch, x)
         out = torch.empty_like(xd)
         acf = torch.empty((16, K), dtype=torch.float64, device="cuda:0")
         e = torch.full((16,), 99, dtype=torch.int32, device="cuda:0")
         lib = _native.lib()
-        assert lib.sts_fill_autocorr(xd.data_ptr(), out.data_ptr(), 16, T, T, T, 0, K, acf.data_ptr(),
+        assert lib.sts_fill_autocorr(xd.data_ptr(), out.data_ptr(), 16, T, T, T, code, K, acf.data_ptr(),
                                      e.data_ptr(), torch.cuda.current_stream().cuda_stream) == 0
         torch.cuda.synchronize()
         assert np.array_equal(host(e), np.zeros(16, np.int32))
@@ -437,7 +440,7 @@ def test_short_fill_acf(torch, monkeypatch, K):
         with monkeypatch.context() as mp:
             mp.setattr(_native, "_lib", _native.load_variant(_native.AB_LIB_PATH))
             mp.setenv("STS_NO_SHORT", "1")
-            f2, a2 = TimeSeriesRDD(None, None, dev(torch, x)).fillAndAutocorr("linear", K)
+            f2, a2 = TimeSeriesRDD(None, None, dev(torch, x)).fillAndAutocorr(method, K)
         assert_bits(host(f2.data), rf, "seg fill T=%d" % T)
         assert_rel(host(acf), host(a2), what="short vs seg T=%d K=%d" % (T, K))
 
