@@ -91,14 +91,23 @@ __device__ __forceinline__ int64_t acf_readlane64(int64_t v, int l) {
 //   * A lane whose range holds no valid step takes the sample of the next lane that has one
 //     -- the first valid step after t0, i.e. exactly F(t0) of fillNext, and the right end of
 //     a linear / nearest gap -- else that of the last lane before it with one (a trailing
-//     run).  So every lane stands for its 1/64 of the filled series, and a long run filled
+//     run).  Under fillPrevious (prev_fill) the order is reversed: a run is filled with the
+//     value before it, so the lane takes the last sampled lane before it, else the next one
+//     (round 3: with the fillNext order, a long interior run under fillPrevious followed by a
+//     level change put the shift on the far side of the change).  So every lane stands for its 1/64 of the filled series, and a long run filled
 //     by copies of one value weighs in the sample as it weighs in the series.
 //   * c = the lower median of the 64 samples.  0.0 only when the series has no valid step at
 //     all (its ACF is NaN for every fill then).
 // A pure function of the series' values: every workgroup / segment that computes it gets the
 // same bits.
 constexpr int kProbeRounds = 4;
-__device__ __forceinline__ double robust_shift(const double* src, int64_t T, int lane) {
+// the lane whose sample a lane without a valid step takes (see robust_shift)
+__device__ __forceinline__ int shift_fallback_lane(unsigned long long above, unsigned long long below, bool prev_fill) {
+    const int next = above ? __ffsll((long long)above) - 1 : -1;
+    const int prev = below ? 63 - __clzll(below) : -1;
+    return prev_fill ? (prev >= 0 ? prev : next) : (next >= 0 ? next : prev);
+}
+__device__ __forceinline__ double robust_shift(const double* src, int64_t T, int lane, bool prev_fill = false) {
     const int64_t t0 = (int64_t)lane * T / 64, t1 = (int64_t)(lane + 1) * T / 64;
     int64_t cur = t0;
     double v = 0.0;
@@ -154,7 +163,7 @@ __device__ __forceinline__ double robust_shift(const double* src, int64_t T, int
     if (vm == 0ull) return 0.0;
     const unsigned long long above = vm & ~((2ull << lane) - 1ull);   // lanes > lane (lane 63: none)
     const unsigned long long below = vm & ((1ull << lane) - 1ull);
-    const int from = found ? lane : (above ? __ffsll((long long)above) - 1 : 63 - __clzll(below));
+    const int from = found ? lane : shift_fallback_lane(above, below, prev_fill);
     v = __shfl(v, from);
     return median_of_lanes(v, true, lane);
 }

@@ -236,7 +236,7 @@ int run_tile(const double* in, double* out, double* lagmat, int64_t S, int64_t T
         a.partials = static_cast<double*>(part.p);
         if (!seg) {
             double* sh = a.partials + np;
-            e = sts::launch_acf_shift(in, S, T, ld_in, sh, st);
+            e = sts::launch_acf_shift(in, S, T, ld_in, method, sh, st);
             if (e != hipSuccess) return hip_fail(e, "acf shift");
             a.shift = sh;
         }
@@ -422,7 +422,7 @@ int sts_fill_autocorr(const double* in, double* filled, int64_t S, int64_t T, in
         hipError_t e = sc.alloc(((size_t)S + np) * sizeof(double));
         if (e != hipSuccess) return hip_fail(e, "hipMallocAsync(acf partials)");
         double* shift = static_cast<double*>(sc.p);
-        HIP_TRY(sts::launch_acf_shift(F, S, T, ldF, shift, st), "acf shift");
+        HIP_TRY(sts::launch_acf_shift(F, S, T, ldF, STS_FILL_NONE, shift, st), "acf shift");
         HIP_TRY(timed(st, [&] { return sts::launch_acf_wide(F, S, T, ldF, shift, K, shift + S, acf, st); }),
                 "autocorr (wide)");
         return es.finish("fill_autocorr");

@@ -392,6 +392,9 @@ __global__ __launch_bounds__(64 * NWV, STS_AR_WAVES_PER_EU) void ar_fit_blk_kern
     const bool al = ((reinterpret_cast<uintptr_t>(xg) & 15) == 0) && (B % 2 == 0);
     // DMA needs whole 16-B pieces inside the row: T even (and a 16-B aligned row)
     const bool dma = DMA && al && !(T & 1);
+    // head / tail of y straight from the DMA block instead of per-step LDS writes in the lag
+    // pass (p <= 6: at p = 7, 8 the changed schedule spills)
+    constexpr bool hd_blk = P <= 6;
     if (dma) {
         const unsigned lb = lds_addr(buf);
 #pragma unroll
@@ -473,9 +476,11 @@ __global__ __launch_bounds__(64 * NWV, STS_AR_WAVES_PER_EU) void ar_fit_blk_kern
 #pragma unroll
             for (int k = P; k >= 2; k--) win[k] = win[k - 1];
             win[1] = yj;
-            if (j < P && lane == 0) w.head[j] = yj;
-            const int t = t0 + j;
-            if (t >= T - P && t < T) w.tail[t - (T - P)] = yj;
+            if (!(hd_blk && dma)) {   // with DMA the raw series is still in the LDS block
+                if (j < P && lane == 0) w.head[j] = yj;
+                const int t = t0 + j;
+                if (t >= T - P && t < T) w.tail[t - (T - P)] = yj;
+            }
         }
     }
     AR_STAMP(1);
@@ -489,9 +494,9 @@ __global__ __launch_bounds__(64 * NWV, STS_AR_WAVES_PER_EU) void ar_fit_blk_kern
     // ---- normal equations, centring, Cholesky: uniform in every lane (ar_normal_chol) ----
     double hd[P], tl[P];
 #pragma unroll
-    for (int u = 0; u < P; u++) {
-        hd[u] = w.head[u];
-        tl[u] = w.tail[u];
+    for (int u = 0; u < P; u++) {   // y = x - mu of the head / tail steps (T >= 2P + 1: raw values)
+        hd[u] = (hd_blk && dma) ? buf[u] - mu : w.head[u];
+        tl[u] = (hd_blk && dma) ? buf[T - P + u] - mu : w.tail[u];
     }
     const int m = T - P;
     const double fm = (double)m;
@@ -610,29 +615,40 @@ __global__ __launch_bounds__(64 * NWV, STS_AR_WAVES_PER_EU) void ar_fit_blk_kern
     double* dst = a.out + s * a.ld_out;
     const bool dma_out = dma && ((reinterpret_cast<uintptr_t>(dst) & 15) == 0);
     const bool st16 = !dma_out && full && al && ((reinterpret_cast<uintptr_t>(dst) & 15) == 0);
-    if (dma_out) wave_lds_sync();   // every read of the fit's scratch (w) is done before the block is rewritten
+    if (dma_out) wave_lds_sync();   // every read of the block (head / tail) is done before it is rewritten
     double xw[P + 1];                          // xw[k] = x_{t-k}
 #pragma unroll
     for (int k = 1; k <= P; k++) xw[k] = xp[k];
     double rprev = 0.0;
-#pragma unroll
-    for (int j = 0; j < B; j++) {
-        const int t = t0 + j;
+    // one step of the remove; j is a constant after unrolling, so only a block's first P steps
+    // carry the "t - k >= 0" test (lane 0's look-back before the series)
+    auto step = [&](int j) -> double {
         double d = x[j] - cpr;
 #pragma unroll
         for (int k = 1; k <= P; k++)
-            if (t - k >= 0) d -= xw[k] * phi[k];
+            if (j >= k || t0 + j - k >= 0) d -= xw[k] * phi[k];
 #pragma unroll
         for (int k = P; k >= 2; k--) xw[k] = xw[k - 1];
         xw[1] = x[j];
-        if (dma_out) {
-            if (j & 1) *reinterpret_cast<double2*>(buf + t - 1) = make_double2(rprev, d);
+        return d;
+    };
+    if (dma_out) {   // the LDS-staged form as its own loop: no per-step branch on the form
+#pragma unroll
+        for (int j = 0; j < B; j++) {
+            const double d = step(j);
+            if (j & 1) *reinterpret_cast<double2*>(buf + t0 + j - 1) = make_double2(rprev, d);
             rprev = d;
-        } else if (st16) {
-            if (j & 1) *reinterpret_cast<double2*>(dst + t - 1) = make_double2(rprev, d);
-            rprev = d;
-        } else if (t < T) {
-            dst[t] = d;
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < B; j++) {
+            const double d = step(j);
+            if (st16) {
+                if (j & 1) *reinterpret_cast<double2*>(dst + t0 + j - 1) = make_double2(rprev, d);
+                rprev = d;
+            } else if (t0 + j < T) {
+                dst[t0 + j] = d;
+            }
         }
     }
     if (dma_out) {   // coalesced 1-KB stores of the staged residuals (T even)

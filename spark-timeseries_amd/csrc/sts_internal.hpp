@@ -75,7 +75,9 @@ int validate(F&& f) {
 hipError_t launch_tile(int method, int tw, const TileArgs& a, hipStream_t st);
 hipError_t launch_acf_finalize(const FinalizeArgs& a, hipStream_t st);
 // per-series robust ACF shift (sts_acf.hpp) for the tile kernel
-hipError_t launch_acf_shift(const double* in, int64_t S, int64_t T, int64_t ld, double* shift, hipStream_t st);
+// method: the fill the series will take (STS_FILL_PREVIOUS reverses the shift's fallback)
+hipError_t launch_acf_shift(const double* in, int64_t S, int64_t T, int64_t ld, int method, double* shift,
+                            hipStream_t st);
 // numLags above the fused kernels' 63 (sts_acf_wide.hip): partial count for S x T x K, and the
 // lag-block MFMA pass + finalize on a filled panel F (shift: launch_acf_shift of F)
 constexpr int kFusedMaxLags = 63;

@@ -599,7 +599,7 @@ __global__ __launch_bounds__(256, 4) void seg_kernel(TileArgs a, int method) {
     if (cx.k0 + 1 <= cx.kLast) load_tile(RB, cx.src, (cx.k0 + 1) * kW, cx.T, lane);
     // ACF shift (sts_acf.hpp robust_shift): 64 samples spread over the whole series that
     // stand for the filled values; its probe loads are in flight with the first two tiles'
-    if (NT > 0) st.c0 = robust_shift(cx.src, cx.T, lane);
+    if (NT > 0) st.c0 = robust_shift(cx.src, cx.T, lane, method == STS_FILL_PREVIOUS);
     masks_to_lds(RA, w.m2[0], lane);
     raw_to_slot(w.ring, RA, lane);
     if (NT > 0 && g == 0) zero_slot<1>(w, lane);     // "tile -1": y = 0 before the series

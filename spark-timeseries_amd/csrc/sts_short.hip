@@ -1,4 +1,4 @@
-// sts_short.hip -- fill('linear' / 'previous' / 'next') + autocorr(numLags <= 24) for short
+// sts_short.hip -- fillts (linear / previous / next / nearest) + autocorr(numLags <= 24) for short
 // series held whole in one wave's registers (round 3: C1, the 10-year daily panels, T <= 2 560).
 //
 // Reference path: TimeSeriesRDD.fill("linear") then mapSeries(autocorr(_, K))
@@ -51,7 +51,8 @@ constexpr int kShortWaves = STS_SHORT_WAVES;
 // of at most two lanes -- read from the LDS block (the fill never rewrites a valid step).
 // The same samples, fallbacks and median as robust_shift: the same bits.
 template <int B>
-__device__ __forceinline__ double shift_from_masks(const double* buf, unsigned long long vm, int T, int lane) {
+__device__ __forceinline__ double shift_from_masks(const double* buf, unsigned long long vm, int T, int lane,
+                                                   bool prev_fill) {
     const int a = (int)((int64_t)lane * T / 64), b = (int)((int64_t)(lane + 1) * T / 64);
     const int ba = a / B;
     const unsigned long long m0 = __shfl(vm, ba), m1 = __shfl(vm, ba + 1 < 64 ? ba + 1 : 63);
@@ -67,14 +68,15 @@ __device__ __forceinline__ double shift_from_masks(const double* buf, unsigned l
     if (vmk == 0ull) return 0.0;
     const unsigned long long above = vmk & ~((2ull << lane) - 1ull);
     const unsigned long long below = vmk & ((1ull << lane) - 1ull);
-    const int from = found ? lane : (above ? __ffsll((long long)above) - 1 : 63 - __clzll(below));
+    const int from = found ? lane : shift_fallback_lane(above, below, prev_fill);
     v = __shfl(v, from);
     return median_of_lanes(v, true, lane);
 }
 
 template <int B, int KM, int M>
 __global__ __launch_bounds__(64 * kShortWaves, 2) void short_fill_acf_kernel(TileArgs a) {
-    static_assert(M == STS_FILL_LINEAR || M == STS_FILL_PREVIOUS || M == STS_FILL_NEXT, "fill method");
+    static_assert(M == STS_FILL_LINEAR || M == STS_FILL_PREVIOUS || M == STS_FILL_NEXT || M == STS_FILL_NEAREST,
+                  "fill method");
     constexpr int BUFD = 64 * B;   // doubles per wave block: the whole series
     __shared__ __attribute__((aligned(16))) double buf_mem[kShortWaves * BUFD];
     const int lane = threadIdx.x & 63;
@@ -105,12 +107,18 @@ __global__ __launch_bounds__(64 * kShortWaves, 2) void short_fill_acf_kernel(Til
         if (t0 + 2 * j + 1 < T && !__builtin_isnan(v.y)) vm |= 1ull << (2 * j + 1);
     }
 
-    // ---- linear fill (S/UnivariateTimeSeries.scala:247-266): a maximal NaN run with a valid
-    //      step L on its left and R on its right takes r[j] = r[j-1] + (x_R - x_L) / (R - L),
-    //      written into the LDS block run by run (a lane walks only its own runs) ----
-    const int fv = vm ? t0 + __builtin_ctzll(vm) : T;          // first valid step of the block
-    const int lv = vm ? t0 + 63 - __builtin_clzll(vm) : -1;    // last valid step of the block
-    const unsigned long long hv = __ballot(vm != 0ull);
+    // ---- the fill, run by run into the LDS block (a lane walks only its own runs).  A run is a
+    //      maximal NaN stretch with valid ends L (or none, -1) and R (or none, T):
+    //      linear   (S/UnivariateTimeSeries.scala:247-266): both ends needed, r[t] = r[t-1] +
+    //               (x_R - x_L) / (R - L), sequentially from L;
+    //      previous (:194-204) x_L;  next (:214-224) x_R;
+    //      nearest  (:156-184) x_L while t - L < R - t, else x_R (ties to R), one end enough;
+    //               index 0 is never rewritten and never an end; no end at all throws. ----
+    // fillNearest's index 0 is not a valid end: out of its mask (the shift keeps using vm)
+    const unsigned long long vf = (M == STS_FILL_NEAREST && lane == 0) ? vm & ~1ull : vm;
+    const int fv = vf ? t0 + __builtin_ctzll(vf) : T;          // first valid step of the block
+    const int lv = vf ? t0 + 63 - __builtin_clzll(vf) : -1;    // last valid step of the block
+    const unsigned long long hv = __ballot(vf != 0ull);
     const unsigned long long below = hv & ((1ull << lane) - 1ull);
     const unsigned long long above = hv & ~((2ull << lane) - 1ull);   // lane 63: none
     const int Lsrc = below ? 63 - __builtin_clzll(below) : lane;
@@ -119,56 +127,49 @@ __global__ __launch_bounds__(64 * kShortWaves, 2) void short_fill_acf_kernel(Til
     const int Lc = below ? lvs : -1;   // last valid step before the block (-1: none)
     const int Rc = above ? fvs : T;    // first valid step after the block (T: none)
     const int tend = (t0 + B < T) ? t0 + B : T;   // end of this block inside the series
-    if (STS_SHORT_DIAG != 2) {
+    // fillNearest over a series with no valid step after index 0: "Input is all NaNs!"
+    const bool all_nan = (M == STS_FILL_NEAREST) && hv == 0ull && T >= 2;
+    // steps [q0, q1) of a run with ends L, R
+    auto fill_run = [&](int q0, int q1, int L, int R) {
+        if (M == STS_FILL_PREVIOUS || M == STS_FILL_NEXT) {
+            if (M == STS_FILL_PREVIOUS ? L >= 0 : R < T) {
+                const double v = buf[M == STS_FILL_PREVIOUS ? L : R];
+                for (int q = q0; q < q1; q++) buf[q] = v;
+            }
+        } else if (M == STS_FILL_NEAREST) {
+            if (L >= 0 || R < T) {
+                const double xL = (L >= 0) ? buf[L] : 0.0, xR = (R < T) ? buf[R] : 0.0;
+                for (int q = q0; q < q1; q++) buf[q] = (R >= T || (L >= 0 && q - L < R - q)) ? xL : xR;
+            }
+        } else if (L >= 0 && R < T) {   // linear
+            const double xL = buf[L];
+            const double inc = (buf[R] - xL) / (double)(R - L);
+            double cur = xL;
+            for (int q = L + 1; q < q0; q++) cur = cur + inc;   // the run's steps in earlier blocks
+            for (int q = q0; q < q1; q++) {
+                cur = cur + inc;
+                buf[q] = cur;
+            }
+        }
+    };
+    if (STS_SHORT_DIAG != 2 && !all_nan) {
         // the block opens inside a run (or at a NaN at t = 0): its left end is Lc, its right
-        // end the block's first valid step or Rc; the run's earlier steps are replayed
-        if (!(vm & 1ull) && t0 < T && M != STS_FILL_LINEAR) {
-            // fillPrevious / fillNext (:194-204, :214-224): the run's steps take x_L / x_R
-            const int R = vm ? fv : Rc;
-            if (M == STS_FILL_PREVIOUS ? Lc >= 0 : R < T) {
-                const double v = buf[M == STS_FILL_PREVIOUS ? Lc : R];
-                const int e = R < tend ? R : tend;
-                for (int q = t0; q < e; q++) buf[q] = v;
-            }
-        } else if (!(vm & 1ull) && t0 < T) {
-            const int R = vm ? fv : Rc;
-            if (Lc >= 0 && R < T) {
-                const double xL = buf[Lc];
-                const double inc = (buf[R] - xL) / (double)(R - Lc);
-                double cur = xL;
-                for (int q = Lc + 1; q < t0; q++) cur = cur + inc;
-                const int e = R < tend ? R : tend;
-                for (int q = t0; q < e; q++) {
-                    cur = cur + inc;
-                    buf[q] = cur;
-                }
-            }
+        // end the block's first valid step or Rc
+        if (!(vf & 1ull) && t0 < T) {
+            const int R = vf ? fv : Rc;
+            const int q0 = (M == STS_FILL_NEAREST && t0 == 0) ? 1 : t0;
+            fill_run(q0, R < tend ? R : tend, Lc, R);
         }
         // runs that start inside the block: step t NaN, t - 1 valid
         const unsigned long long inT = (tend - t0 >= 64) ? ~0ull : ((1ull << (tend > t0 ? tend - t0 : 0)) - 1ull);
-        unsigned long long rs = ~vm & (vm << 1) & inT;
+        unsigned long long rs = ~vf & (vf << 1) & inT;
         while (rs) {
             const int j = __builtin_ctzll(rs);
             rs &= rs - 1ull;
             const int t = t0 + j;
-            const unsigned long long hi = (j + 1 < 64) ? vm >> (j + 1) : 0ull;
+            const unsigned long long hi = (j + 1 < 64) ? vf >> (j + 1) : 0ull;
             const int R = hi ? t + 1 + __builtin_ctzll(hi) : Rc;
-            if (M != STS_FILL_LINEAR) {
-                if (M == STS_FILL_PREVIOUS || R < T) {
-                    const double v = buf[M == STS_FILL_PREVIOUS ? t - 1 : R];
-                    const int e = R < tend ? R : tend;
-                    for (int q = t; q < e; q++) buf[q] = v;
-                }
-            } else if (R < T) {
-                const double xL = buf[t - 1];
-                const double inc = (buf[R] - xL) / (double)(R - (t - 1));
-                double cur = xL;
-                const int e = R < tend ? R : tend;
-                for (int q = t; q < e; q++) {
-                    cur = cur + inc;
-                    buf[q] = cur;
-                }
-            }
+            fill_run(t, R < tend ? R : tend, t - 1, R);
         }
     }
     wave_lds_sync();   // the LDS block now holds the filled series
@@ -182,11 +183,11 @@ __global__ __launch_bounds__(64 * kShortWaves, 2) void short_fill_acf_kernel(Til
             if (u < T) *reinterpret_cast<double2*>(dst + u) = *reinterpret_cast<const double2*>(buf + u);
         }
     }
-    if (a.err && lane == 0) a.err[s] = STS_OK;   // fillLinear / Previous / Next never throw
+    if (a.err && lane == 0) a.err[s] = all_nan ? STS_ERR_ALL_NAN : STS_OK;
     const int K = a.K;
     if (K <= 0 || a.acf_fused == nullptr || STS_SHORT_DIAG == 1) return;
     // the ACF shift of the RAW series (sts_acf.hpp robust_shift) while the stores drain
-    const double c0 = (STS_SHORT_DIAG != 4) ? shift_from_masks<B>(buf, vm, T, lane) : buf[0];
+    const double c0 = (STS_SHORT_DIAG != 4) ? shift_from_masks<B>(buf, vm, T, lane, M == STS_FILL_PREVIOUS) : buf[0];
 
     // ---- ACF: y = F - c, lag products P_d = sum_t y_t y_{t-d}, middle sums ----
     double x[B];
@@ -283,7 +284,8 @@ __global__ __launch_bounds__(64 * kShortWaves, 2) void short_fill_acf_kernel(Til
 
 // fill('linear') + fused ACF for 128 <= T <= 2 560, T even, K <= 24, 16-B aligned rows
 bool short_ok(int method, int64_t T, int K) {
-    return (method == STS_FILL_LINEAR || method == STS_FILL_PREVIOUS || method == STS_FILL_NEXT) &&
+    return (method == STS_FILL_LINEAR || method == STS_FILL_PREVIOUS || method == STS_FILL_NEXT ||
+            method == STS_FILL_NEAREST) &&
            T >= 2 * kAcfEdge && T <= 64 * 40 && !(T & 1) && K > 0 && K <= 24 &&
            T > 2 * (int64_t)K;
 }
@@ -323,6 +325,7 @@ hipError_t launch_short(int method, const TileArgs& a, hipStream_t st) {
     case STS_FILL_LINEAR: return launch_short_m<STS_FILL_LINEAR>(a, st);
     case STS_FILL_PREVIOUS: return launch_short_m<STS_FILL_PREVIOUS>(a, st);
     case STS_FILL_NEXT: return launch_short_m<STS_FILL_NEXT>(a, st);
+    case STS_FILL_NEAREST: return launch_short_m<STS_FILL_NEAREST>(a, st);
     default: return hipErrorInvalidValue;
     }
 }

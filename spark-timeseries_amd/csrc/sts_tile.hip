@@ -1219,21 +1219,23 @@ __global__ __launch_bounds__(256) void acf_finalize_kernel(FinalizeArgs a) {
 // One wave per series: the robust ACF shift (sts_acf.hpp) of every series, once per call,
 // for the tile kernel's workgroups to load (instead of each of a series' ~15 workgroups
 // sampling and ranking it again).
-__global__ __launch_bounds__(256) void acf_shift_kernel(const double* in, int64_t S, int64_t T, int64_t ld,
+__global__ __launch_bounds__(256) void acf_shift_kernel(const double* in, int64_t S, int64_t T, int64_t ld, int prev,
                                                         double* shift) {
     const int lane = threadIdx.x & 63;
     const int64_t s = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (s >= S) return;
-    const double c = robust_shift(in + s * ld, T, lane);
+    const double c = robust_shift(in + s * ld, T, lane, prev != 0);
     if (lane == 0) shift[s] = c;
 }
 
 }  // namespace
 
-hipError_t launch_acf_shift(const double* in, int64_t S, int64_t T, int64_t ld, double* shift, hipStream_t st) {
+hipError_t launch_acf_shift(const double* in, int64_t S, int64_t T, int64_t ld, int method, double* shift,
+                            hipStream_t st) {
     if (S <= 0 || T <= 0) return hipSuccess;
     dim3 grid((unsigned)((S + 3) / 4)), block(256);
-    hipLaunchKernelGGL(acf_shift_kernel, grid, block, 0, st, in, S, T, ld, shift);
+    hipLaunchKernelGGL(acf_shift_kernel, grid, block, 0, st, in, S, T, ld, method == STS_FILL_PREVIOUS ? 1 : 0,
+                       shift);
     return hipGetLastError();
 }
 
