@@ -78,9 +78,7 @@ def main():
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    world, rank, local = dist_env()
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
@@ -157,12 +155,15 @@ def main():
     elif world > 1 and args.workload == "c4":
         gather = ResultGather(S, (1 + p_ar,), torch.float64, dev)
 
+    # the headline step: one fused fill + ACF launch over the rank's shard, then the all-gather
+    # of the ACF block (fill_acf_step, the same code the gloo test drives with a CPU stand-in)
+    fill_acf = fill_acf_step(lambda: raise_for_status(
+        lib.sts_fill_autocorr(x.data_ptr(), out.data_ptr(), S, T, T, T, 0, K, acf.data_ptr(), err.data_ptr(), sp),
+        "fill_autocorr"), acf, gather)
+
     def step():
         if args.workload in ("c3", "c1"):
-            raise_for_status(lib.sts_fill_autocorr(x.data_ptr(), out.data_ptr(), S, T, T, T, 0, K, acf.data_ptr(),
-                                                   err.data_ptr(), sp), "fill_autocorr")
-            if world > 1:
-                gather(acf)
+            fill_acf()
         elif args.workload in ("c2", "stage_c2"):
             raise_for_status(lib.sts_fill_diff_ewma(x.data_ptr(), out.data_ptr(), S, T, T, T, 3, 1, smooth.data_ptr(),
                                                     err.data_ptr(), sp), "fill_diff_ewma")
@@ -206,34 +207,11 @@ def main():
             if world > 1:
                 gather(torch.cat([c_fit[:, None], coef_fit], 1))
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    lib.sts_profile_begin()
-    t0 = time.perf_counter()
-    ev0 = torch.cuda.Event(enable_timing=True)
-    ev1 = torch.cuda.Event(enable_timing=True)
-    ev0.record(stream)
-    for _ in range(args.steps):
-        step()
-    ev1.record(stream)
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    wall = time.perf_counter() - t0
     kern_ms = np.zeros(1, dtype=np.float64)
     launches = np.zeros(1, dtype=np.int64)
-    lib.sts_profile_end(kern_ms.ctypes.data, launches.ctypes.data)
-    elapsed = wall
-    if world > 1:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
-
+    _, elapsed = timed_region(step, args.steps, args.warmup, world, lambda: torch.cuda.synchronize(dev), dev,
+                              on_start=lib.sts_profile_begin,
+                              on_stop=lambda: lib.sts_profile_end(kern_ms.ctypes.data, launches.ctypes.data))
     elems = float(S) * T * world * args.steps
     value = elems / elapsed
     ms_per_step = elapsed / args.steps * 1e3
@@ -285,28 +263,93 @@ def main():
         cpu = cpu_baseline(args, S, T, K, seed, nan_p, out, acf, p_ar, smooth,
                            gpar if args.workload == "garch_fit" else None)
 
-    if rank == 0:
-        line = {
-            "metric": "series-elements/sec + % HBM roofline (fill+lag+ACF) at 1/2/4/8 MI355X",
-            "value": value, "unit": "series-elements/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": None, "dtype": "f64",
-            "data": "synthetic: Philox4x32-10 counter-based panel generated in HBM (SURVEY.md 8(d)), %g NaN" % nan_p,
-            "config": {"workload": desc, "series_per_gpu": S, "steps_per_series": T,
-                       "numLags": K if args.workload in ("c3", "c1") else None,
-                       "fill": {"c3": "linear", "c1": "linear", "c2": "previous", "stage_c2": "previous", "c4": None,
-                                "c5": "nearest",
-                                "ewma_fit": None, "garch_fit": None, "stats": None, "nan_instants": None,
-                                "to_instants": None, "wire_decode": None}[args.workload],
-                       "parallelism": "dp%d (series sharded by key, one process per GPU)" % world},
-            "roofline": roofline,
-            "cpu_baseline": cpu,
-        }
-        if staging is not None:
-            line["staging"] = staging
-        print(json.dumps(line), flush=True)
+    line = result_line(args.workload, value, world, args.steps, args.warmup, ms_per_step, desc, S, T, K, nan_p,
+                       roofline, cpu)
+    if staging is not None:
+        line["staging"] = staging
+    emit(line, rank)
     if world > 1:
         dist.destroy_process_group()
+
+
+# ---- the harness pieces every workload and the N > 1 gloo test (tests/test_bench_dist.py) share ----
+
+def dist_env():
+    """(world, rank, local rank) from torch.distributed.run's environment (1, 0, 0 without it)."""
+    return (int(os.environ.get("WORLD_SIZE", "1")), int(os.environ.get("RANK", "0")),
+            int(os.environ.get("LOCAL_RANK", "0")))
+
+
+def fill_acf_step(kernel_call, acf, gather=None):
+    """One C1 / C3 step: the fused fill + ACF call over the rank's shard, then (N > 1) the
+    all-gather of its ACF block into every rank's (S_total, K) result -- the reference's
+    rdd.mapSeries(...).collect of per-series results (S/TimeSeriesRDD.scala:188-199),
+    partitions in key order."""
+    def step():
+        kernel_call()
+        if gather is not None:
+            step.gathered = gather(acf)
+    step.gathered = None
+    return step
+
+
+def timed_region(step, steps, warmup, world, sync, reduce_device, on_start=None, on_stop=None):
+    """W untimed warmup steps, then exactly K timed steps bracketed by a barrier and a device
+    synchronize on both sides; returns (this rank's wall seconds, the MAX over ranks)."""
+    import torch
+    import torch.distributed as dist
+    for _ in range(warmup):
+        step()
+    sync()
+    if world > 1:
+        dist.barrier()
+    sync()
+    if on_start is not None:
+        on_start()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    sync()
+    if world > 1:
+        dist.barrier()
+    sync()
+    wall = time.perf_counter() - t0
+    if on_stop is not None:
+        on_stop()
+    elapsed = wall
+    if world > 1:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=reduce_device)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    return wall, elapsed
+
+
+FILL_OF = {"c3": "linear", "c1": "linear", "c2": "previous", "stage_c2": "previous", "c4": None, "c5": "nearest",
+           "ewma_fit": None, "garch_fit": None, "stats": None, "nan_instants": None, "to_instants": None,
+           "wire_decode": None}
+
+
+def result_line(workload, value, world, steps, warmup, ms_per_step, desc, S, T, K, nan_p, roofline, cpu):
+    """The ONE JSON line of the driver contract (value = whole-job series-elements/s)."""
+    return {
+        "metric": "series-elements/sec + % HBM roofline (fill+lag+ACF) at 1/2/4/8 MI355X",
+        "value": value, "unit": "series-elements/s", "n_gpus": world, "steps": steps,
+        "warmup": warmup, "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic: Philox4x32-10 counter-based panel generated in HBM (SURVEY.md 8(d)), %g NaN" % nan_p,
+        "config": {"workload": desc, "series_per_gpu": S, "steps_per_series": T,
+                   "numLags": K if workload in ("c3", "c1") else None,
+                   "fill": FILL_OF[workload],
+                   "parallelism": "dp%d (series sharded by key, one process per GPU)" % world},
+        "roofline": roofline,
+        "cpu_baseline": cpu,
+    }
+
+
+def emit(line, rank):
+    """Rank 0 prints the line; every other rank prints nothing."""
+    if rank == 0:
+        print(json.dumps(line), flush=True)
 
 
 def staging_leg(args, lib, x, out, smooth, S, T):
