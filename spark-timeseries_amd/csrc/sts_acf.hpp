@@ -25,6 +25,15 @@
 //     the first or last kAcfEdge steps cannot cancel digits out of them.
 //
 // The lag products P_i = sum_j y_j y_{j+i} (j + i < T) need no correction at all.
+//
+//  3. (round 4) Where the one-pass value can still differ from the reference's, the
+//     reference's own loop runs instead.  acf_suspect bounds, per lag, the one-pass rounding
+//     error (cancellation R = sum y^2 / variance) and the deviation the reference's rounded
+//     means put into ITS result (a constant 100.1 series: the mean rounds to 100.1 - d, every
+//     diff is d, and the reference returns 1.0 where the exact answer is 0/0); a series with
+//     any suspect lag is recomputed by acf_exact_lag -- the reference's two passes, means first,
+//     in its order -- so its NaN pattern and bits are the reference's.  On well-conditioned
+//     series (every bench panel) nothing is flagged and the one-pass path stands.
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -171,6 +180,90 @@ __device__ __forceinline__ double robust_shift(const double* src, int64_t T, int
 // True when series position t contributes to the middle sums (rule 2).
 __device__ __forceinline__ bool acf_mid(int64_t t, int64_t T) { return t >= kAcfEdge && t < T - kAcfEdge; }
 
+// Rule 3: may the one-pass result r of one lag differ from the reference's by more than the
+// ACF tolerance?  sum / sq: the slice sums of y = x - c and of y^2, v = sq - sum^2 / N.
+//   * NaN / inf data (a non-finite sum): both paths give NaN -- not suspect.
+//   * v <= 0 or a non-finite r: a (near-)constant slice; the reference's rounded mean makes
+//     its variance N d^2 > 0 (1.0 for a constant 100.1, tiny values for a constant-but-one-end
+//     series) -- suspect.
+//   * one-pass error: |dr| ~ eps G (sqrt(R1 R2) + |r| (R1 + R2) / 2) with R = sq / v (digits
+//     cancelled; 1 when c is the mean) and G = max(sqrt(N) / 8, 16); the numpy emulation
+//     (tests/test_acf_robust.py) measures G <= 4 on the spike-train rows.
+//   * the reference's own deviation from its rounded means: recursive summation of N values
+//     errs by at most u N rms(x) in the mean (u = 2^-53; a constant series reaches ~0.1 of
+//     that: the bound's quarter is used), which moves the covariance by N d1 d2 and the
+//     variances by N d^2.
+// Suspect when their sum exceeds 1e-11 |r| (a tenth of the 1e-10 bar) and the reference's own
+// rounding-noise level eps sqrt(N) (below which its value is noise: white-noise correlations).
+__device__ __forceinline__ bool acf_suspect(double r, double sum1, double sq1, double sum2, double sq2, double v1,
+                                            double v2, double N, double c) {
+    if (!(__builtin_isfinite(sum1) && __builtin_isfinite(sq1) && __builtin_isfinite(sum2) && __builtin_isfinite(sq2)))
+        return false;
+    if (!(v1 > 0.0) || !(v2 > 0.0) || !__builtin_isfinite(r)) return true;
+    constexpr double eps = 0x1p-52;
+    const double R1 = sq1 / v1, R2 = sq2 / v2, ar = __builtin_fabs(r), rn = __builtin_sqrt(N);
+    const double G = __builtin_fmax(rn * 0.125, 16.0);
+    const double e_ours = eps * G * (__builtin_sqrt(R1 * R2) + ar * 0.5 * (R1 + R2));
+    const double d1 = 0x1p-55 * N * (__builtin_fabs(c) + __builtin_sqrt(sq1 / N));
+    const double d2 = 0x1p-55 * N * (__builtin_fabs(c) + __builtin_sqrt(sq2 / N));
+    const double e_ref = N * d1 * d2 / __builtin_sqrt(v1 * v2) + ar * 0.5 * (N * d1 * d1 / v1 + N * d2 * d2 / v2);
+    return e_ours + e_ref > __builtin_fmax(1e-11 * ar, eps * rn);
+}
+
+// The reference's autocorr of lag i (1 <= i < T) over F (S/UnivariateTimeSeries.scala:71-89,
+// Breeze mean = left-to-right sum / count): means first, then the centred sums, every sum
+// sequential in the reference's order (-ffp-contract=off): the reference's bits.  One lane per
+// lag; adjacent lags read adjacent addresses (coalesced), F[j] is wave-uniform.  Cost ~3 T
+// dependent steps per lane: the fallback of rule 3 and the T <= 2K path only.
+__device__ __forceinline__ double acf_exact_lag(const double* F, int64_t T, int i) {
+    const int64_t len = T - i;
+    const double* a = F + i;
+    double s1 = 0.0, s2 = 0.0;
+    int64_t j = 0;
+    for (; j + 8 <= len; j += 8) {
+        double p[8], q[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            p[k] = a[j + k];
+            q[k] = F[j + k];
+        }
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            s1 += p[k];
+            s2 += q[k];
+        }
+    }
+    for (; j < len; j++) {
+        s1 += a[j];
+        s2 += F[j];
+    }
+    const double m1 = s1 / (double)len, m2 = s2 / (double)len;
+    double v1 = 0.0, v2 = 0.0, cv = 0.0;
+    j = 0;
+    for (; j + 8 <= len; j += 8) {
+        double p[8], q[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            p[k] = a[j + k];
+            q[k] = F[j + k];
+        }
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            const double d1 = p[k] - m1, d2 = q[k] - m2;
+            v1 += d1 * d1;
+            v2 += d2 * d2;
+            cv += d1 * d2;
+        }
+    }
+    for (; j < len; j++) {
+        const double d1 = a[j] - m1, d2 = F[j] - m2;
+        v1 += d1 * d1;
+        v2 += d2 * d2;
+        cv += d1 * d2;
+    }
+    return cv / (__builtin_sqrt(v1) * __builtin_sqrt(v2));
+}
+
 // The reference's correlation for lag i (1 <= i <= kAcfEdge, T >= 2 * kAcfEdge) from
 //   Pi = sum_{j < T-i} y_j y_{j+i},  Sm / Qm = sum / sum of squares of y over the middle,
 //   hy(j) = y_j and tz(j) = y_{T-1-j} for j < kAcfEdge.
@@ -179,9 +272,10 @@ __device__ __forceinline__ bool acf_mid(int64_t t, int64_t T) { return t >= kAcf
 // operands in the same order to get the same bits (the fused and separate finalizes do).
 // The edge length E is kAcfEdge on the fused K <= 63 paths and K itself on the wide path
 // (sts_acf_wide.hip); T >= 2E, i <= E.
+// c: the shift of y = x - c; *suspect: rule 3's verdict on the result.
 template <class HY, class TZ>
 __device__ __forceinline__ double acf_combine_e(double Pi, double Sm, double Qm, int i, int64_t T, int E, HY hy,
-                                                TZ tz) {
+                                                TZ tz, double c, bool* suspect) {
     double sum1 = Sm, sq1 = Qm, sum2 = Sm, sq2 = Qm;
     for (int j = 0; j < E; j++) {
         const double y = hy(j), z = tz(j);
@@ -201,12 +295,15 @@ __device__ __forceinline__ double acf_combine_e(double Pi, double Sm, double Qm,
     const double v1 = sq1 - sum1 * sum1 / N;
     const double v2 = sq2 - sum2 * sum2 / N;
     const double cv = Pi - sum1 * sum2 / N;
-    return cv / (__builtin_sqrt(v1) * __builtin_sqrt(v2));   // S/UnivariateTimeSeries.scala:89
+    const double r = cv / (__builtin_sqrt(v1) * __builtin_sqrt(v2));   // S/UnivariateTimeSeries.scala:89
+    *suspect = acf_suspect(r, sum1, sq1, sum2, sq2, v1, v2, N, c);
+    return r;
 }
 
 template <class HY, class TZ>
-__device__ __forceinline__ double acf_combine(double Pi, double Sm, double Qm, int i, int64_t T, HY hy, TZ tz) {
-    return acf_combine_e(Pi, Sm, Qm, i, T, kAcfEdge, hy, tz);
+__device__ __forceinline__ double acf_combine(double Pi, double Sm, double Qm, int i, int64_t T, HY hy, TZ tz,
+                                              double c, bool* suspect) {
+    return acf_combine_e(Pi, Sm, Qm, i, T, kAcfEdge, hy, tz, c, suspect);
 }
 
 }  // namespace sts

@@ -151,19 +151,7 @@ __global__ __launch_bounds__(256) void acf_wide_finalize_kernel(const double* __
         out = __builtin_nan("");
     } else if (T <= 2 * (int64_t)K) {
         // the reference's loop (S/UnivariateTimeSeries.scala:71-89), means first
-        const int64_t len = T - i;
-        double s1 = 0.0, s2 = 0.0;
-        for (int64_t j = 0; j < len; j++) s1 += x[i + j];
-        for (int64_t j = 0; j < len; j++) s2 += x[j];
-        const double m1 = s1 / (double)len, m2 = s2 / (double)len;
-        double v1 = 0.0, v2 = 0.0, cv = 0.0;
-        for (int64_t j = 0; j < len; j++) {
-            const double d1 = x[i + j] - m1, d2 = x[j] - m2;
-            v1 += d1 * d1;
-            v2 += d2 * d2;
-            cv += d1 * d2;
-        }
-        out = cv / (__builtin_sqrt(v1) * __builtin_sqrt(v2));
+        out = acf_exact_lag(x, T, i);
     } else {
         const int b = (i - 1) / kWideLags, d = (i - 1) % kWideLags;
         const double c = shift[s];
@@ -174,8 +162,11 @@ __global__ __launch_bounds__(256) void acf_wide_finalize_kernel(const double* __
             Sm += pr[64];
             Qm += pr[65];
         }
+        bool sus;
         out = acf_combine_e(Pi, Sm, Qm, i, T, K, [&](int j) { return x[j] - c; },
-                            [&](int j) { return x[T - 1 - j] - c; });
+                            [&](int j) { return x[T - 1 - j] - c; }, c, &sus);
+        // sts_acf.hpp rule 3: the wave's 64 lags take the reference's loop when any is suspect
+        if (__ballot(sus)) out = acf_exact_lag(x, T, i);
     }
     acf[s * K + (i - 1)] = out;
 }

@@ -223,9 +223,10 @@ int run_tile(const double* in, double* out, double* lagmat, int64_t S, int64_t T
                       !sts::ab_knob("STS_NO_FUSED_ACF");
     a.err_all = one_seg ? 1 : 0;
     a.acf_fused = fuse ? acf : nullptr;
-    // fill('linear' / 'previous' / 'next') + ACF with K <= 24 on T <= 2560 (C1): one wave holds the whole series
-    // (sts_short.hip); STS_NO_SHORT keeps the segment kernel (A/B build)
-    const bool short_k = fuse && sts::short_ok(method, T, K) && !sts::ab_knob("STS_NO_SHORT");
+    // any of the four fills + ACF with K <= 24 on T <= 2560 (C1): one wave holds the whole series
+    // (sts_short.hip; its rule-3 fallback re-reads the filled series from out); STS_NO_SHORT keeps
+    // the segment kernel (A/B build)
+    const bool short_k = fuse && out && sts::short_ok(method, T, K) && !sts::ab_knob("STS_NO_SHORT");
     if (err && !one_seg) HIP_TRY(hipMemsetAsync(err, 0, (size_t)S * sizeof(int32_t), st), "hipMemsetAsync(err)");
     Scratch part(st);
     if (K > 0 && !fuse) {

@@ -666,12 +666,20 @@ __global__ __launch_bounds__(256, 4) void seg_kernel(TileArgs a, int method) {
             const int i = lane + 1;
             const double Pi = 0.0 + __shfl(lagacc, (lane + 1) & 63), Sm = 0.0 + sm, Qm = 0.0 + qm;
             const double* tail = tail_base;   // y of the last tile, indexed by series position - kb_last
-            const double r = acf_combine(
+            bool sus;
+            double r = acf_combine(
                 Pi, Sm, Qm, i, T,
                 [&](int j) {   // j is wave-uniform: a scalar lane select, not an LDS-crossbar shuffle
                     return readlane_d((j & 1) ? head.y : head.x, j >> 1);
                 },
-                [&](int j) { return tail[T - 1 - j - kb_last]; });
+                [&](int j) { return tail[T - 1 - j - kb_last]; }, st.c0, &sus);
+            // sts_acf.hpp rule 3: a suspect series takes the reference's loop over F, which this
+            // wave wrote itself (one segment per series): order its stores before the reads
+            if (__ballot(sus && lane < K)) {
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+                const double* F = cx.dst ? cx.dst : cx.src;
+                if (lane < K) r = acf_exact_lag(F, T, i);
+            }
             if (lane < K) a.acf_fused[s * K + lane] = r;
         }
     }

@@ -277,7 +277,14 @@ __global__ __launch_bounds__(64 * kShortWaves, 2) void short_fill_acf_kernel(Til
     const double v1 = sq1 - sum1 * sum1 / N;
     const double v2 = sq2 - sum2 * sum2 / N;
     const double cv = Pi - sum1 * sum2 / N;
-    if (lane < K) a.acf_fused[s * K + lane] = cv / (__builtin_sqrt(v1) * __builtin_sqrt(v2));   // :89
+    double r = cv / (__builtin_sqrt(v1) * __builtin_sqrt(v2));   // :89
+    // sts_acf.hpp rule 3: a suspect series takes the reference's loop over the filled series
+    // this wave stored (the LDS block is scratch by now): order the stores before the reads
+    if (__ballot(lane < K && acf_suspect(r, sum1, sq1, sum2, sq2, v1, v2, N, c0))) {
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+        if (lane < K) r = acf_exact_lag(a.out + s * a.ld_out, T, lane + 1);
+    }
+    if (lane < K) a.acf_fused[s * K + lane] = r;
 }
 
 }  // namespace

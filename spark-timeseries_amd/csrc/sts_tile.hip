@@ -34,47 +34,19 @@
 #include "sts_internal.hpp"
 #include "sts_acf.hpp"
 #include "sts_scan.hpp"
-#include "sts_dma.hpp"
 
 #include <hip/hip_runtime.h>
 
 #include <type_traits>
 
-#ifndef STS_MFMA_UNROLL
-#define STS_MFMA_UNROLL 1 // fully unrolled full-range MFMA phase (A/B: ~1.5 % faster)
-#endif
-
-#ifndef STS_LDS_BARRIER
-#define STS_LDS_BARRIER 1
-#endif
-
-#ifndef STS_DIAG
-#define STS_DIAG 0        // diagnostic builds only (tools/variant.sh): 1 = no MFMA, 2 = no LDS operand reads,
-                          // 3 / 4 = cost models of I8 (Ozaki-split) lag products (timing only, see below)
-#endif
-
-#ifndef STS_TILE_DB
-#define STS_TILE_DB 0     // K <= 60: double-buffered tiles, lag products interleaved into the next tile
-#endif
+// Measured-negative variants of this kernel (rounds 1-3: double-buffered tiles with the lag
+// products interleaved into the next tile, LDS-DMA tile prefetch, early / split prefetch issue,
+// middle sums in the y pass, the no-MFMA / no-operand diagnostics and the I8 Ozaki cost models)
+// are not in this source: their records are in DESIGN.md §5.2 / profiles/INDEX.md and their code
+// at commit bd59bf8 (tools/var_rev.sh builds a library from any revision for same-box A/B).
 
 #ifndef STS_TILE_WGS
 #define STS_TILE_WGS 4    // workgroups per CU the register budget is sized for (128 VGPRs; LDS 40.5 KB x 4 fits)
-#endif
-
-#ifndef STS_TILE_DMA
-#define STS_TILE_DMA 0    // A/B: the next interior tile arrives by LDS-DMA into a staging buffer, issued at tile start
-#endif
-
-#ifndef STS_PF_POS
-#define STS_PF_POS 0      // A/B: 1 = the next tile's register prefetch is issued before the store pass
-#endif
-
-#ifndef STS_SUMS_Y
-#define STS_SUMS_Y 0      // A/B: fast-path tiles take the middle sums in the y pass, not under the MFMAs
-#endif
-
-#ifndef STS_EARLY
-#define STS_EARLY 0       // A/B: 1 = fill-only tiles issue the next loads at tile start, 2 = all tiles
 #endif
 
 
@@ -85,13 +57,9 @@ namespace {
 // thread of the kernel wrote, so global loads (the register prefetch) and stores need no
 // ordering here -- and a fence on all address spaces would pin them in program order.
 __device__ __forceinline__ void lds_barrier() {
-#if STS_LDS_BARRIER
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-#else
-    __syncthreads();
-#endif
 }
 
 typedef double d4 __attribute__((ext_vector_type(4)));
@@ -210,8 +178,8 @@ __device__ __forceinline__ int px2_(int q2) { return PAD ? q2 + ((q2 >> 4) << 1)
 // + j%q -- every lag 0 .. 16 NT - q exactly once per step, and the same lag map h(j) - i in
 // every accumulator; TOEPLITZ (K = 61..63) uses NT = floor((K + 15) / 16) + 1 MFMAs with
 // U_t holding lag 16t + j - i.
-template <int TW, int NT, bool SHIFTED, int NTH, bool DB = false, bool DMA = false>
-__global__ __launch_bounds__(NTH, (DB || DMA) ? 2 : STS_TILE_WGS) void tile_kernel(TileArgs a, int method) {
+template <int TW, int NT, bool SHIFTED, int NTH>
+__global__ __launch_bounds__(NTH, STS_TILE_WGS) void tile_kernel(TileArgs a, int method) {
     constexpr int kThreads = NTH;          // 256 (4 waves) or 128 (2 waves, TW = 2048)
     constexpr int kWaves = NTH / 64;
     static_assert(TW / 64 % kWaves == 0, "whole 64-step chunks per wave");
@@ -234,13 +202,8 @@ __global__ __launch_bounds__(NTH, (DB || DMA) ? 2 : STS_TILE_WGS) void tile_kern
     constexpr int RPT = (NP2 + kThreads - 1) / kThreads;     // prefetch registers per thread
     static_assert(EW % 64 == 0, "extended tile must be whole words");
     static_assert(NW <= 128, "word scan handles at most 128 words");
-    // padded (px) for the shifted scheme; DB: two tile buffers, tile k in buffer k & 1, so tile
-    // k's lag products can run during tile k + 1's phases
-    __shared__ __attribute__((aligned(16))) double vals_mem[(DB ? 2 : 1) * EWP];
-    double* vals = vals_mem;
-    // DMA: raw staging image of the next interior extended tile (lane-linear 1-KB pieces)
-    constexpr int NDMA = (NP2 + 63) / 64;                    // 1-KB DMA instructions per tile
-    __shared__ __attribute__((aligned(16))) double stg_mem[DMA ? NDMA * 128 : 2];
+    // padded (px) for the shifted scheme
+    __shared__ __attribute__((aligned(16))) double vals[EWP];
     __shared__ unsigned long long mask[NW];
     __shared__ int lastUpTo[NW];           // last valid E-position in words <= w (-1: none)
     __shared__ int firstFrom[NW];          // first valid E-position in words >= w (kBig: none)
@@ -287,7 +250,6 @@ __global__ __launch_bounds__(NTH, (DB || DMA) ? 2 : STS_TILE_WGS) void tile_kern
         sh_c[2] = -1;
     }
     double acc_s = 0.0, acc_q = 0.0;   // sum y, sum y^2 over this thread's middle positions
-    bool ysums = false;                // STS_SUMS_Y: this tile's middle sums were taken in the y pass
 
     // register prefetch of one INTERIOR extended tile [e0, e0 + EW); the first and last tile
     // of a series (which touch its ends) are loaded synchronously with bounds checks
@@ -319,27 +281,6 @@ __global__ __launch_bounds__(NTH, (DB || DMA) ? 2 : STS_TILE_WGS) void tile_kern
         asm volatile("" : "=v"(R0), "=v"(R1), "=v"(R2), "=v"(R3), "=v"(R4));               \
         asm volatile("" : "=v"(R5), "=v"(R6), "=v"(R7), "=v"(R8));                         \
     } while (0)
-// DMA: wave w issues the 1-KB pieces m = w, w + kWaves, ... of interior tile kk into the
-// staging image (pieces past the tile read its first piece into the image's tail)
-#define STS_DMA_ISSUE(kk)                                                                   \
-    do {                                                                                    \
-        const double* s0_ = src + ((kk) * TW - kHB);                                        \
-        for (int m_ = wave; m_ < NDMA; m_ += kWaves) {                                      \
-            const int q2_ = m_ * 64 + lane;                                                 \
-            glds16(s0_ + 2 * (q2_ < NP2 ? q2_ : 0), lds_addr(stg_mem) + (unsigned)(m_ << 10)); \
-        }                                                                                   \
-    } while (0)
-#define STS_DMA_TAKE()                                                                      \
-    do {                                                                                    \
-        const double2* g2_ = reinterpret_cast<const double2*>(stg_mem);                     \
-        STS_TK1(0) STS_TK1(1) STS_TK1(2) STS_TK1(3) STS_TK1(4)                              \
-        STS_TK1(5) STS_TK1(6) STS_TK1(7) STS_TK1(8)                                         \
-    } while (0)
-#define STS_TK1(j)                                                                          \
-    if constexpr (j < RPT) {                                                                \
-        const int q2_ = tid + j * kThreads;                                                 \
-        R##j = g2_[q2_ < NP2 ? q2_ : NP2 - 1];                                              \
-    }
 // (the bound test only where it can fail: a runtime test on every register kept a spilled
 // exec mask per register alive across the tile loop)
 #define STS_ST1(j)                                                                          \
@@ -352,47 +293,17 @@ __global__ __launch_bounds__(NTH, (DB || DMA) ? 2 : STS_TILE_WGS) void tile_kern
 #pragma unroll
     for (int t = 0; t < NA; t++) U[t] = d4{0.0, 0.0, 0.0, 0.0};
     bool series_err = false;
-#if STS_DIAG >= 3
-    // COST MODEL of the lag products on the I8 MFMA (timing only, the
-    // numbers it produces are not the ACF).  An Ozaki split of y into D = 7 signed 8-bit digits
-    // relative to a per-tile power-of-two scale needs the 28 digit pairs of weight <= 6, each a
-    // v_mfma_i32_16x16x64_i8 per 1024 steps and window shift (4 shifts): 112 I8 MFMAs per wave
-    // per tile (16 cycles each) instead of 64 FP64 ones (64 cycles each), with 7 exact int32
-    // accumulators (one per weight) flushed into the FP64 lag sums once per tile.
-    //   STS_DIAG 3: the I8 MFMAs (7 per 64-step chunk) with their operand fetches (4 x 16 B per
-    //               chunk from LDS + 14 byte aligns for the unaligned digit windows) in place of
-    //               the FP64 ones, mid sums in the store pass, per-tile flush;
-    //   STS_DIAG 4: 3 + the digit split itself: the tile's max |y| (wave reductions + LDS),
-    //               a quantisation pass after the store pass (re-read y, scale, floor / cvt into
-    //               a 56-bit integer, balanced digits, byte transposes, 7 bytes per step into
-    //               LDS digit planes) and one more barrier; the MFMAs read the planes.
-    typedef int i4 __attribute__((ext_vector_type(4)));
-    i4 UI[7];
-#pragma unroll
-    for (int w = 0; w < 7; w++) UI[w] = i4{0, 0, 0, 0};
-#endif
-#if STS_DIAG == 4
-    __shared__ __attribute__((aligned(16))) unsigned planes[7 * (EW / 4)];
-    __shared__ double wmax[kWaves];
-    double tmax = 0.0;
-#endif
-
 #ifdef STS_STAMPS
     unsigned long long st_acc[12] = {0};
     unsigned long long st_prev = __builtin_amdgcn_s_memtime();
 #endif
     bool have = interior(k_begin);
-    if constexpr (DMA) {
-        if (have) STS_DMA_ISSUE(k_begin);
-        STS_CLEAR();
-    } else {
-        if (have) STS_ISSUE(k_begin);
-        else STS_CLEAR();
-    }
+    if (have) STS_ISSUE(k_begin);
+    else STS_CLEAR();
     // ACF shift (sts_acf.hpp: median of 64 raw samples of the series), computed once per
     // series by acf_shift_kernel before this launch: a scalar load
     // (made wave-uniform in SGPRs here: a VGPR load result used inside the tile loop gets a
-    // vmcnt(0) at its use in every tile, which would also wait for the next tile's DMA)
+    // vmcnt(0) at its use in every tile, which would also wait for the next tile's prefetch)
     const double c0 = [&] {
         if constexpr (NT == 0) return 0.0;
         const double v = a.shift[s];
@@ -408,7 +319,6 @@ __global__ __launch_bounds__(NTH, (DB || DMA) ? 2 : STS_TILE_WGS) void tile_kern
     constexpr int qA0 = kHB;                // E-position of the tile's first step
     constexpr int NTA = NT > 0 ? NT : 1;    // array extent (NT = 0 instantiates no MFMA code)
     constexpr int CPW = TW / 64 / kWaves;   // 64-step chunks per wave
-    constexpr int kG1 = (CPW * 3) / 8, kG2 = (CPW * 5) / 8;   // DB group boundaries
     auto mid_sums = [&](int p, double y) {
         // sum y / sum y^2 over the series' middle (sts_acf.hpp rule 2): lane l of the chunk
         // at series position p holds y(p + l)
@@ -455,7 +365,6 @@ __global__ __launch_bounds__(NTH, (DB || DMA) ? 2 : STS_TILE_WGS) void tile_kern
                 // wave 0 of the first tile also runs chunk -1 (the look-back, y = 0), whose
                 // shifted windows hold the series' first QS t steps
                 if (F == 0 && kk == 0 && wave == 0) chunk_mfma(vb);   // y = 0 there: no middle-sum term
-#if STS_MFMA_UNROLL
                 if (full && tile_mid) {
                     // full chunk range, unrolled: per-lane LDS indices made opaque once per
                     // group (else LICM hoists all of them out of the tile loop and spills),
@@ -471,66 +380,21 @@ __global__ __launch_bounds__(NTH, (DB || DMA) ? 2 : STS_TILE_WGS) void tile_kern
                     }
 #pragma unroll
                     for (int cc = F; cc < TE; cc++) {
-#if STS_DIAG >= 3   // I8 cost model (see the declaration of UI)
-                        {
-#if STS_DIAG == 4
-                            const i4* pq = reinterpret_cast<const i4*>(planes);
-                            constexpr int SH = 2;
-#else
-                            const i4* pq = reinterpret_cast<const i4*>(vb);
-                            constexpr int SH = 1;
-#endif
-                            i4 o[4];
-                            o[0] = pq[(ia[0] + 72 * cc) >> SH];
-                            o[1] = pq[(ib[0] + 72 * cc) >> SH];
-                            o[2] = pq[(ia[1] + 72 * cc) >> SH];
-                            o[3] = pq[(ib[1] + 72 * cc) >> SH];
-                            const unsigned sa = (unsigned)lane & 3u;
-#pragma unroll
-                            for (int u = 0; u < 4; u++) {
-                                o[u].x = (int)__builtin_amdgcn_alignbyte((unsigned)o[u].y, (unsigned)o[u].x, sa);
-                                o[u].y = (int)__builtin_amdgcn_alignbyte((unsigned)o[u].z, (unsigned)o[u].y, sa);
-                                o[u].z = (int)__builtin_amdgcn_alignbyte((unsigned)o[u].w, (unsigned)o[u].z, sa);
-                                if (u < 2) o[u].w = (int)__builtin_amdgcn_alignbyte((unsigned)o[u].x, (unsigned)o[u].w, sa);
-                            }
-                            UI[0] = __builtin_amdgcn_mfma_i32_16x16x64_i8(o[0], o[1], UI[0], 0, 0, 0);
-                            UI[1] = __builtin_amdgcn_mfma_i32_16x16x64_i8(o[0], o[3], UI[1], 0, 0, 0);
-                            UI[2] = __builtin_amdgcn_mfma_i32_16x16x64_i8(o[2], o[1], UI[2], 0, 0, 0);
-                            UI[3] = __builtin_amdgcn_mfma_i32_16x16x64_i8(o[2], o[3], UI[3], 0, 0, 0);
-                            UI[4] = __builtin_amdgcn_mfma_i32_16x16x64_i8(o[1], o[0], UI[4], 0, 0, 0);
-                            UI[5] = __builtin_amdgcn_mfma_i32_16x16x64_i8(o[3], o[0], UI[5], 0, 0, 0);
-                            UI[6] = __builtin_amdgcn_mfma_i32_16x16x64_i8(o[3], o[2], UI[6], 0, 0, 0);
-                        }
-                        __builtin_amdgcn_sched_barrier(0);
-#else
                         double av[NTA], bv[NTA];
 #pragma unroll
                         for (int t = 0; t < NT; t++) {
-#if STS_DIAG == 2   // diagnostic only: no LDS operand reads
-                            av[t] = (double)(ia[t] + cc);
-                            bv[t] = (double)(ib[t] - cc);
-#else
                             av[t] = vb[ia[t] + 72 * cc];
                             bv[t] = vb[ib[t] + 72 * cc];
-#endif
                         }
 #pragma unroll
                         for (int t = 0; t < NT; t++)
-#if STS_DIAG == 1   // diagnostic only: no MFMA
-                            U[t % NA][t] += av[t] * bv[t];
-#else
                             U[t % NA] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[t], bv[t], U[t % NA], 0, 0, 0);
-#endif
-                        if (!STS_SUMS_Y || !ysums) {
-                            acc_s += av[0];   // middle sums: VALU under the MFMA pipe
-                            acc_q = __builtin_fma(av[0], av[0], acc_q);
-                        }
+                        acc_s += av[0];   // middle sums: VALU under the MFMA pipe
+                        acc_q = __builtin_fma(av[0], av[0], acc_q);
                         __builtin_amdgcn_sched_barrier(0);   // one chunk's operands live at a time
-#endif
                     }
                     c = cend;
                 }
-#endif
                 for (; c < cend; c++) mid_sums(tt0 + 64 * c, chunk_mfma(vb + px(qA0 + 64 * c)));   // chunk start: a multiple of 32
             } else {
                 // U_t += y(j0 + l) x y(j0 + 16t + l)
@@ -547,17 +411,7 @@ __global__ __launch_bounds__(NTH, (DB || DMA) ? 2 : STS_TILE_WGS) void tile_kern
             }
         }
     };
-    // DB: the previous tile, whose lag products run in groups inside this tile's phases
-    const double* prev_vals = vals_mem;
-    int64_t prev_k = -1;
-    int prev_t0 = 0, prev_t1 = 0;
     for (int64_t k = k_begin; k < k_end; k++) {
-        if constexpr (DB) vals = vals_mem + (k & 1) * EWP;
-        if constexpr (DB && NT > 0) {
-            // group 1: under the wait for this tile's prefetched registers
-            if (prev_k >= 0) mfma_group(std::integral_constant<int, 0>{}, std::integral_constant<int, kG1>{},
-                                        prev_vals, prev_k, prev_t0, prev_t1);
-        }
         const int t0 = (int)(k * TW);
         const int t1 = (t0 + TW < T) ? t0 + TW : (int)T;
         const int e0 = t0 - kHB;
@@ -567,12 +421,6 @@ __global__ __launch_bounds__(NTH, (DB || DMA) ? 2 : STS_TILE_WGS) void tile_kern
         //      wave v holds steps 128v + 512j + 2*lane (+1), i.e. words 2v + 8j and 2v + 8j + 1
         //      as an even/odd bit interleave ----
         if (have) {
-            if constexpr (DMA) {
-                // every wave's pieces have landed (own DMA waited, then the barrier for the others)
-                dma_wait();
-                lds_barrier();
-                STS_DMA_TAKE();
-            }
             double2* v2_ = reinterpret_cast<double2*>(vals);
             const int pst_ = opq(px2(tid));   // px2(tid + j kThreads) = px2(tid) + j PX2S
             STS_ST1(0) STS_ST1(1) STS_ST1(2) STS_ST1(3) STS_ST1(4) STS_ST1(5) STS_ST1(6) STS_ST1(7) STS_ST1(8)
@@ -609,18 +457,6 @@ __global__ __launch_bounds__(NTH, (DB || DMA) ? 2 : STS_TILE_WGS) void tile_kern
         STAMP(0);
         lds_barrier();
         STAMP(1);
-        // DMA: the staging image is free again (every thread took its pieces before the
-        // barrier): the next tile streams in during this whole tile
-        if constexpr (DMA) {
-            if (have_next) STS_DMA_ISSUE(k + 1);
-        }
-#if STS_EARLY
-        // A/B: the next tile's loads right after this tile's registers are in LDS
-        if constexpr (STS_EARLY == 2 || NT == 0) {
-            if (have_next) STS_ISSUE(k + 1);
-            else STS_CLEAR();
-        }
-#endif
 
         // positions to produce: [qA, qB) (E-relative); the ACF needs REACH steps past the tile
         const int qA = kHB;
@@ -744,11 +580,6 @@ __global__ __launch_bounds__(NTH, (DB || DMA) ? 2 : STS_TILE_WGS) void tile_kern
                 if (lane == 0) sh_d[2] = v;
             }
         }
-        if constexpr (DB && NT > 0) {
-            // group 2: waves 1-3 wait here for wave 0's scan anyway
-            if (prev_k >= 0) mfma_group(std::integral_constant<int, kG1>{}, std::integral_constant<int, kG2>{},
-                                        prev_vals, prev_k, prev_t0, prev_t1);
-        }
         STAMP(4);
         lds_barrier();
         STAMP(5);
@@ -867,16 +698,6 @@ __global__ __launch_bounds__(NTH, (DB || DMA) ? 2 : STS_TILE_WGS) void tile_kern
         lds_barrier();
         STAMP(7);
 
-#if STS_PF_POS == 1
-        // A/B: the next tile's loads before the store pass (in flight during stores + MFMA)
-        if constexpr (!DMA) {
-            if (have_next) STS_ISSUE(k + 1);
-            else STS_CLEAR();
-        }
-#endif
-#if STS_PF_POS == 2
-        bool pf_lo = false;   // registers 0-3 of the next tile issued inside the store pass
-#endif
         // ---- 5. filled output + lag matrix (16-B stores), then y = F - F(0) in place
         //      (0 past the series end) for the MFMA phase; start the next tile's loads ----
         {
@@ -888,9 +709,7 @@ __global__ __launch_bounds__(NTH, (DB || DMA) ? 2 : STS_TILE_WGS) void tile_kern
             // every index and guard below is a compile-time constant
             const bool fast = (dst == nullptr || al) && !a.lagmat && (t1 - t0 == TW) &&
                               (NT == 0 || e0 + qW + REACH <= T);
-            ysums = false;
             if (fast) {
-                if constexpr (STS_SUMS_Y && NT > 0 && !DB) ysums = true;
                 constexpr int FS = TW / 2 / kThreads;                          // stored double2
                 constexpr int FY = NT > 0 ? (NP2 - kHB / 2 + kThreads - 1) / kThreads : FS;
                 constexpr int FH = (FY + 1) / 2;     // two halves: fewer live registers
@@ -904,14 +723,6 @@ __global__ __launch_bounds__(NTH, (DB || DMA) ? 2 : STS_TILE_WGS) void tile_kern
                 asm volatile("" : "+v"(dpo));   // per tile: else LICM keeps dst + dpo as a 64-bit VGPR pair
 #pragma unroll
                 for (int h = 0; h < 2; h++) {
-#if STS_PF_POS == 2
-                    // A/B: the first half of the next tile's loads between the two store halves
-                    if (h == 1 && have_next) {
-                        const double2* s2_ = reinterpret_cast<const double2*>(src + ((k + 1) * TW - kHB));
-                        STS_LD1(0) STS_LD1(1) STS_LD1(2) STS_LD1(3)
-                        pf_lo = true;
-                    }
-#endif
                     double2 fv[FH];
 #pragma unroll
                     for (int j = 0; j < FH; j++) {
@@ -936,18 +747,6 @@ __global__ __launch_bounds__(NTH, (DB || DMA) ? 2 : STS_TILE_WGS) void tile_kern
                             y.x = fv[j].x - c0;
                             y.y = fv[j].y - c0;
                             v2[pvq + jj * PX2S] = y;
-#if STS_DIAG >= 3   // cost model: the middle sums move from the MFMA loop to this pass
-                            acc_s += y.x + y.y;
-                            acc_q = __builtin_fma(y.x, y.x, __builtin_fma(y.y, y.y, acc_q));
-#elif STS_SUMS_Y
-                            if (jj < FS) {   // the tile's own positions (a fast tile is a middle tile)
-                                acc_s = (acc_s + y.x) + y.y;
-                                acc_q = __builtin_fma(y.y, y.y, __builtin_fma(y.x, y.x, acc_q));
-                            }
-#endif
-#if STS_DIAG == 4
-                            tmax = __builtin_fmax(tmax, __builtin_fmax(__builtin_fabs(y.x), __builtin_fabs(y.y)));
-#endif
                         }
                     }
                 }
@@ -985,116 +784,22 @@ __global__ __launch_bounds__(NTH, (DB || DMA) ? 2 : STS_TILE_WGS) void tile_kern
             // the look-back range as y = 0
             if (SHIFTED && NT > 0 && e0 < 0 && tid < kHB / 2) v2[px2(tid)] = make_double2(0.0, 0.0);
         }
-#if STS_EARLY
-        if constexpr (!(STS_EARLY == 2 || NT == 0))
-#endif
-        {
-            if constexpr (DMA) STS_CLEAR();
-#if STS_PF_POS == 0
-            else if (have_next) STS_ISSUE(k + 1);   // in flight during the MFMA phase of tile k
-            else STS_CLEAR();
-#elif STS_PF_POS == 2
-            else if (have_next) {
-                if (!pf_lo) STS_ISSUE(k + 1);
-                else {
-                    const double2* s2_ = reinterpret_cast<const double2*>(src + ((k + 1) * TW - kHB));
-                    STS_LD1(4) STS_LD1(5) STS_LD1(6) STS_LD1(7) STS_LD1(8)
-                }
-            } else STS_CLEAR();
-#endif
-        }
+        if (have_next) STS_ISSUE(k + 1);   // in flight during the MFMA phase of tile k
+        else STS_CLEAR();
         STAMP(8);
 
         if constexpr (NT > 0) {
-            if constexpr (DB) {
-                // group 3 of the previous tile, then the barrier that publishes this tile's y
-                if (prev_k >= 0) mfma_group(std::integral_constant<int, kG2>{}, std::integral_constant<int, CPW>{},
-                                            prev_vals, prev_k, prev_t0, prev_t1);
-                lds_barrier();
-                STAMP(9);
-                prev_vals = vals;
-                prev_k = k;
-                prev_t0 = t0;
-                prev_t1 = t1;
-            } else {
-#if STS_DIAG == 4   // cost model: the tile's max |y| -> scale, then the digit split into LDS planes
-                {
-#pragma unroll
-                    for (int d = 32; d >= 1; d >>= 1) tmax = __builtin_fmax(tmax, __shfl_xor(tmax, d));
-                    if (lane == 0) wmax[wave] = tmax;
-                }
-#endif
-                lds_barrier();
-                STAMP(9);
-#if STS_DIAG == 4
-                {
-                    double m = wmax[0];
-#pragma unroll
-                    for (int w = 1; w < kWaves; w++) m = __builtin_fmax(m, wmax[w]);
-                    int ex;
-                    (void)__builtin_frexp(m, &ex);
-                    const double sc_hi = __builtin_ldexp(1.0, 23 - ex), sc_lo = __builtin_ldexp(1.0, 55 - ex);
-                    const double2* v2q = reinterpret_cast<const double2*>(vals);
-                    for (int q2 = tid; q2 < NP2; q2 += kThreads) {
-                        const double2 y = v2q[px2(q2)];
-                        unsigned dl[2], dh[2];
-#pragma unroll
-                        for (int e = 0; e < 2; e++) {
-                            const double yy = e ? y.y : y.x;
-                            const double h = __builtin_floor(yy * sc_hi);
-                            const double r = __builtin_floor(__builtin_fma(h, -0x1p32, yy * sc_lo));
-                            const unsigned lo = (unsigned)r;
-                            const int hi = (int)h;
-                            const unsigned lo2 = lo + 0x80808080u;
-                            const int hi2 = hi + 0x808080 + (lo2 < lo ? 1 : 0);
-                            dl[e] = lo2 ^ 0x80808080u;
-                            dh[e] = (unsigned)hi2 ^ 0x808080u;
-                        }
-                        // byte transposes into the digit planes (7 bytes per step)
-                        const unsigned w0 = __builtin_amdgcn_perm(dl[1], dl[0], 0x05010400u);
-                        const unsigned w1 = __builtin_amdgcn_perm(dl[1], dl[0], 0x07030602u);
-                        const unsigned w2 = __builtin_amdgcn_perm(dh[1], dh[0], 0x05010400u);
-                        const unsigned w3 = __builtin_amdgcn_perm(dh[1], dh[0], 0x07030602u);
-                        unsigned* pl = planes + (q2 >> 1);
-                        pl[0 * (EW / 4)] = __builtin_amdgcn_perm(w0, w1, 0x05040100u);
-                        pl[1 * (EW / 4)] = __builtin_amdgcn_perm(w0, w1, 0x07060302u);
-                        pl[2 * (EW / 4)] = __builtin_amdgcn_perm(w2, w3, 0x05040100u);
-                        pl[3 * (EW / 4)] = __builtin_amdgcn_perm(w2, w3, 0x07060302u);
-                        pl[4 * (EW / 4)] = w0 ^ w2;
-                        pl[5 * (EW / 4)] = w1 ^ w3;
-                        pl[6 * (EW / 4)] = w0 ^ w3;
-                    }
-                    tmax = 0.0;
-                }
-                lds_barrier();
-#endif
-                // ---- 6. lag products on MFMA ----
-                mfma_group(std::integral_constant<int, 0>{}, std::integral_constant<int, CPW>{}, vals, k, t0, t1);
-#if STS_DIAG >= 3   // cost model: the per-tile flush of the 7 exact accumulators into the FP64 sums
-#pragma unroll
-                for (int w = 0; w < 7; w++) {
-#pragma unroll
-                    for (int r = 0; r < 4; r++) U[w & 1][r] = __builtin_fma((double)UI[w][r], c0 + (double)w, U[w & 1][r]);
-                    UI[w] = i4{0, 0, 0, 0};
-                }
-#endif
-            }
+            lds_barrier();
+            STAMP(9);
+            // ---- 6. lag products on MFMA ----
+            mfma_group(std::integral_constant<int, 0>{}, std::integral_constant<int, CPW>{}, vals, k, t0, t1);
         }
         have = have_next;
         STAMP(10);
-        if constexpr (!(DB && NT > 0)) lds_barrier();   // vals / mask / lists are reused by the next tile
+        lds_barrier();   // vals / mask / lists are reused by the next tile
         STAMP(11);
     }
-    if constexpr (DB && NT > 0) {
-        if (prev_k >= 0) mfma_group(std::integral_constant<int, 0>{}, std::integral_constant<int, CPW>{}, prev_vals,
-                                    prev_k, prev_t0, prev_t1);
-        lds_barrier();   // the finalize below reuses the buffers as scratch
-    }
-    vals = vals_mem;
 #undef STS_ISSUE
-#undef STS_DMA_ISSUE
-#undef STS_DMA_TAKE
-#undef STS_TK1
 #undef STS_LD1
 #undef STS_ST1
 #undef STS_CLEAR
@@ -1174,7 +879,7 @@ __global__ __launch_bounds__(NTH, (DB || DMA) ? 2 : STS_TILE_WGS) void tile_kern
 // 80-89) with the robust head / tail handling of sts_acf.hpp.  Lane l computes lag i = l + 1.
 // Series with T <= 2K (or shorter than the two edges) run the reference's two-pass loop
 // directly (reproduces its NaN pattern exactly when a NaN sits in the middle of a short
-// series).
+// series), and so does every series with a lag sts_acf.hpp's rule 3 finds suspect.
 __global__ __launch_bounds__(256) void acf_finalize_kernel(FinalizeArgs a) {
     const int lane = threadIdx.x & 63;
     const int64_t s = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -1188,19 +893,7 @@ __global__ __launch_bounds__(256) void acf_finalize_kernel(FinalizeArgs a) {
     if (i >= T) {
         out = __builtin_nan("");
     } else if (T <= 2 * (int64_t)K || T < 2 * kAcfEdge) {
-        const int64_t len = T - i;
-        double s1 = 0.0, s2 = 0.0;
-        for (int64_t j = 0; j < len; j++) s1 += F[i + j];
-        for (int64_t j = 0; j < len; j++) s2 += F[j];
-        const double m1 = s1 / (double)len, m2 = s2 / (double)len;
-        double v1 = 0.0, v2 = 0.0, cv = 0.0;
-        for (int64_t j = 0; j < len; j++) {
-            double d1 = F[i + j] - m1, d2 = F[j] - m2;
-            v1 += d1 * d1;
-            v2 += d2 * d2;
-            cv += d1 * d2;
-        }
-        out = cv / (__builtin_sqrt(v1) * __builtin_sqrt(v2));
+        out = acf_exact_lag(F, T, i);
     } else {
         double Pi = 0.0, Sm = 0.0, Qm = 0.0;
         const double* pp = a.partials + s * a.parts_per_series * kPartStride;
@@ -1210,8 +903,11 @@ __global__ __launch_bounds__(256) void acf_finalize_kernel(FinalizeArgs a) {
             Sm += pp[kPartSum];
             Qm += pp[kPartSq];
         }
+        bool sus;
         out = acf_combine(Pi, Sm, Qm, i, T, [&](int j) { return F[j] - c; },
-                          [&](int j) { return F[T - 1 - j] - c; });
+                          [&](int j) { return F[T - 1 - j] - c; }, c, &sus);
+        // sts_acf.hpp rule 3: a series with any suspect lag takes the reference's loop (all lags)
+        if (__ballot(sus)) out = acf_exact_lag(F, T, i);
     }
     a.acf[s * K + lane] = out;
 }
@@ -1252,9 +948,9 @@ hipError_t launch_tile(int method, int tw, const TileArgs& a, hipStream_t st) {
         else hipLaunchKernelGGL((tile_kernel<2048, 4, true, kThreads / 2>), grid, dim3(kThreads / 2), 0, st, a, method);
 #endif
     } else if (tw == 4096) {
-        if (a.K == 0) hipLaunchKernelGGL((tile_kernel<4096, 0, false, kThreads, false, STS_TILE_DMA>), grid, block, 0, st, a, method);
-        else if (a.K <= 24) hipLaunchKernelGGL((tile_kernel<4096, 2, true, kThreads, STS_TILE_DB, STS_TILE_DMA>), grid, block, 0, st, a, method);
-        else if (a.K <= 60) hipLaunchKernelGGL((tile_kernel<4096, 4, true, kThreads, STS_TILE_DB, STS_TILE_DMA>), grid, block, 0, st, a, method);
+        if (a.K == 0) hipLaunchKernelGGL((tile_kernel<4096, 0, false, kThreads>), grid, block, 0, st, a, method);
+        else if (a.K <= 24) hipLaunchKernelGGL((tile_kernel<4096, 2, true, kThreads>), grid, block, 0, st, a, method);
+        else if (a.K <= 60) hipLaunchKernelGGL((tile_kernel<4096, 4, true, kThreads>), grid, block, 0, st, a, method);
         else if (a.K <= 63) hipLaunchKernelGGL((tile_kernel<4096, 5, false, kThreads>), grid, block, 0, st, a, method);
         else return hipErrorInvalidValue;
     } else {

@@ -278,6 +278,10 @@ def test_autocorr_nan_and_constant(torch):
     rows = [np.full(100, 5.0), np.r_[np.full(50, 1.0), np.full(50, 3.0)], np.arange(100.0)]
     a = np.arange(100.0); a[40] = NaN; rows.append(a)
     b = np.arange(30.0); b[15] = NaN; rows.append(b[:30])   # short series: NaN only in the middle
+    # non-dyadic constants: the reference's rounded mean makes every diff the same d != 0, so
+    # it returns 1.0 (not NaN) -- sts_acf.hpp rule 3 takes its loop
+    rows += [np.full(100, 100.1), np.full(3000, 1234.567), np.full(20000, 0.3)]
+    c = np.full(5000, 100.1); c[-1] = 100.2; rows.append(c)   # constant but one end
     got = [host(uts.autocorr(dev(torch, r), K)) for r in rows]
     ref = [oracle.autocorr(r, K) for r in rows]
     for g, r in zip(got, ref):
@@ -438,17 +442,15 @@ def test_short_fill_acf(torch, monkeypatch, method, K):
         x[12, 22:200] = NaN                                   # run across several small blocks
         x[13, 1:] = NaN                                       # only x[0] (nearest: all NaN)
         x[14, 1:T // 2] = NaN; x[14, 0] = 5.0                 # nearest: x[0] is never an end
+        x[15] = 100.1; x[15, 3:T // 2] = NaN                  # constant at a non-dyadic level: the
+        #                                                       reference's rounded means give 1.0
         rf, racf, err = oracle.panel_fill_autocorr(x, method, K)
         got_f, got_a, got_e = run(_native.lib(), x, T)
         assert np.array_equal(got_e, err), (method, T, got_e, err)
         ok = err == 0
         assert_bits(got_f[ok], rf[ok], "fill %s T=%d K=%d" % (method, T, K))
-        # the ACF where it is defined: a lag slice of a filled series that is constant (row 10
-        # under previous / next / nearest) makes it 0 / 0, and the two-pass oracle's
-        # rounding of that 0 is not a value to match
-        posed = np.array([np.isnan(r).any() or all(np.ptp(r[i:]) > 0 and np.ptp(r[:T - i]) > 0
-                                                   for i in range(1, K + 1)) for r in rf])
-        ok = ok & posed
+        # every row, including the (near-)constant lag slices (rows 6, 10, 15: the reference's
+        # own two-pass values, taken by sts_acf.hpp rule 3)
         assert_rel(got_a[ok], racf[ok], what="acf %s T=%d K=%d" % (method, T, K))
         monkeypatch.setenv("STS_NO_SHORT", "1")
         seg_f, seg_a, seg_e = run(_native.load_variant(_native.AB_LIB_PATH), x, T)
