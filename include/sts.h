@@ -332,7 +332,9 @@ int sts_staging_release(void);
 int sts_staging_set_limit(int max_sets);
 /* Staging pool of the current device: out8 = {sets alive, idle, borrowed, limit, high-water
  * mark of sets alive, sets abandoned after a device error, calls that had to wait for a set,
- * device bytes per set}. */
+ * the bound on an idle set's device bytes (and, alike, its pinned bytes): 5 slots x (64 MB + the
+ * per-argument alignment).  A call whose ONE series exceeds a 64 MB chunk grows its set's slots
+ * for its own duration; the set is trimmed back to the bound when the call ends}. */
 int sts_staging_pool_info(int64_t* out8);
 /* Statistics of the calling thread's last _host call: out8 = {wall ms, H2D ms, kernel ms,
  * D2H ms (summed per-chunk event times on the staging streams; they overlap each other),

@@ -304,7 +304,10 @@ struct ArWaveLds {
 // round-2 form gave lane j row j and moved every column through v_readlane, LDS and a wave
 // barrier: ~13 k cycles per series of dependent broadcasts and LDS round trips, the largest
 // single phase after the block wait (tools/ar_stamps.py, profiles/r03_v7_ar_stamps.jsonl).
-// Same operations in the same order as the lane-parallel form (identical bits):
+// The same algebra as the lane-parallel form, but NOT its bits: centring multiplies by ifm = 1 / m
+// (cs_i cs_k ifm, not cs_i cs_k / m) and the solves multiply by reciprocal pivots; the fitted c / phi
+// agree with the reference within the fit's 1e-10 tolerance (tests/test_parity_gpu.py, the
+// refinement step absorbs the rounding difference), not bit for bit:
 //   A[i][k] (k <= i) = P_{i-k} - sum_{u < P-i} y_u y_{u+i-k} - sum_{v = P-i}^{P-1-(i-k)} t_v t_{v+i-k}
 // with y_u the head y(0..p-1) and t_v the tail y(T-p..T-1) (T >= 2p + 1: disjoint); column 0
 // is Y, rows / columns 1..p the lags; cs = the design's column sums; centring eliminates the

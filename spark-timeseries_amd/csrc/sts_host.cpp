@@ -54,6 +54,9 @@ constexpr int kSlots = STS_STAGE_SLOTS;
 constexpr size_t kChunkBytes = size_t(STS_STAGE_MB) << 20;   // device bytes (in + out) per chunk
 constexpr size_t kAlign = 256;
 constexpr int kDefaultSets = 4;                                // slot sets per device (sts_staging_set_limit)
+// what a slot keeps between calls: one chunk plus the per-argument alignment; a call whose single
+// series is larger than a chunk grows its slots for that call only (Borrow trims them again)
+constexpr size_t kSlotKeep = kChunkBytes + 16 * kAlign;
 
 size_t align_up(size_t b) { return (b + kAlign - 1) / kAlign * kAlign; }
 
@@ -143,6 +146,21 @@ struct Borrow {
             sl.busy = false;
             sl.copy_out = false;
         }
+        // a set goes back to the pool at its bound (kSlots x kSlotKeep of HBM and of pinned
+        // memory): buffers a one-series-larger-than-a-chunk call grew are freed here (drained above)
+        if (ok)
+            for (Slot& sl : set->slot) {
+                if (sl.dev_cap > kSlotKeep) {
+                    (void)hipFree(sl.dev);
+                    sl.dev = nullptr;
+                    sl.dev_cap = 0;
+                }
+                if (sl.pin_cap > kSlotKeep) {
+                    (void)hipHostFree(sl.pin);
+                    sl.pin = nullptr;
+                    sl.pin_cap = 0;
+                }
+            }
         if (ok) pool().give_back(dev, set);
         else pool().forget(dev);
     }
@@ -402,7 +420,7 @@ int sts_staging_pool_info(int64_t* out8) {
     if (e != hipSuccess) return hip_status(e, "hipGetDevice");
     const auto in = pool().info(dev);
     const int64_t v[8] = {in.live, in.idle, in.borrowed, in.cap, in.high, in.lost, in.waits,
-                          (int64_t)kSlots * (int64_t)kChunkBytes};
+                          (int64_t)kSlots * (int64_t)kSlotKeep};
     std::memcpy(out8, v, sizeof v);
     return STS_OK;
 }

@@ -120,7 +120,10 @@ void throw_for(JNIEnv* env, int status, jint nobs = 0, jint nvars = 0) {
     throw_string(env, g_rte, msg);
 }
 
-// ---- the calling thread's pinned buffers (grow-only; freed when the thread ends) ----
+// ---- the calling thread's pinned buffers: grown for a call, kept between calls only up to
+//      kPinKeep each (an executor thread holds at most 2 x kPinKeep of pinned memory while it
+//      lives; a larger partition's buffers are freed when its call ends), freed with the thread ----
+constexpr size_t kPinKeep = size_t(256) << 20;
 struct PinBuf {
     void* p = nullptr;
     size_t cap = 0;
@@ -134,11 +137,35 @@ struct PinBuf {
         }
         return static_cast<double*>(p);
     }
+    void trim() {
+        if (cap > kPinKeep) {
+            sts_host_free(p);
+            p = nullptr;
+            cap = 0;
+        }
+    }
     ~PinBuf() {
         if (p) sts_host_free(p);
     }
 };
 thread_local PinBuf t_in, t_out;
+
+// One call's panel buffer: the thread's pinned buffer, or -- when pinned memory cannot be had
+// -- the heap (the staging pipeline handles pageable memory too, at a lower PCIe rate).
+struct CallBuf {
+    PinBuf* pb;
+    std::vector<double> own;
+    double* p = nullptr;
+    CallBuf(PinBuf* b, int64_t count) : pb(b) {
+        const size_t n = (size_t)(count > 0 ? count : 1);
+        p = pb->get(n * sizeof(double));
+        if (!p) {
+            own.resize(n);
+            p = own.data();
+        }
+    }
+    ~CallBuf() { pb->trim(); }
+};
 
 bool check_len(JNIEnv* env, jarray a, int64_t need, const char* what) {
     if (!a) {
@@ -159,8 +186,10 @@ struct Region {
     jsize n;
     std::vector<double> own;
     double* p = nullptr;
+    PinBuf* pb_ = nullptr;
     // pinned: use the thread's pinned buffer `pb` (the panel); copy_in: read the array
-    Region(JNIEnv* e, jdoubleArray a, int64_t count, bool copy_in, PinBuf* pb = nullptr) : env(e), arr(a), n((jsize)count) {
+    Region(JNIEnv* e, jdoubleArray a, int64_t count, bool copy_in, PinBuf* pb = nullptr)
+        : env(e), arr(a), n((jsize)count), pb_(pb) {
         if (pb) p = pb->get((size_t)(count > 0 ? count : 1) * sizeof(double));
         if (!p) {
             own.resize((size_t)(count > 0 ? count : 1));
@@ -170,6 +199,9 @@ struct Region {
     }
     void copy_out() {
         if (n > 0 && !env->ExceptionCheck()) env->SetDoubleArrayRegion(arr, 0, n, p);
+    }
+    ~Region() {
+        if (pb_) pb_->trim();
     }
 };
 
@@ -543,9 +575,8 @@ JNIEXPORT jobjectArray JNICALL Java_com_cloudera_sparkts_StsNative_fillRecords(J
     const int code = method_code(env, method);
     if (code < 0) return nullptr;
     const int64_t n = prod(S, T);
-    double* in = t_in.get((size_t)(n > 0 ? n : 1) * sizeof(double));
-    double* out = t_out.get((size_t)(n > 0 ? n : 1) * sizeof(double));
-    if (!in || !out) return throw_for(env, STS_ERR_HIP), nullptr;
+    CallBuf bin(&t_in, n), bout(&t_out, n);
+    double *in = bin.p, *out = bout.p;
     if (!gather_records(env, recs, S, T, in)) return nullptr;
     const int st = sts_fill_host(in, out, S, T, T, code, nullptr);
     if (st != STS_OK) return throw_for(env, st), nullptr;
@@ -562,9 +593,8 @@ JNIEXPORT jobjectArray JNICALL Java_com_cloudera_sparkts_StsNative_fillDiffEwmaR
     if (!check_len(env, smoothing, S, "fillDiffEwmaRecords: smoothing array shorter than the record count"))
         return nullptr;
     const int64_t n = prod(S, T);
-    double* in = t_in.get((size_t)(n > 0 ? n : 1) * sizeof(double));
-    double* out = t_out.get((size_t)(n > 0 ? n : 1) * sizeof(double));
-    if (!in || !out) return throw_for(env, STS_ERR_HIP), nullptr;
+    CallBuf bin(&t_in, n), bout(&t_out, n);
+    double *in = bin.p, *out = bout.p;
     if (!gather_records(env, recs, S, T, in)) return nullptr;
     Region rs(env, smoothing, S, true);
     const int st = sts_fill_diff_ewma_host(in, out, S, T, T, code, lag, rs.p, nullptr);
@@ -583,9 +613,8 @@ JNIEXPORT jobjectArray JNICALL Java_com_cloudera_sparkts_StsNative_arFitRemoveRe
         !check_len(env, coef, prod(S, p), "arFitRemoveRecords: coefficient array shorter than S * maxLag"))
         return nullptr;
     const int64_t n = prod(S, T);
-    double* in = t_in.get((size_t)(n > 0 ? n : 1) * sizeof(double));
-    double* out = t_out.get((size_t)(n > 0 ? n : 1) * sizeof(double));
-    if (!in || !out) return throw_for(env, STS_ERR_HIP), nullptr;
+    CallBuf bin(&t_in, n), bout(&t_out, n);
+    double *in = bin.p, *out = bout.p;
     if (!gather_records(env, recs, S, T, in)) return nullptr;
     Region rc(env, c, S, false), rk(env, coef, prod(S, p), false);
     const int st = sts_ar_fit_remove_host(in, out, S, T, T, p, noIntercept ? 1 : 0, rc.p, rk.p, nullptr);

@@ -170,8 +170,7 @@ def timeSeriesRDDFromObservations(targetIndex, keys, timestamps, values, device=
     val_d = torch.as_tensor(np.asarray(values, dtype=np.float64), device=dev)
     check(_native.lib().sts_observations_to_panel(ptr(sid_d), ptr(loc_d), ptr(val_d), n, ptr(panel), S, T, T,
                                                   _stream(dev)), "timeSeriesRDDFromObservations")
-    rdd = TimeSeriesRDD(targetIndex, list(order), panel)
-    rdd.partitions = parts
+    rdd = TimeSeriesRDD(targetIndex, list(order), panel, partitions=parts)
     return rdd
 
 

@@ -25,15 +25,25 @@ def shard_range(n_series: int, rank: int, world: int):
 
 
 class TimeSeriesRDD:
-    def __init__(self, index, keys: Optional[Sequence[str]], data):
+    """A partition's panel: `data` (S, T), its `keys` (record order) and the shared `index`.
+    `partitions` (optional, one int per record) is the Spark partition each record lives in --
+    timeSeriesRDDFromObservations sets it (the reference's shuffle by key hash); every
+    transformation below keeps keys, order and partitions."""
+
+    def __init__(self, index, keys: Optional[Sequence[str]], data, partitions: Optional[Sequence[int]] = None):
         self.index = index
         self.data = data
         self.keys = list(keys) if keys is not None else None
+        self.partitions = list(partitions) if partitions is not None else None
+
+    def _derive(self, data, index=None) -> "TimeSeriesRDD":
+        """A transformed panel with the same keys, record order and partitions."""
+        return TimeSeriesRDD(self.index if index is None else index, self.keys, data, self.partitions)
 
     # --- S/TimeSeriesRDD.scala:180-182 ---
     def fill(self, method: str) -> "TimeSeriesRDD":
         """fill(method) == mapSeries(UnivariateTimeSeries.fillts(_, method))."""
-        return TimeSeriesRDD(self.index, self.keys, uts.fillts(self.data, method))
+        return self._derive(uts.fillts(self.data, method))
 
     # --- S/TimeSeriesRDD.scala:188-199 ---
     def mapSeries(self, f: Callable, index=None) -> "TimeSeriesRDD":
@@ -44,7 +54,7 @@ class TimeSeriesRDD:
         per series)."""
         from .pipelines import apply_per_series, is_batched
         out = f(self.data) if is_batched(f) else apply_per_series(f, self.data)
-        return TimeSeriesRDD(self.index if index is None else index, self.keys, out)
+        return self._derive(out, index)
 
     def autocorr(self, numLags: int):
         """rdd.mapValues(autocorr(_, numLags)) over the partition: (S, numLags)."""
@@ -62,7 +72,7 @@ class TimeSeriesRDD:
             raise TypeError("fillAndAutocorr runs on device-resident partitions (torch GPU tensors)")
         check(lib.sts_fill_autocorr(ptr(p.t), ptr(filled), p.S, p.T, p.ld, p.T, code, numLags, ptr(acf), None,
                                     p.stream), "fill_autocorr")
-        return TimeSeriesRDD(self.index, self.keys, filled), acf
+        return self._derive(filled), acf
 
     # --- S/TimeSeriesRDD.scala:204-206 ---
     def seriesStats(self) -> "StatCounters":
@@ -107,7 +117,7 @@ class TimeSeriesRDD:
                 index = kept.cpu().numpy()
         else:
             index = kept.cpu().numpy()
-        return TimeSeriesRDD(index, self.keys, p.out(out))
+        return self._derive(p.out(out), index)
 
     # --- S/TimeSeriesRDD.scala:215-324 ---
     def toInstants(self, group=None):

@@ -8,17 +8,28 @@ the oracle.
 import os
 import sys
 
+import pytest
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 for p in (ROOT, os.path.join(ROOT, "oracle"), os.path.join(ROOT, "spark-timeseries_amd")):
     if p not in sys.path:
         sys.path.insert(0, p)
 
 
+def pytest_addoption(parser):
+    # tools/ab_variants.sh: the parity gate of an A/B variant library must run THAT library (the
+    # package itself reads no environment variable, so the selection is an explicit option)
+    parser.addoption("--sts-lib", default=None, help="run the tests against this build of libsts_hip.so")
+
+
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (HIP device) and libsts_hip.so")
-
-
-import pytest  # noqa: E402
+    path = config.getoption("--sts-lib")
+    if path:
+        if not os.path.exists(path):
+            raise pytest.UsageError("--sts-lib %s: no such library" % path)
+        from sparkts import _native
+        _native.use_library(path)
 
 
 @pytest.fixture

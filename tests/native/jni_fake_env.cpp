@@ -15,6 +15,7 @@
 
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <string>
@@ -170,6 +171,12 @@ int sts_fill_method_from_name(const char* name) {
     return -2;
 }
 int sts_host_alloc(size_t bytes, void** out) {
+    // JNI_FAKE_NO_PIN=1: pinned memory cannot be had (the shim must fall back to the heap)
+    const char* nopin = std::getenv("JNI_FAKE_NO_PIN");
+    if (nopin && nopin[0] == '1') {
+        *out = nullptr;
+        return STS_ERR_HIP;
+    }
     *out = std::malloc(bytes ? bytes : 16);
     return *out ? STS_OK : STS_ERR_HIP;
 }

@@ -112,3 +112,24 @@ def test_indexed_row_matrix_needs_uniform_index():
     assert not _is_uniform(irregular)
     with pytest.raises(UnsupportedOperationException, match="only supported for uniform indices"):
         TimeSeriesRDD(irregular, None, np.zeros((2, 3))).toIndexedRowMatrix()
+
+
+def test_sts_lib_option_runs_the_named_build(tmp_path):
+    """tools/ab_variants.sh gates each variant library on the parity tests with --sts-lib (the
+    package reads no environment variable): the option must load THAT build, and a missing
+    build must stop the run instead of silently testing the product library."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    ab = os.path.join(root, "spark-timeseries_amd", "build", "libsts_hip_ab.so")
+    probe = tmp_path / "test_probe.py"
+    probe.write_text("def test_probe():\n    from sparkts import _native\n    print('LIB=' + _native.lib()._name)\n")
+    conf = tmp_path / "conftest.py"
+    conf.write_text(open(os.path.join(root, "tests", "conftest.py")).read().replace(
+        "ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))", "ROOT = %r" % root))
+    run = lambda lib: subprocess.run([sys.executable, "-m", "pytest", str(probe), "-q", "-s", "-p", "no:cacheprovider",
+                                      "--sts-lib", lib], capture_output=True, text=True, cwd=str(tmp_path))
+    r = run(ab)
+    assert r.returncode == 0 and ("LIB=" + ab) in r.stdout, r.stdout + r.stderr
+    r = run(str(tmp_path / "missing.so"))
+    assert r.returncode != 0 and "no such library" in (r.stdout + r.stderr)

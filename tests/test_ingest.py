@@ -109,3 +109,17 @@ def test_observation_record_order_matches_the_reference_with_partitions():
     order, _ = sio.observation_key_order(["￿", "\U0001F600", "a"], 1)
     assert order == ["a", "\U0001F600", "￿"]
     assert sorted(["￿", "\U0001F600", "a"]) == ["a", "￿", "\U0001F600"]
+
+
+def test_partitions_are_declared_and_carried_through_transformations():
+    """TimeSeriesRDD declares `partitions` (None unless the ingest set it) and every
+    transformation keeps it with the keys and the record order."""
+    from sparkts import TimeSeriesRDD
+    x = np.arange(12.0).reshape(3, 4)
+    plain = TimeSeriesRDD(None, ["a", "b", "c"], x)
+    assert plain.partitions is None and plain.mapSeries(lambda v: v * 2.0).partitions is None
+    rdd = TimeSeriesRDD(None, ["a", "b", "c"], x, partitions=[0, 0, 1])
+    out = rdd.mapSeries(lambda v: v + 1.0)
+    assert out.partitions == [0, 0, 1] and out.keys == ["a", "b", "c"]
+    assert np.array_equal(np.asarray(out.data), x + 1.0)
+    assert out.mapSeries(lambda v: v, index=range(4)).partitions == [0, 0, 1]
