@@ -34,6 +34,7 @@
 #include "sts_internal.hpp"
 #include "sts_acf.hpp"
 #include "sts_scan.hpp"
+#include "sts_dma.hpp"
 
 #include <hip/hip_runtime.h>
 
@@ -44,6 +45,14 @@
 // middle sums in the y pass, the no-MFMA / no-operand diagnostics and the I8 Ozaki cost models)
 // are not in this source: their records are in DESIGN.md §5.2 / profiles/INDEX.md and their code
 // at commit bd59bf8 (tools/var_rev.sh builds a library from any revision for same-box A/B).
+
+#ifndef STS_TILE_PERSIST
+#define STS_TILE_PERSIST 0   // A/B build flag: tiles per chunk of the persistent sweep (0: off)
+#endif
+
+#ifndef STS_TILE_DMA
+#define STS_TILE_DMA 0    // A/B build flag: K <= 60 on 2048-step tiles whose next tile streams in by LDS-DMA
+#endif
 
 #ifndef STS_TILE_WGS
 #define STS_TILE_WGS 4    // workgroups per CU the register budget is sized for (128 VGPRs; LDS 40.5 KB x 4 fits)
@@ -63,6 +72,7 @@ __device__ __forceinline__ void lds_barrier() {
 }
 
 typedef double d4 __attribute__((ext_vector_type(4)));
+typedef double d2v __attribute__((ext_vector_type(2)));   // 16-B non-temporal stores
 
 constexpr int kThreads = 256;
 constexpr int kBig = 1 << 30;
@@ -178,8 +188,15 @@ __device__ __forceinline__ int px2_(int q2) { return PAD ? q2 + ((q2 >> 4) << 1)
 // + j%q -- every lag 0 .. 16 NT - q exactly once per step, and the same lag map h(j) - i in
 // every accumulator; TOEPLITZ (K = 61..63) uses NT = floor((K + 15) / 16) + 1 MFMAs with
 // U_t holding lag 16t + j - i.
-template <int TW, int NT, bool SHIFTED, int NTH>
+// DMA: the next interior tile streams by LDS-DMA into a raw staging image from the start of the
+// current one (the whole tile's time in flight, no prefetch registers held across phases); it
+// takes TW = 2048 for four 4-wave workgroups per CU (vals 20 KB + staging 18 KB).
+// PERSIST: gridDim.x resident workgroups sweep the chunks with stride gridDim.x (so that at any
+// time they work on neighbouring chunks: a dense sweep of the panel, as a grid-stride copy makes),
+// each prefetching its next chunk's first tile under the current chunk's last MFMA phase.
+template <int TW, int NT, bool SHIFTED, int NTH, bool DMA = false, bool PERSIST = false>
 __global__ __launch_bounds__(NTH, STS_TILE_WGS) void tile_kernel(TileArgs a, int method) {
+    static_assert(!(DMA && PERSIST), "one prefetch scheme");
     constexpr int kThreads = NTH;          // 256 (4 waves) or 128 (2 waves, TW = 2048)
     constexpr int kWaves = NTH / 64;
     static_assert(TW / 64 % kWaves == 0, "whole 64-step chunks per wave");
@@ -202,6 +219,8 @@ __global__ __launch_bounds__(NTH, STS_TILE_WGS) void tile_kernel(TileArgs a, int
     constexpr int RPT = (NP2 + kThreads - 1) / kThreads;     // prefetch registers per thread
     static_assert(EW % 64 == 0, "extended tile must be whole words");
     static_assert(NW <= 128, "word scan handles at most 128 words");
+    constexpr int NDMA = (NP2 + 63) / 64;                    // DMA: 1-KB pieces per extended tile
+    __shared__ __attribute__((aligned(16))) double stg_mem[DMA ? NDMA * 128 : 2];
     // padded (px) for the shifted scheme
     __shared__ __attribute__((aligned(16))) double vals[EWP];
     __shared__ unsigned long long mask[NW];
@@ -223,54 +242,65 @@ __global__ __launch_bounds__(NTH, STS_TILE_WGS) void tile_kernel(TileArgs a, int
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform: scalar loop control
-    // one workgroup = one CHUNK of tiles_per_chunk consecutive tiles of one series
+    // one workgroup = one CHUNK of tiles_per_chunk consecutive tiles of one series (PERSIST: the
+    // chunks ch, ch + G, ch + 2G, ...)
     const int64_t nchunk = a.S * a.chunks_per_series;
-    const int64_t ch = xcd_remap(blockIdx.x, nchunk);
-    const int64_t s = ch / a.chunks_per_series;
-    const int64_t cidx = ch - s * a.chunks_per_series;
-    const int64_t k_begin = cidx * a.tiles_per_chunk;
-    const int64_t k_end = (k_begin + a.tiles_per_chunk < a.tiles_per_series) ? k_begin + a.tiles_per_chunk
-                                                                              : a.tiles_per_series;
+    const int64_t G = PERSIST ? (int64_t)gridDim.x : nchunk;
+    int64_t ch = xcd_remap(blockIdx.x, G);
     const int64_t T = a.T;
-    const double* src = a.in + s * a.ld_in;
-    const bool src_al = (reinterpret_cast<uintptr_t>(src) & 15) == 0;
     const bool needL = (method == STS_FILL_LINEAR || method == STS_FILL_PREVIOUS || method == STS_FILL_NEAREST);
     const bool needN = (method == STS_FILL_LINEAR || method == STS_FILL_NEXT || method == STS_FILL_NEAREST);
-    double* dst = a.out ? a.out + s * a.ld_out : nullptr;
     const int64_t lrows = T - a.max_lag;
     const int ncols = a.max_lag + (a.include_original ? 1 : 0);
     const int init = a.include_original ? 0 : 1;
-
-    if (tid < 2) {
-        carry_L[tid] = -1;
-        carry_t[tid] = -kBig;   // matches no tile start
-    }
-    if (tid == 0) {
-        sh_c[0] = -kBig;
-        sh_c[2] = -1;
-    }
-    double acc_s = 0.0, acc_q = 0.0;   // sum y, sum y^2 over this thread's middle positions
+    // PERSIST: the row of chunk c's series and its first tile kk when that tile is interior (else
+    // null: the tile is loaded with bounds checks when it starts)
+    auto chunk_first = [&](int64_t c, int64_t& kk) -> const double* {
+        const int64_t ss = c / a.chunks_per_series;
+        kk = (c - ss * a.chunks_per_series) * a.tiles_per_chunk;
+        const double* p = a.in + ss * a.ld_in;
+        const int64_t e0 = kk * TW - kHB;
+        return (e0 >= 0 && e0 + EW <= T && (reinterpret_cast<uintptr_t>(p) & 15) == 0) ? p : nullptr;
+    };
 
     // register prefetch of one INTERIOR extended tile [e0, e0 + EW); the first and last tile
     // of a series (which touch its ends) are loaded synchronously with bounds checks
     static_assert(RPT <= 9, "prefetch registers are spelled out for RPT <= 9");
     double2 R0, R1, R2, R3, R4, R5, R6, R7, R8;   // named: an array here ends up in scratch
-    auto interior = [&](int64_t kk) {
-        const int64_t e0 = kk * TW - kHB;
-        return e0 >= 0 && e0 + EW <= T && src_al;
-    };
     // (a macro, not a lambda: a captured register array would be forced to scratch)
 #define STS_LD1(j)                                                                          \
     if constexpr (j < RPT) {                                                                \
         const int q2_ = tid + j * kThreads;                                                 \
         R##j = s2_[q2_ < NP2 ? q2_ : NP2 - 1];                                              \
     }
-#define STS_ISSUE(kk)                                                                       \
+// DMA: wave w issues the 1-KB pieces m = w, w + kWaves, ... of interior tile kk into the
+// staging image (lanes past the tile read its first double2 into the image's tail)
+#define STS_DMA_ISSUE(kk)                                                                   \
     do {                                                                                    \
-        const double2* s2_ = reinterpret_cast<const double2*>(src + ((kk) * TW - kHB));     \
+        const double* s0_ = src + ((kk) * TW - kHB);                                        \
+        for (int m_ = wave; m_ < NDMA; m_ += kWaves) {                                      \
+            const int q2_ = m_ * 64 + lane;                                                 \
+            glds16(s0_ + 2 * (q2_ < NP2 ? q2_ : 0), lds_addr(stg_mem) + (unsigned)(m_ << 10)); \
+        }                                                                                   \
+    } while (0)
+#define STS_TK1(j)                                                                          \
+    if constexpr (j < RPT) {                                                                \
+        const int q2_ = tid + j * kThreads;                                                 \
+        R##j = g2_[q2_ < NP2 ? q2_ : NP2 - 1];                                              \
+    }
+#define STS_DMA_TAKE()                                                                      \
+    do {                                                                                    \
+        const double2* g2_ = reinterpret_cast<const double2*>(stg_mem);                     \
+        STS_TK1(0) STS_TK1(1) STS_TK1(2) STS_TK1(3) STS_TK1(4)                              \
+        STS_TK1(5) STS_TK1(6) STS_TK1(7) STS_TK1(8)                                         \
+    } while (0)
+#define STS_ISSUE_AT(p, kk)                                                                 \
+    do {                                                                                    \
+        const double2* s2_ = reinterpret_cast<const double2*>((p) + ((kk) * TW - kHB));     \
         STS_LD1(0) STS_LD1(1) STS_LD1(2) STS_LD1(3) STS_LD1(4)                              \
         STS_LD1(5) STS_LD1(6) STS_LD1(7) STS_LD1(8)                                         \
     } while (0)
+#define STS_ISSUE(kk) STS_ISSUE_AT(src, kk)
 // define R on the no-prefetch path too, so the registers are dead between their store to
 // LDS and the next issue (otherwise the loop-carried values stay live across the body).  An
 // empty asm that "writes" them defines them with no instruction (round 3: the zeroing moves
@@ -289,6 +319,36 @@ __global__ __launch_bounds__(NTH, STS_TILE_WGS) void tile_kernel(TileArgs a, int
         if ((j + 1) * kThreads <= NP2 || q2_ < NP2) v2_[pst_ + j * PX2S] = R##j;            \
     }
 
+    bool have = false;
+    if constexpr (PERSIST) {   // the first chunk's first tile
+        int64_t kk;
+        const double* p = chunk_first(ch, kk);
+        have = p != nullptr;
+        if (have) STS_ISSUE_AT(p, kk);
+        else STS_CLEAR();
+    }
+    for (;;) {   // the chunks of this workgroup (one unless PERSIST)
+    const int64_t s = ch / a.chunks_per_series;
+    const int64_t cidx = ch - s * a.chunks_per_series;
+    const int64_t k_begin = cidx * a.tiles_per_chunk;
+    const int64_t k_end = (k_begin + a.tiles_per_chunk < a.tiles_per_series) ? k_begin + a.tiles_per_chunk
+                                                                              : a.tiles_per_series;
+    const double* src = a.in + s * a.ld_in;
+    const bool src_al = (reinterpret_cast<uintptr_t>(src) & 15) == 0;
+    double* dst = a.out ? a.out + s * a.ld_out : nullptr;
+    auto interior = [&](int64_t kk) {
+        const int64_t e0 = kk * TW - kHB;
+        return e0 >= 0 && e0 + EW <= T && src_al;
+    };
+    if (tid < 2) {
+        carry_L[tid] = -1;
+        carry_t[tid] = -kBig;   // matches no tile start
+    }
+    if (tid == 0) {
+        sh_c[0] = -kBig;
+        sh_c[2] = -1;
+    }
+    double acc_s = 0.0, acc_q = 0.0;   // sum y, sum y^2 over this thread's middle positions
     d4 U[NA];
 #pragma unroll
     for (int t = 0; t < NA; t++) U[t] = d4{0.0, 0.0, 0.0, 0.0};
@@ -297,9 +357,16 @@ __global__ __launch_bounds__(NTH, STS_TILE_WGS) void tile_kernel(TileArgs a, int
     unsigned long long st_acc[12] = {0};
     unsigned long long st_prev = __builtin_amdgcn_s_memtime();
 #endif
-    bool have = interior(k_begin);
-    if (have) STS_ISSUE(k_begin);
-    else STS_CLEAR();
+    if constexpr (!PERSIST) {
+        have = interior(k_begin);
+        if constexpr (DMA) {
+            if (have) STS_DMA_ISSUE(k_begin);
+            STS_CLEAR();
+        } else {
+            if (have) STS_ISSUE(k_begin);
+            else STS_CLEAR();
+        }
+    }
     // ACF shift (sts_acf.hpp: median of 64 raw samples of the series), computed once per
     // series by acf_shift_kernel before this launch: a scalar load
     // (made wave-uniform in SGPRs here: a VGPR load result used inside the tile loop gets a
@@ -421,6 +488,12 @@ __global__ __launch_bounds__(NTH, STS_TILE_WGS) void tile_kernel(TileArgs a, int
         //      wave v holds steps 128v + 512j + 2*lane (+1), i.e. words 2v + 8j and 2v + 8j + 1
         //      as an even/odd bit interleave ----
         if (have) {
+            if constexpr (DMA) {
+                // every wave's pieces have landed (own DMA waited, then the barrier for the others)
+                dma_wait();
+                lds_barrier();
+                STS_DMA_TAKE();
+            }
             double2* v2_ = reinterpret_cast<double2*>(vals);
             const int pst_ = opq(px2(tid));   // px2(tid + j kThreads) = px2(tid) + j PX2S
             STS_ST1(0) STS_ST1(1) STS_ST1(2) STS_ST1(3) STS_ST1(4) STS_ST1(5) STS_ST1(6) STS_ST1(7) STS_ST1(8)
@@ -453,10 +526,24 @@ __global__ __launch_bounds__(NTH, STS_TILE_WGS) void tile_kernel(TileArgs a, int
                 vals[px(q)] = (t >= 0 && t < T) ? src[t] : __builtin_nan("");
             }
         }
-        const bool have_next = (k + 1 < k_end) && interior(k + 1);
+        // the next tile of this chunk, or (PERSIST) the first tile of the next chunk
+        const double* nsrc = src;
+        int64_t nk = k + 1;
+        bool have_next = false;
+        if (k + 1 < k_end) {
+            have_next = interior(k + 1);
+        } else if constexpr (PERSIST) {
+            nsrc = (ch + G < nchunk) ? chunk_first(ch + G, nk) : nullptr;
+            have_next = nsrc != nullptr;
+        }
         STAMP(0);
         lds_barrier();
         STAMP(1);
+        // DMA: the staging image is free again (every thread read its pieces before the
+        // barrier): the next tile streams in during this whole tile
+        if constexpr (DMA) {
+            if (have_next) STS_DMA_ISSUE(k + 1);
+        }
 
         // positions to produce: [qA, qB) (E-relative); the ACF needs REACH steps past the tile
         const int qA = kHB;
@@ -707,8 +794,7 @@ __global__ __launch_bounds__(NTH, STS_TILE_WGS) void tile_kernel(TileArgs a, int
             // fast path: a full tile not at the series end -- the written range is exactly
             // [kHB, kHB + TW) and every y the MFMA phase reads is F - c0 (no zero tail), so
             // every index and guard below is a compile-time constant
-            const bool fast = (dst == nullptr || al) && !a.lagmat && (t1 - t0 == TW) &&
-                              (NT == 0 || e0 + qW + REACH <= T);
+            const bool fast = (dst == nullptr || al) && (t1 - t0 == TW) && (NT == 0 || e0 + qW + REACH <= T);
             if (fast) {
                 constexpr int FS = TW / 2 / kThreads;                          // stored double2
                 constexpr int FY = NT > 0 ? (NP2 - kHB / 2 + kThreads - 1) / kThreads : FS;
@@ -764,15 +850,6 @@ __global__ __launch_bounds__(NTH, STS_TILE_WGS) void tile_kernel(TileArgs a, int
                             if (q + 1 < qW) dst[t + 1] = f.y;
                         }
                     }
-                    if (a.lagmat) {
-                        double* lm = a.lagmat + s * lrows * ncols;
-                        for (int c = init; c <= a.max_lag; c++) {
-                            double* col = lm + (int64_t)(c - init) * lrows;
-                            const int64_t r0 = (int64_t)t - a.max_lag + c;
-                            if (r0 >= 0 && r0 < lrows) col[r0] = f.x;
-                            if (q + 1 < qW && r0 + 1 >= 0 && r0 + 1 < lrows) col[r0 + 1] = f.y;
-                        }
-                    }
                 }
                 if (NT > 0 && q < qBfull) {
                     f.x = (q < qB) ? f.x - c0 : 0.0;
@@ -784,8 +861,41 @@ __global__ __launch_bounds__(NTH, STS_TILE_WGS) void tile_kernel(TileArgs a, int
             // the look-back range as y = 0
             if (SHIFTED && NT > 0 && e0 < 0 && tid < kHB / 2) v2[px2(tid)] = make_double2(0.0, 0.0);
         }
-        if (have_next) STS_ISSUE(k + 1);   // in flight during the MFMA phase of tile k
-        else STS_CLEAR();
+        if constexpr (DMA) {
+            STS_CLEAR();
+        } else {
+            if (have_next) STS_ISSUE_AT(nsrc, nk);   // in flight during the MFMA phase of tile k
+            else STS_CLEAR();
+        }
+        // lag matrix (fill only; S/Lag.scala:62-77): column c - init holds x[r + max_lag - c] at
+        // row r.  Each column's rows of this tile go out as 16-B pairs aligned on the column's
+        // own address (one wave instruction = 1 KB of one column; round 3 stored the two halves
+        // of every pair with separate 8-B stores), non-temporal (the matrix is not re-read
+        // here); the pair straddling the tile's first / last row is stored per element.
+        if constexpr (NT == 0) {
+            if (a.lagmat) {
+                double* lm = a.lagmat + s * lrows * ncols;
+                for (int c = init; c <= a.max_lag; c++) {
+                    double* col = lm + (int64_t)(c - init) * lrows;
+                    const int sh = a.max_lag - c;
+                    const int rlo = t0 - sh > 0 ? t0 - sh : 0;
+                    const int rhi = (int64_t)(t1 - sh) < lrows ? t1 - sh : (int)lrows;
+                    if (rlo >= rhi) continue;
+                    const int par = (int)((reinterpret_cast<uintptr_t>(col) >> 3) & 1);   // col + r 16-B aligned iff r + par even
+                    const int rp = rlo - ((rlo + par) & 1);
+                    for (int r = rp + 2 * tid; r < rhi; r += 2 * kThreads) {
+                        const int q = r + sh - e0;
+                        if (r >= rlo && r + 1 < rhi) {
+                            const d2v v = {vals[px(q)], vals[px(q + 1)]};
+                            __builtin_nontemporal_store(v, reinterpret_cast<d2v*>(col + r));
+                        } else {
+                            if (r >= rlo) col[r] = vals[px(q)];
+                            if (r + 1 < rhi) col[r + 1] = vals[px(q + 1)];
+                        }
+                    }
+                }
+            }
+        }
         STAMP(8);
 
         if constexpr (NT > 0) {
@@ -800,6 +910,10 @@ __global__ __launch_bounds__(NTH, STS_TILE_WGS) void tile_kernel(TileArgs a, int
         STAMP(11);
     }
 #undef STS_ISSUE
+#undef STS_ISSUE_AT
+#undef STS_DMA_ISSUE
+#undef STS_DMA_TAKE
+#undef STS_TK1
 #undef STS_LD1
 #undef STS_ST1
 #undef STS_CLEAR
@@ -872,6 +986,14 @@ __global__ __launch_bounds__(NTH, STS_TILE_WGS) void tile_kernel(TileArgs a, int
             }
         }
     }
+    if constexpr (!PERSIST) {
+        break;
+    } else {
+        ch += G;
+        if (ch >= nchunk) break;
+        lds_barrier();   // vals (the diagonal scratch) and the word tables are reused
+    }
+    }   // chunk loop
 }
 
 // One wave per series: combine the chunk partials in chunk order (deterministic) and form
@@ -946,6 +1068,25 @@ hipError_t launch_tile(int method, int tw, const TileArgs& a, hipStream_t st) {
     } else if (tw == 2048 && a.K > 0 && a.K <= 60) {   // 2-wave workgroups (A/B build: STS_TILE_W=2048)
         if (a.K <= 24) hipLaunchKernelGGL((tile_kernel<2048, 2, true, kThreads / 2>), grid, dim3(kThreads / 2), 0, st, a, method);
         else hipLaunchKernelGGL((tile_kernel<2048, 4, true, kThreads / 2>), grid, dim3(kThreads / 2), 0, st, a, method);
+#endif
+#if STS_TILE_PERSIST
+    } else if (tw == 4096 && a.K <= 60) {   // variant build: resident workgroups sweep the chunks
+        static int ncu = 0;
+        if (ncu <= 0) {
+            int dev = 0, v = 0;
+            if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0) v = 256;
+            ncu = v;
+        }
+        const int64_t g = nchunk < 4 * ncu ? nchunk : 4 * ncu;
+        dim3 pg((unsigned)g);
+        if (a.K == 0) hipLaunchKernelGGL((tile_kernel<4096, 0, false, kThreads, false, true>), pg, block, 0, st, a, method);
+        else if (a.K <= 24) hipLaunchKernelGGL((tile_kernel<4096, 2, true, kThreads, false, true>), pg, block, 0, st, a, method);
+        else hipLaunchKernelGGL((tile_kernel<4096, 4, true, kThreads, false, true>), pg, block, 0, st, a, method);
+#endif
+#if STS_TILE_DMA
+    } else if (tw == 2048 && a.K > 0 && a.K <= 60) {   // variant build: LDS-DMA prefetch, 4-wave workgroups
+        if (a.K <= 24) hipLaunchKernelGGL((tile_kernel<2048, 2, true, kThreads, true>), grid, block, 0, st, a, method);
+        else hipLaunchKernelGGL((tile_kernel<2048, 4, true, kThreads, true>), grid, block, 0, st, a, method);
 #endif
     } else if (tw == 4096) {
         if (a.K == 0) hipLaunchKernelGGL((tile_kernel<4096, 0, false, kThreads>), grid, block, 0, st, a, method);

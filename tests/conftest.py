@@ -28,6 +28,9 @@ def pytest_configure(config):
     if path:
         if not os.path.exists(path):
             raise pytest.UsageError("--sts-lib %s: no such library" % path)
+        # torch first: it loads the HIP runtime the library must bind to (a library loaded
+        # before it pulls /opt/rocm's runtime in, and sts_init then sees no device)
+        import torch  # noqa: F401
         from sparkts import _native
         _native.use_library(path)
 

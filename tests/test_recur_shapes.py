@@ -141,3 +141,31 @@ def test_recur_fill_diff_ewma(torch, S, T, lag):
         d = oracle.differences_at_lag(f, lag)
         ref.append(oracle.ewma_add(d, v))
     assert_bits(host(out, T), np.array(ref), "fill_diff_ewma")
+
+
+# Row-contiguous panels (ld == T, T even, 8+ series per 75-KB batch) take rows_kernel: whole-row
+# batches by LDS-DMA, double-buffered, one persistent workgroup per CU.  Batch edges (S not a
+# multiple of the batch, odd S: the smoothing piece's dword clamp), the smallest / largest rows it
+# takes (T = 2, T = 1200: 8 series per batch) and the first row it does not (T = 1202), and more
+# batches than workgroups (S = 20 000 at T = 390: 834 batches over <= 256 CUs).
+@pytest.mark.parametrize("S,T", [(1, 2), (5, 2), (300, 390), (301, 390), (24, 390), (25, 390), (17, 1200),
+                                 (9, 1202), (20_000, 390), (777, 64)])
+@pytest.mark.parametrize("lag", [1, 8])
+def test_recur_fill_diff_ewma_rows(torch, S, T, lag):
+    from sparkts import _native
+    lib = _native.lib()
+    rng = np.random.default_rng(7 * S + T + lag)
+    x = 100 + rng.standard_normal((S, T)).cumsum(axis=1)
+    x[rng.random((S, T)) < 0.1] = NaN
+    x[0, : min(T, 5)] = NaN
+    if S > 3:
+        x[3, :] = NaN
+    s = rng.uniform(0.05, 0.95, S)             # a different smoothing per series
+    xd = torch.as_tensor(x, device="cuda:0")
+    out = torch.full_like(xd, 7.0)
+    assert lib.sts_fill_diff_ewma(xd.data_ptr(), out.data_ptr(), S, T, T, T, 3, lag,
+                                  dvec(torch, s).data_ptr(), None, None) == 0
+    ref = []
+    for r, v in zip(x, s):
+        ref.append(oracle.ewma_add(oracle.differences_at_lag(oracle.fill_previous(r), lag), v))
+    assert_bits(out.cpu().numpy(), np.array(ref), "fill_diff_ewma rows")
