@@ -154,14 +154,15 @@ struct RecurLane {
 template <int OP, int H, int SPW = 64, int CH = 32, bool V2 = false>
 __global__ __launch_bounds__(64) void recur_kernel(RecurArgs a) {
     // V2: 16-B loads / stores (two consecutive steps per lane, half the memory instructions);
-    // rows padded to an even stride so the 16-B LDS accesses stay aligned
-    constexpr int kRow = V2 ? CH + 2 : CH + 1;
+    // rows padded to an even stride so the 16-B LDS accesses stay aligned, and = 2 mod 4
+    // doubles so the 16 lanes' per-row 8-B reads hit distinct bank pairs.  (Round 4: 130-step
+    // chunks -- three for C2's 390 steps instead of 3 x 128 + 6 -- ran 2.14 against 1.43 ms:
+    // a 130-step row does not fill whole 128-double load instructions, so every instruction
+    // then spans two rows; profiles/r04_v4_ab_c2.jsonl.)
+    constexpr int kRow = V2 ? (CH % 4 == 2 ? CH : CH + 2) : CH + 1;
     constexpr int EPL = V2 ? 2 : 1;               // elements per lane per instruction
-    // load instructions per chunk per lane (the last one partial when SPW x CH is not a
-    // multiple of the wave's 64 x EPL elements: CH = 130, three chunks for C2's 390 steps)
-    constexpr int NLD = (SPW * CH + 64 * EPL - 1) / (64 * EPL);
-    constexpr bool PART = SPW * CH % (64 * EPL) != 0;
-    static_assert((V2 ? CH % 2 == 0 : (CH % 64 == 0 || 64 % CH == 0)), "chunk shape");
+    constexpr int NLD = SPW * CH / (64 * EPL);    // load instructions per chunk per lane
+    static_assert(SPW * CH % (64 * EPL) == 0 && (V2 ? CH % 2 == 0 : (CH % 64 == 0 || 64 % CH == 0)), "chunk shape");
     __shared__ __attribute__((aligned(16))) double tile[SPW * kRow];
     const int lane = threadIdx.x;
     const int64_t s0 = (int64_t)blockIdx.x * SPW;
@@ -181,7 +182,6 @@ __global__ __launch_bounds__(64) void recur_kernel(RecurArgs a) {
         for (int i = 0; i < NLD; i++) {
             const int e = (i * 64 + lane) * EPL;
             const int row = e / CH, col = e % CH;
-            if (PART && i == NLD - 1 && row >= SPW) continue;
             const double* src = a.in + (s0 + row) * a.ld_in + tc + col;
             if (V2) {
                 if (row < ns && col + 1 < len) {
@@ -202,7 +202,6 @@ __global__ __launch_bounds__(64) void recur_kernel(RecurArgs a) {
         for (int i = 0; i < NLD; i++) {
             const int e = (i * 64 + lane) * EPL;
             const int row = e / CH, col = e % CH;
-            if (PART && i == NLD - 1 && row >= SPW) continue;
             if (V2) {
                 if (row < ns && col < len) *reinterpret_cast<double2*>(&tile[row * kRow + col]) = pre[i];
             } else {
@@ -220,7 +219,6 @@ __global__ __launch_bounds__(64) void recur_kernel(RecurArgs a) {
         for (int i = 0; i < NLD; i++) {
             const int e = (i * 64 + lane) * EPL;
             const int row = e / CH, col = e % CH;
-            if (PART && i == NLD - 1 && row >= SPW) continue;
             double* d = a.out + (s0 + row) * a.ld_out + tc + col;
             if (V2) {
                 if (row < ns && col + 1 < len) *reinterpret_cast<double2*>(d) = *reinterpret_cast<const double2*>(&tile[row * kRow + col]);
@@ -463,15 +461,6 @@ hipError_t launch_h(const RecurArgs& a, int need, hipStream_t st) {
 #endif
     if (need <= 8 && rows16(a)) {   // the C2 shape: 16 series x 128-step chunks, 16-B accesses
         dim3 g((unsigned)((a.S + kSpw - 1) / kSpw)), b(64);
-        // 130-step chunks where they need fewer chunks than 128 (C2's 390 steps: 3 instead of
-        // 3 x 128 + a 6-step fourth chunk that costs a whole load / barrier / store round)
-        if (kCh == 128 && (a.T + 129) / 130 < (a.T + 127) / 128) {
-            if (need <= 1) hipLaunchKernelGGL((recur_kernel<OP, 1, kSpw, 130, true>), g, b, 0, st, a);
-            else if (need <= 2) hipLaunchKernelGGL((recur_kernel<OP, 2, kSpw, 130, true>), g, b, 0, st, a);
-            else if (need <= 4) hipLaunchKernelGGL((recur_kernel<OP, 4, kSpw, 130, true>), g, b, 0, st, a);
-            else hipLaunchKernelGGL((recur_kernel<OP, 8, kSpw, 130, true>), g, b, 0, st, a);
-            return hipGetLastError();
-        }
         if (need <= 1) hipLaunchKernelGGL((recur_kernel<OP, 1, kSpw, kCh, true>), g, b, 0, st, a);
         else if (need <= 2) hipLaunchKernelGGL((recur_kernel<OP, 2, kSpw, kCh, true>), g, b, 0, st, a);
         else if (need <= 4) hipLaunchKernelGGL((recur_kernel<OP, 4, kSpw, kCh, true>), g, b, 0, st, a);
