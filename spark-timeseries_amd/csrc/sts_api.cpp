@@ -191,16 +191,7 @@ int run_tile(const double* in, double* out, double* lagmat, int64_t S, int64_t T
     const bool seg = seg_ok && (force ? !std::strcmp(force, "seg") : T <= 16384);
     // STS_TILE_W=2048: 2-wave workgroups on 2048-step tiles for K <= 60 (A/B build only)
     const char* tw_env = (!seg && K > 0 && K <= 60 && !lagmat) ? sts::ab_knob("STS_TILE_W") : nullptr;
-#ifndef STS_TILE_DMA
-#define STS_TILE_DMA 0
-#endif
-#if STS_TILE_DMA
-    // variant build (tools/variant.sh ... -DSTS_TILE_DMA=1): 2048-step tiles with the LDS-DMA prefetch
-    const int tw = seg ? sts::kSegW : (K > 0 && K <= 60 && !lagmat) ? 2048 : (K > 0) ? 4096 : tile_width(T);
-    (void)tw_env;
-#else
     const int tw = seg ? sts::kSegW : (K > 0) ? (tw_env && std::atoi(tw_env) == 2048 ? 2048 : 4096) : tile_width(T);
-#endif
     sts::TileArgs a{};
     a.in = in;
     a.out = out;
@@ -216,13 +207,7 @@ int run_tile(const double* in, double* out, double* lagmat, int64_t S, int64_t T
     // STS_TILES_PER_CHUNK: tiles per tile-kernel workgroup, for A/B runs only
     const char* tpc_env = seg ? nullptr : sts::ab_knob("STS_TILES_PER_CHUNK");
     const int seg_knob = seg_env ? std::atoi(seg_env) : 0, tpc_knob = tpc_env ? std::atoi(tpc_env) : 0;
-#ifndef STS_TILE_PERSIST
-#define STS_TILE_PERSIST 0
-#endif
-    const int64_t per_chunk = seg ? (seg_knob > 0 ? seg_knob : sts::kSegTiles)
-                                  : (tpc_knob > 0 ? tpc_knob
-                                     : (STS_TILE_PERSIST && tw == 4096 && K <= 60) ? STS_TILE_PERSIST
-                                     : kTilesPerChunk * (STS_TILE_DMA && tw == 2048 ? 2 : 1));
+    const int64_t per_chunk = seg ? (seg_knob > 0 ? seg_knob : sts::kSegTiles) : (tpc_knob > 0 ? tpc_knob : kTilesPerChunk);
     a.tiles_per_chunk = a.tiles_per_series < per_chunk ? a.tiles_per_series : per_chunk;
     a.chunks_per_series = (a.tiles_per_series + a.tiles_per_chunk - 1) / a.tiles_per_chunk;
     a.K = K;

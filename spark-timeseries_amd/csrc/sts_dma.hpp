@@ -28,16 +28,6 @@ __device__ __forceinline__ void glds16(const double* gsrc, unsigned lds_byte_add
                  : "memory");
 }
 
-// The 4-B form (global_load_lds_dword): 64 lanes x 4 B -> LDS [lds_addr, lds_addr + 256 B).
-__device__ __forceinline__ void glds4(const unsigned* gsrc, unsigned lds_byte_addr) {
-    unsigned keep;
-    lds_byte_addr = __builtin_amdgcn_readfirstlane(lds_byte_addr);
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
-                 : "=&s"(keep)
-                 : "v"(gsrc), "s"(lds_byte_addr)
-                 : "memory");
-}
-
 __device__ __forceinline__ void dma_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
 // order this wave's LDS accesses (no workgroup barrier: the buffers are per wave)

@@ -16,7 +16,6 @@
 // shape (1M series x 390 steps): 64-step row segments beat 32 (1.68 vs 1.98 ms) and 128
 // (2.86 ms); the series count per wave (16 / 32 / 64) hardly matters.
 #include "sts_internal.hpp"
-#include "sts_dma.hpp"
 
 #include <hip/hip_runtime.h>
 
@@ -74,21 +73,6 @@ struct RecurLane {
     }
     __device__ __forceinline__ void init(const RecurArgs& a, int64_t sl, bool live) {
         load(a, sl, live);
-        finish(a);
-    }
-    // EWMA ops with the smoothing value already at hand (rows_kernel: from LDS, so that no
-    // vector-memory load -- and no vmcnt wait behind the in-flight DMA -- sits in its loop)
-    __device__ __forceinline__ void init_sm(const RecurArgs& a, double smv) {
-        carry = __builtin_nan("");
-        hp = a.lag;
-        start = (OP == kFillDiffEwma) ? a.lag : a.start;
-        e = 0.0;
-#pragma unroll
-        for (int j = 0; j < H; j++) {
-            cf[j] = 0.0;
-            h[j] = 0.0;
-        }
-        sm = smv;
         finish(a);
     }
     // STEADY: t >= steady_from() (every t-guard below is then a constant; same operations)
@@ -154,12 +138,11 @@ struct RecurLane {
 template <int OP, int H, int SPW = 64, int CH = 32, bool V2 = false>
 __global__ __launch_bounds__(64) void recur_kernel(RecurArgs a) {
     // V2: 16-B loads / stores (two consecutive steps per lane, half the memory instructions);
-    // rows padded to an even stride so the 16-B LDS accesses stay aligned, and = 2 mod 4
-    // doubles so the 16 lanes' per-row 8-B reads hit distinct bank pairs.  (Round 4: 130-step
-    // chunks -- three for C2's 390 steps instead of 3 x 128 + 6 -- ran 2.14 against 1.43 ms:
-    // a 130-step row does not fill whole 128-double load instructions, so every instruction
-    // then spans two rows; profiles/r04_v4_ab_c2.jsonl.)
-    constexpr int kRow = V2 ? (CH % 4 == 2 ? CH : CH + 2) : CH + 1;
+    // rows padded to an even stride so the 16-B LDS accesses stay aligned
+    // (round 4: 130-step chunks -- three for C2's 390 steps instead of 3 x 128 + 6 -- ran 2.14
+    // against 1.43 ms: a 130-step row does not fill whole 128-double load instructions, so every
+    // instruction then spans two rows; profiles/r04_v4_ab_c2.jsonl)
+    constexpr int kRow = V2 ? CH + 2 : CH + 1;
     constexpr int EPL = V2 ? 2 : 1;               // elements per lane per instruction
     constexpr int NLD = SPW * CH / (64 * EPL);    // load instructions per chunk per lane
     static_assert(SPW * CH % (64 * EPL) == 0 && (V2 ? CH % 2 == 0 : (CH % 64 == 0 || 64 % CH == 0)), "chunk shape");
@@ -231,175 +214,6 @@ __global__ __launch_bounds__(64) void recur_kernel(RecurArgs a) {
     }
 }
 
-// Whole-row batches for panels stored row after row (ld == T): a batch of NS series is one
-// contiguous span of the panel, so it moves in address order -- LDS-DMA in, 16-B stores out,
-// every row read and written whole (the DRAM-page pattern of a straight copy; the chunk kernel
-// above reads each row in ~1-KB pieces at different times).  One persistent 4-wave workgroup
-// per CU double-buffers the batches in LDS: batch i+1 streams in while lanes 0..NS-1 of waves
-// 0 and 1 run their series' recurrence over batch i in place and all four waves then store it.
-// Every wave issues the same number of DMA pieces (kRowPcsW) and stores (kRowStW) per batch --
-// tail lanes re-store the batch's last pair with its own bytes and tail pieces re-read
-// in-bounds data into unused LDS -- so the wait for batch i is a constant vmcnt: the younger
-// stores of batch i-1 and the pieces of batch i+1 stay in flight.  The last piece carries the
-// batch's smoothing values (4-B DMA), so the loop holds no vector-memory load hipcc would wait
-// for with a vmcnt(0) (that would also wait for the DMA in flight).
-constexpr int kRowPcsW = 19;                       // DMA pieces (1 KB) per wave per batch
-constexpr int kRowBufD = 4 * kRowPcsW * 128;       // doubles per buffer (76 KB): two fit one CU's LDS
-constexpr int kRowSpan = kRowBufD - 128;           // panel part of a buffer; the last piece holds sm
-constexpr int kRowStW = kRowSpan / 2 / 256 + 1;    // 16-B store rounds per thread per batch (19)
-static_assert(kRowStW * 512 >= kRowSpan, "store rounds cover the span");
-static_assert(kRowPcsW + kRowStW <= 63, "vmcnt field");
-
-template <int N>
-__device__ __forceinline__ void vm_wait() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
-
-template <int OP, int H>
-__global__ __launch_bounds__(256, 1) void rows_kernel(RecurArgs a, int NS, int64_t nb) {
-    __shared__ __attribute__((aligned(16))) double buf[2 * kRowBufD];
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int64_t T = a.T;
-    const int64_t last2 = a.S * T - 2;             // last in-bounds 16-B pair of the panel
-    const int64_t G = gridDim.x;
-    auto dma = [&](int64_t b, int slot) {          // batch b -> buffer slot (kRowPcsW pieces per wave)
-        const double* src = a.in + b * NS * T;
-        const int64_t room = last2 - b * NS * T;   // clamp: tail pieces re-read in-bounds bytes
-        const unsigned base = lds_addr(buf + slot * kRowBufD);
-#pragma unroll 1
-        for (int j = 0; j < kRowPcsW; j++) {
-            const int m = wave * kRowPcsW + j;
-            if (m == 4 * kRowPcsW - 1) {
-                // the last piece: smoothing of the batch's series (dwords 0 .. 2 NS - 1)
-                const int64_t d = b * NS * 2 + (lane < 2 * NS ? lane : 0);
-                const int64_t dl = 2 * a.S - 1;
-                glds4(reinterpret_cast<const unsigned*>(a.sm) + (d < dl ? d : dl), base + (unsigned)(kRowSpan * 8));
-            } else {
-                int64_t q = (int64_t)m * 128 + 2 * lane;
-                q = q < room ? q : room;
-                glds16(src + q, base + (unsigned)(m << 10));
-            }
-        }
-    };
-    int64_t b = blockIdx.x;
-    if (b >= nb) return;
-    dma(b, 0);
-    bool next_issued = b + G < nb;
-    if (next_issued) dma(b + G, 1);
-    for (int it = 0; b < nb; it++, b += G) {
-        const int slot = it & 1;
-        // batch b has landed: younger are this wave's stores of the previous batch (it > 0) and
-        // the pieces of batch b + G (if issued)
-        if (it > 0) {
-            if (next_issued) vm_wait<kRowStW + kRowPcsW>();
-            else vm_wait<kRowStW>();
-        } else {
-            if (next_issued) vm_wait<kRowPcsW>();
-            else vm_wait<0>();
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-        __builtin_amdgcn_s_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-        const int nsb = (int)((a.S - b * NS < NS) ? a.S - b * NS : NS);   // series in this batch
-        double* bb = buf + slot * kRowBufD;
-        // recurrence: series j of the batch on lane j / 3 of wave j % 3 (waves 0..2: each step is a
-        // dependent FP64 chain, so three waves on three SIMDs instead of one); the row moves
-        // through registers 16 steps at a time, the next 16 read before the current ones run
-        // (an LDS round trip per step cost ~100 cycles: 2.98 against 1.42 ms on C2)
-        if (wave < 3) {
-            const int j = lane * 3 + wave;
-            if (j < nsb) {
-                RecurLane<OP, H> rl;
-                rl.init_sm(a, bb[kRowSpan + j]);
-                double2* row = reinterpret_cast<double2*>(bb + (int64_t)j * T);
-                const int np = (int)(T >> 1);          // pairs (T even)
-                const int nblk = np >> 3;
-                double2 cur[8];
-                if (nblk > 0) {
-#pragma unroll
-                    for (int i = 0; i < 8; i++) cur[i] = row[i];
-                }
-                for (int bk = 0; bk < nblk; bk++) {
-                    double2 nxt[8];
-                    const bool more = bk + 1 < nblk;
-                    if (more) {
-#pragma unroll
-                        for (int i = 0; i < 8; i++) nxt[i] = row[(bk + 1) * 8 + i];
-                    }
-                    const int64_t t0 = (int64_t)bk * 16;
-                    if (bk == 0) {   // steady_from() <= 8 (H, lag <= 8)
-#pragma unroll
-                        for (int i = 0; i < 8; i++) {
-                            cur[i].x = rl.step(cur[i].x, t0 + 2 * i);
-                            cur[i].y = rl.step(cur[i].y, t0 + 2 * i + 1);
-                        }
-                    } else {
-#pragma unroll
-                        for (int i = 0; i < 8; i++) {
-                            cur[i].x = rl.template step<true>(cur[i].x, t0 + 2 * i);
-                            cur[i].y = rl.template step<true>(cur[i].y, t0 + 2 * i + 1);
-                        }
-                    }
-#pragma unroll
-                    for (int i = 0; i < 8; i++) row[bk * 8 + i] = cur[i];
-                    if (more) {
-#pragma unroll
-                        for (int i = 0; i < 8; i++) cur[i] = nxt[i];
-                    }
-                }
-                for (int p2 = nblk * 8; p2 < np; p2++) {
-                    double2 v = row[p2];
-                    v.x = rl.step(v.x, 2 * (int64_t)p2);
-                    v.y = rl.step(v.y, 2 * (int64_t)p2 + 1);
-                    row[p2] = v;
-                }
-            }
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-        __builtin_amdgcn_s_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-        // store the batch: kRowStW 16-B rounds per thread, tail lanes repeat the last pair
-        {
-            const int64_t np = (int64_t)nsb * T / 2;
-            double2* dst = reinterpret_cast<double2*>(a.out + b * NS * T);
-            const double2* src2 = reinterpret_cast<const double2*>(bb);
-#pragma unroll
-            for (int r = 0; r < kRowStW; r++) {
-                int64_t p = (int64_t)r * 256 + tid;
-                p = p < np ? p : np - 1;
-                dst[p] = src2[p];
-            }
-        }
-        // every LDS read of this slot is done before any wave refills it
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-        __builtin_amdgcn_s_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-        next_issued = b + 2 * G < nb;
-        if (next_issued) dma(b + 2 * G, slot);
-    }
-}
-
-// rows_kernel applies: a row-contiguous 16-B aligned panel (ld == T, T even) of rows short
-// enough for 8+ series per batch
-inline int rows_ns(const RecurArgs& a) {
-    if (a.ld_in != a.T || a.ld_out != a.T || (a.T & 1) || a.T < 2) return 0;
-    if (((reinterpret_cast<uintptr_t>(a.in) | reinterpret_cast<uintptr_t>(a.out)) & 15) != 0) return 0;
-    int64_t ns = kRowSpan / a.T;
-    if (ns > 32) ns = 32;                    // the smoothing piece holds 64 dwords (and 3 x 11 lanes compute)
-    return ns >= 8 ? (int)ns : 0;
-}
-
-inline int cu_count() {
-    static int n[64] = {0};
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
-    if (n[dev] <= 0) {
-        int v = 0;
-        if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0) v = 256;
-        n[dev] = v;
-    }
-    return n[dev];
-}
-
 // Fallbacks for histories longer than 32 steps (correct, not tuned):
 // in-place differencing decomposes into `lag` independent chains t = r, r+lag, ...
 __global__ __launch_bounds__(256) void diff_chain_kernel(double* x, int64_t S, int64_t T, int64_t ld, int lag,
@@ -443,22 +257,6 @@ inline bool rows16(const RecurArgs& a) {
 
 template <int OP>
 hipError_t launch_h(const RecurArgs& a, int need, hipStream_t st) {
-#ifdef STS_ROWS
-    // the fused C2 pipeline on row-contiguous panels: whole-row batches (rows_kernel)
-    if constexpr (OP == kFillDiffEwma) if (need <= 8) {
-        const int ns = rows_ns(a);
-        if (ns > 0) {
-            const int64_t nb = (a.S + ns - 1) / ns;
-            const int64_t g = nb < cu_count() ? nb : cu_count();
-            dim3 grid((unsigned)g), block(256);
-            if (need <= 1) hipLaunchKernelGGL((rows_kernel<OP, 1>), grid, block, 0, st, a, ns, nb);
-            else if (need <= 2) hipLaunchKernelGGL((rows_kernel<OP, 2>), grid, block, 0, st, a, ns, nb);
-            else if (need <= 4) hipLaunchKernelGGL((rows_kernel<OP, 4>), grid, block, 0, st, a, ns, nb);
-            else hipLaunchKernelGGL((rows_kernel<OP, 8>), grid, block, 0, st, a, ns, nb);
-            return hipGetLastError();
-        }
-    }
-#endif
     if (need <= 8 && rows16(a)) {   // the C2 shape: 16 series x 128-step chunks, 16-B accesses
         dim3 g((unsigned)((a.S + kSpw - 1) / kSpw)), b(64);
         if (need <= 1) hipLaunchKernelGGL((recur_kernel<OP, 1, kSpw, kCh, true>), g, b, 0, st, a);

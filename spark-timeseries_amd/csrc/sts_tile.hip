@@ -34,7 +34,6 @@
 #include "sts_internal.hpp"
 #include "sts_acf.hpp"
 #include "sts_scan.hpp"
-#include "sts_dma.hpp"
 
 #include <hip/hip_runtime.h>
 
@@ -45,18 +44,6 @@
 // middle sums in the y pass, the no-MFMA / no-operand diagnostics and the I8 Ozaki cost models)
 // are not in this source: their records are in DESIGN.md §5.2 / profiles/INDEX.md and their code
 // at commit bd59bf8 (tools/var_rev.sh builds a library from any revision for same-box A/B).
-
-#ifndef STS_TILE_WSCAN
-#define STS_TILE_WSCAN 0   // A/B build flag: per-wave word ranges, scans and NaN lists (no wave-0 scan phase)
-#endif
-
-#ifndef STS_TILE_PERSIST
-#define STS_TILE_PERSIST 0   // A/B build flag: tiles per chunk of the persistent sweep (0: off)
-#endif
-
-#ifndef STS_TILE_DMA
-#define STS_TILE_DMA 0    // A/B build flag: K <= 60 on 2048-step tiles whose next tile streams in by LDS-DMA
-#endif
 
 #ifndef STS_TILE_WGS
 #define STS_TILE_WGS 4    // workgroups per CU the register budget is sized for (128 VGPRs; LDS 40.5 KB x 4 fits)
@@ -146,47 +133,35 @@ __device__ __forceinline__ int dpp(int old, int v) {
 __device__ __forceinline__ int rl(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
 __device__ __forceinline__ int imax(int a, int b) { return a > b ? a : b; }
 __device__ __forceinline__ int imin(int a, int b) { return a < b ? a : b; }
-// inclusive prefix max over lanes 0..lane; *all = the wave's max.  The wave totals come from
-// the row-local scans' readlanes: hipcc (ROCm 7.2) folded a readlane at lane 63 of the
-// combined result to the row-local value, dropping the carry from the rows below it.
-__device__ __forceinline__ int wave_prefix_max(int v, int lane, int* all = nullptr) {
+// inclusive prefix max over lanes 0..lane
+__device__ __forceinline__ int wave_prefix_max(int v, int lane) {
     constexpr int I = -0x7fffffff - 1;
     v = imax(v, dpp<0x111>(I, v));
     v = imax(v, dpp<0x112>(I, v));
     v = imax(v, dpp<0x114>(I, v));
     v = imax(v, dpp<0x118>(I, v));
     const int p1 = rl(v, 15), p2 = imax(p1, rl(v, 31)), p3 = imax(p2, rl(v, 47));
-    if (all) *all = imax(p3, rl(v, 63));
     const int r = opq(lane) >> 4;   // opaque: the row masks are recomputed per use, not hoisted into spilled SGPRs
     return imax(v, r == 0 ? I : r == 1 ? p1 : r == 2 ? p2 : p3);
 }
-// inclusive prefix sum over lanes 0..lane; *all = the wave's sum; rows (if given) = the
-// row-local sums and the carries into rows 1..3, for uniform lookups of single lanes
-__device__ __forceinline__ int wave_prefix_sum(int v, int lane, int* all = nullptr, int* rows = nullptr) {
+// inclusive prefix sum over lanes 0..lane
+__device__ __forceinline__ int wave_prefix_sum(int v, int lane) {
     v += dpp<0x111>(0, v);
     v += dpp<0x112>(0, v);
     v += dpp<0x114>(0, v);
     v += dpp<0x118>(0, v);
     const int p1 = rl(v, 15), p2 = p1 + rl(v, 31), p3 = p2 + rl(v, 47);
-    if (all) *all = p3 + rl(v, 63);
-    if (rows) {
-        rows[0] = v;
-        rows[1] = p1;
-        rows[2] = p2;
-        rows[3] = p3;
-    }
     const int r = opq(lane) >> 4;   // opaque: the row masks are recomputed per use, not hoisted into spilled SGPRs
     return v + (r == 0 ? 0 : r == 1 ? p1 : r == 2 ? p2 : p3);
 }
-// inclusive suffix min over lanes lane..63; *all = the wave's min
-__device__ __forceinline__ int wave_suffix_min(int v, int lane, int* all = nullptr) {
+// inclusive suffix min over lanes lane..63
+__device__ __forceinline__ int wave_suffix_min(int v, int lane) {
     constexpr int I = 0x7fffffff;
     v = imin(v, dpp<0x101>(I, v));
     v = imin(v, dpp<0x102>(I, v));
     v = imin(v, dpp<0x104>(I, v));
     v = imin(v, dpp<0x108>(I, v));
     const int s3 = rl(v, 48), s2 = imin(s3, rl(v, 32)), s1 = imin(s2, rl(v, 16));
-    if (all) *all = imin(s1, rl(v, 0));
     const int r = opq(lane) >> 4;   // opaque: the row masks are recomputed per use, not hoisted into spilled SGPRs
     return imin(v, r == 0 ? s1 : r == 1 ? s2 : r == 2 ? s3 : I);
 }
@@ -204,15 +179,12 @@ __device__ __forceinline__ int px2_(int q2) { return PAD ? q2 + ((q2 >> 4) << 1)
 // + j%q -- every lag 0 .. 16 NT - q exactly once per step, and the same lag map h(j) - i in
 // every accumulator; TOEPLITZ (K = 61..63) uses NT = floor((K + 15) / 16) + 1 MFMAs with
 // U_t holding lag 16t + j - i.
-// DMA: the next interior tile streams by LDS-DMA into a raw staging image from the start of the
-// current one (the whole tile's time in flight, no prefetch registers held across phases); it
-// takes TW = 2048 for four 4-wave workgroups per CU (vals 20 KB + staging 18 KB).
-// PERSIST: gridDim.x resident workgroups sweep the chunks with stride gridDim.x (so that at any
-// time they work on neighbouring chunks: a dense sweep of the panel, as a grid-stride copy makes),
-// each prefetching its next chunk's first tile under the current chunk's last MFMA phase.
-template <int TW, int NT, bool SHIFTED, int NTH, bool DMA = false, bool PERSIST = false>
-__global__ __launch_bounds__(NTH, NTH == 128 ? 2 * STS_TILE_WGS : STS_TILE_WGS) void tile_kernel(TileArgs a, int method) {
-    static_assert(!(DMA && PERSIST), "one prefetch scheme");
+// M: the fill method (STS_FILL_*), a template parameter (round 4: as a kernel argument its tests
+// were hoisted out of the tile loop as masks and spilled; compile-time, every method-dependent
+// branch folds away)
+template <int TW, int NT, bool SHIFTED, int NTH, int M>
+__global__ __launch_bounds__(NTH, STS_TILE_WGS) void tile_kernel(TileArgs a) {
+    constexpr int method = M;
     constexpr int kThreads = NTH;          // 256 (4 waves) or 128 (2 waves, TW = 2048)
     constexpr int kWaves = NTH / 64;
     static_assert(TW / 64 % kWaves == 0, "whole 64-step chunks per wave");
@@ -235,8 +207,6 @@ __global__ __launch_bounds__(NTH, NTH == 128 ? 2 * STS_TILE_WGS : STS_TILE_WGS) 
     constexpr int RPT = (NP2 + kThreads - 1) / kThreads;     // prefetch registers per thread
     static_assert(EW % 64 == 0, "extended tile must be whole words");
     static_assert(NW <= 128, "word scan handles at most 128 words");
-    constexpr int NDMA = (NP2 + 63) / 64;                    // DMA: 1-KB pieces per extended tile
-    __shared__ __attribute__((aligned(16))) double stg_mem[DMA ? NDMA * 128 : 2];
     // padded (px) for the shifted scheme
     __shared__ __attribute__((aligned(16))) double vals[EWP];
     __shared__ unsigned long long mask[NW];
@@ -254,87 +224,58 @@ __global__ __launch_bounds__(NTH, NTH == 128 ? 2 * STS_TILE_WGS : STS_TILE_WGS) 
     // live across tiles for them): the last valid index before sh_c[0] is sh_c[1]; the first
     // valid index at or after sh_c[2] is sh_c[3]
     __shared__ int sh_c[4];
-#if STS_TILE_WSCAN
-    // WSCAN: wave v owns words [v WPW, (v + 1) WPW): it scans them in registers and imputes
-    // their NaNs; the waves exchange only a summary each (last / first valid position, long-run
-    // flag).  lastBefore / firstAfter: the last valid E-position before word w / the first after
-    // it (written and read by the owning wave only).  sc: the global-scan caches, double-buffered
-    // by tile parity (several waves may read and write them in one phase).
-    constexpr int WPW = 2 * RPT;
-    static_assert(kWaves * WPW >= NW && WPW <= 64, "per-wave word ranges cover the tile");
-    __shared__ int lastBefore[NW], firstAfter[NW];
-    __shared__ int wsum[3][kWaves];
-    __shared__ int sc[2][4];
-#endif
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform: scalar loop control
-    // one workgroup = one CHUNK of tiles_per_chunk consecutive tiles of one series (PERSIST: the
-    // chunks ch, ch + G, ch + 2G, ...)
+    // one workgroup = one CHUNK of tiles_per_chunk consecutive tiles of one series
     const int64_t nchunk = a.S * a.chunks_per_series;
-    const int64_t G = PERSIST ? (int64_t)gridDim.x : nchunk;
-    int64_t ch = xcd_remap(blockIdx.x, G);
+    const int64_t ch = xcd_remap(blockIdx.x, nchunk);
+    const int64_t s = ch / a.chunks_per_series;
+    const int64_t cidx = ch - s * a.chunks_per_series;
+    const int64_t k_begin = cidx * a.tiles_per_chunk;
+    const int64_t k_end = (k_begin + a.tiles_per_chunk < a.tiles_per_series) ? k_begin + a.tiles_per_chunk
+                                                                              : a.tiles_per_series;
     const int64_t T = a.T;
-    const bool needL = (method == STS_FILL_LINEAR || method == STS_FILL_PREVIOUS || method == STS_FILL_NEAREST);
-    const bool needN = (method == STS_FILL_LINEAR || method == STS_FILL_NEXT || method == STS_FILL_NEAREST);
+    const double* src = a.in + s * a.ld_in;
+    const bool src_al = (reinterpret_cast<uintptr_t>(src) & 15) == 0;
+    constexpr bool needL = (method == STS_FILL_LINEAR || method == STS_FILL_PREVIOUS || method == STS_FILL_NEAREST);
+    constexpr bool needN = (method == STS_FILL_LINEAR || method == STS_FILL_NEXT || method == STS_FILL_NEAREST);
+    double* dst = a.out ? a.out + s * a.ld_out : nullptr;
     const int64_t lrows = T - a.max_lag;
     const int ncols = a.max_lag + (a.include_original ? 1 : 0);
     const int init = a.include_original ? 0 : 1;
-    // PERSIST: the row of chunk c's series and its first tile kk when that tile is interior (else
-    // null: the tile is loaded with bounds checks when it starts)
-    auto chunk_first = [&](int64_t c, int64_t& kk) -> const double* {
-        const int64_t ss = c / a.chunks_per_series;
-        kk = (c - ss * a.chunks_per_series) * a.tiles_per_chunk;
-        const double* p = a.in + ss * a.ld_in;
-        const int64_t e0 = kk * TW - kHB;
-        return (e0 >= 0 && e0 + EW <= T && (reinterpret_cast<uintptr_t>(p) & 15) == 0) ? p : nullptr;
-    };
+
+    if (tid < 2) {
+        carry_L[tid] = -1;
+        carry_t[tid] = -kBig;   // matches no tile start
+    }
+    if (tid == 0) {
+        sh_c[0] = -kBig;
+        sh_c[2] = -1;
+    }
+    double acc_s = 0.0, acc_q = 0.0;   // sum y, sum y^2 over this thread's middle positions
 
     // register prefetch of one INTERIOR extended tile [e0, e0 + EW); the first and last tile
     // of a series (which touch its ends) are loaded synchronously with bounds checks
     static_assert(RPT <= 9, "prefetch registers are spelled out for RPT <= 9");
     double2 R0, R1, R2, R3, R4, R5, R6, R7, R8;   // named: an array here ends up in scratch
+    auto interior = [&](int64_t kk) {
+        const int64_t e0 = kk * TW - kHB;
+        return e0 >= 0 && e0 + EW <= T && src_al;
+    };
     // (a macro, not a lambda: a captured register array would be forced to scratch)
-#if STS_TILE_WSCAN
-    // WSCAN: register j of wave v holds double2 v 64 RPT + 64 j + lane (wave v's own range)
-#define STS_Q2(j) (wave * (64 * RPT) + 64 * (j) + lane)
-#else
-#define STS_Q2(j) (tid + (j) * kThreads)
-#endif
 #define STS_LD1(j)                                                                          \
     if constexpr (j < RPT) {                                                                \
-        const int q2_ = STS_Q2(j);                                                          \
+        const int q2_ = tid + j * kThreads;                                                 \
         R##j = s2_[q2_ < NP2 ? q2_ : NP2 - 1];                                              \
     }
-// DMA: wave w issues the 1-KB pieces m = w, w + kWaves, ... of interior tile kk into the
-// staging image (lanes past the tile read its first double2 into the image's tail)
-#define STS_DMA_ISSUE(kk)                                                                   \
+#define STS_ISSUE(kk)                                                                       \
     do {                                                                                    \
-        const double* s0_ = src + ((kk) * TW - kHB);                                        \
-        for (int m_ = wave; m_ < NDMA; m_ += kWaves) {                                      \
-            const int q2_ = m_ * 64 + lane;                                                 \
-            glds16(s0_ + 2 * (q2_ < NP2 ? q2_ : 0), lds_addr(stg_mem) + (unsigned)(m_ << 10)); \
-        }                                                                                   \
-    } while (0)
-#define STS_TK1(j)                                                                          \
-    if constexpr (j < RPT) {                                                                \
-        const int q2_ = STS_Q2(j);                                                          \
-        R##j = g2_[q2_ < NP2 ? q2_ : NP2 - 1];                                              \
-    }
-#define STS_DMA_TAKE()                                                                      \
-    do {                                                                                    \
-        const double2* g2_ = reinterpret_cast<const double2*>(stg_mem);                     \
-        STS_TK1(0) STS_TK1(1) STS_TK1(2) STS_TK1(3) STS_TK1(4)                              \
-        STS_TK1(5) STS_TK1(6) STS_TK1(7) STS_TK1(8)                                         \
-    } while (0)
-#define STS_ISSUE_AT(p, kk)                                                                 \
-    do {                                                                                    \
-        const double2* s2_ = reinterpret_cast<const double2*>((p) + ((kk) * TW - kHB));     \
+        const double2* s2_ = reinterpret_cast<const double2*>(src + ((kk) * TW - kHB));     \
         STS_LD1(0) STS_LD1(1) STS_LD1(2) STS_LD1(3) STS_LD1(4)                              \
         STS_LD1(5) STS_LD1(6) STS_LD1(7) STS_LD1(8)                                         \
     } while (0)
-#define STS_ISSUE(kk) STS_ISSUE_AT(src, kk)
 // define R on the no-prefetch path too, so the registers are dead between their store to
 // LDS and the next issue (otherwise the loop-carried values stay live across the body).  An
 // empty asm that "writes" them defines them with no instruction (round 3: the zeroing moves
@@ -347,65 +288,12 @@ __global__ __launch_bounds__(NTH, NTH == 128 ? 2 * STS_TILE_WGS : STS_TILE_WGS) 
     } while (0)
 // (the bound test only where it can fail: a runtime test on every register kept a spilled
 // exec mask per register alive across the tile loop)
-#if STS_TILE_WSCAN
-    // (registers below the last wave's first partial one are in range for every wave)
-#define STS_ST1(j)                                                                          \
-    if constexpr (j < RPT) {                                                                \
-        const int q2_ = STS_Q2(j);                                                          \
-        if ((kWaves - 1) * 64 * RPT + (j + 1) * 64 <= NP2 || q2_ < NP2)                     \
-            v2_[pst_ + j * (PAD ? 72 : 64)] = R##j;                                         \
-    }
-#define STS_EDGE1(j)                                                                        \
-    if constexpr (j < RPT) {                                                                \
-        const int q2_ = STS_Q2(j);                                                          \
-        const int t_ = e0 + 2 * q2_;                                                        \
-        R##j.x = (q2_ < NP2 && t_ >= 0 && t_ < T) ? src[t_] : __builtin_nan("");            \
-        R##j.y = (q2_ < NP2 && t_ + 1 >= 0 && t_ + 1 < T) ? src[t_ + 1] : __builtin_nan(""); \
-    }
-#else
 #define STS_ST1(j)                                                                          \
     if constexpr (j < RPT) {                                                                \
         const int q2_ = tid + j * kThreads;                                                 \
         if ((j + 1) * kThreads <= NP2 || q2_ < NP2) v2_[pst_ + j * PX2S] = R##j;            \
     }
-#endif
 
-    bool have = false;
-    if constexpr (PERSIST) {   // the first chunk's first tile
-        int64_t kk;
-        const double* p = chunk_first(ch, kk);
-        have = p != nullptr;
-        if (have) STS_ISSUE_AT(p, kk);
-        else STS_CLEAR();
-    }
-    for (;;) {   // the chunks of this workgroup (one unless PERSIST)
-    const int64_t s = ch / a.chunks_per_series;
-    const int64_t cidx = ch - s * a.chunks_per_series;
-    const int64_t k_begin = cidx * a.tiles_per_chunk;
-    const int64_t k_end = (k_begin + a.tiles_per_chunk < a.tiles_per_series) ? k_begin + a.tiles_per_chunk
-                                                                              : a.tiles_per_series;
-    const double* src = a.in + s * a.ld_in;
-    const bool src_al = (reinterpret_cast<uintptr_t>(src) & 15) == 0;
-    double* dst = a.out ? a.out + s * a.ld_out : nullptr;
-    auto interior = [&](int64_t kk) {
-        const int64_t e0 = kk * TW - kHB;
-        return e0 >= 0 && e0 + EW <= T && src_al;
-    };
-    if (tid < 2) {
-        carry_L[tid] = -1;
-        carry_t[tid] = -kBig;   // matches no tile start
-    }
-    if (tid == 0) {
-        sh_c[0] = -kBig;
-        sh_c[2] = -1;
-    }
-#if STS_TILE_WSCAN
-    if (tid < 2) {
-        sc[tid][0] = -kBig;
-        sc[tid][2] = -1;
-    }
-#endif
-    double acc_s = 0.0, acc_q = 0.0;   // sum y, sum y^2 over this thread's middle positions
     d4 U[NA];
 #pragma unroll
     for (int t = 0; t < NA; t++) U[t] = d4{0.0, 0.0, 0.0, 0.0};
@@ -414,16 +302,9 @@ __global__ __launch_bounds__(NTH, NTH == 128 ? 2 * STS_TILE_WGS : STS_TILE_WGS) 
     unsigned long long st_acc[12] = {0};
     unsigned long long st_prev = __builtin_amdgcn_s_memtime();
 #endif
-    if constexpr (!PERSIST) {
-        have = interior(k_begin);
-        if constexpr (DMA) {
-            if (have) STS_DMA_ISSUE(k_begin);
-            STS_CLEAR();
-        } else {
-            if (have) STS_ISSUE(k_begin);
-            else STS_CLEAR();
-        }
-    }
+    bool have = interior(k_begin);
+    if (have) STS_ISSUE(k_begin);
+    else STS_CLEAR();
     // ACF shift (sts_acf.hpp: median of 64 raw samples of the series), computed once per
     // series by acf_shift_kernel before this launch: a scalar load
     // (made wave-uniform in SGPRs here: a VGPR load result used inside the tile loop gets a
@@ -540,279 +421,11 @@ __global__ __launch_bounds__(NTH, NTH == 128 ? 2 * STS_TILE_WGS : STS_TILE_WGS) 
         const int t1 = (t0 + TW < T) ? t0 + TW : (int)T;
         const int e0 = t0 - kHB;
 
-#if STS_TILE_WSCAN
-        // positions to produce: [qA, qB) (E-relative); the ACF needs REACH steps past the tile
-        const int qA = kHB;
-        const int qW = kHB + (t1 - t0);                  // end of the written range
-        int qB = qW + REACH;
-        if (e0 + qB > T) qB = (int)T - e0;
-
-        // ---- 1. the tile's registers (prefetched, or bounds-checked loads at series edges) ->
-        //      LDS; each wave turns its registers' validity ballots into its own words (lane k
-        //      holds word v WPW + k: register j gives words 2j, 2j + 1 as an even / odd bit
-        //      interleave) and scans them in registers ----
-        if (have) {
-            if constexpr (DMA) {
-                // every wave's pieces have landed (own DMA waited, then the barrier for the others)
-                dma_wait();
-                lds_barrier();
-                STS_DMA_TAKE();
-            }
-        } else {
-            STS_EDGE1(0) STS_EDGE1(1) STS_EDGE1(2) STS_EDGE1(3) STS_EDGE1(4) STS_EDGE1(5) STS_EDGE1(6)
-            STS_EDGE1(7) STS_EDGE1(8)
-        }
-        int mlo = 0, mhi = 0;   // lane k: word v WPW + k (low / high dword)
-        {
-            double2* v2_ = reinterpret_cast<double2*>(vals);
-            const int pst_ = opq(px2(wave * (64 * RPT) + lane));   // px2(x + 64 j) = px2(x) + (PAD ? 72 : 64) j
-            STS_ST1(0) STS_ST1(1) STS_ST1(2) STS_ST1(3) STS_ST1(4) STS_ST1(5) STS_ST1(6) STS_ST1(7) STS_ST1(8)
-#define STS_BAL1(j)                                                                         \
-    if constexpr (j < RPT) {                                                                \
-        const unsigned long long bx_ = __ballot(!isnan_d(R##j.x));                          \
-        const unsigned long long by_ = __ballot(!isnan_d(R##j.y));                          \
-        const unsigned long long lo_ = interleave2((unsigned)bx_, (unsigned)by_);           \
-        const unsigned long long hi_ = interleave2((unsigned)(bx_ >> 32), (unsigned)(by_ >> 32)); \
-        wlane<2 * j>(mlo, (unsigned)lo_);                                                   \
-        wlane<2 * j>(mhi, (unsigned)(lo_ >> 32));                                           \
-        wlane<2 * j + 1>(mlo, (unsigned)hi_);                                               \
-        wlane<2 * j + 1>(mhi, (unsigned)(hi_ >> 32));                                       \
-    }
-            STS_BAL1(0) STS_BAL1(1) STS_BAL1(2) STS_BAL1(3) STS_BAL1(4) STS_BAL1(5) STS_BAL1(6)
-            STS_BAL1(7) STS_BAL1(8)
-#undef STS_BAL1
-        }
-        const int wv = wave * WPW + lane;                 // this lane's word
-        const bool wok = lane < WPW && wv < NW;
-        const unsigned long long wm = wok ? (((unsigned long long)(unsigned)mhi << 32) | (unsigned)mlo) : ~0ull;
-        // NaN positions to impute: invalid AND inside [qA, qB)
-        unsigned long long wn = 0ull;
-        if (wok && method != STS_FILL_NONE) {
-            const int lo = qA - wv * 64, hi = qB - wv * 64;   // bit range [lo, hi)
-            if (hi > 0 && lo < 64) {
-                wn = ~wm;
-                if (lo > 0) wn &= ~0ull << lo;
-                if (hi < 64) wn &= (1ull << hi) - 1ull;
-            }
-        }
-        const int wl = (wok && wm) ? wv * 64 + 63 - __clzll(wm) : -1;
-        const int wf = (wok && wm) ? wv * 64 + __ffsll(wm) - 1 : kBig;
-        int wmax, wmin, wcnt, pcr[4];
-        const int pm = wave_prefix_max(wl, lane, &wmax);      // inclusive, within the wave
-        const int sm = wave_suffix_min(wf, lane, &wmin);
-        wave_prefix_sum(__popcll(wn), lane, &wcnt, pcr);      // inclusive NaN count (row-local + carries)
-        const bool lgw = method == STS_FILL_LINEAR && __ballot(wok && __popcll(~wm) > kLongRun / 2) != 0ull;
-        if (wok) {
-            mask[wv] = wm;
-            wneed[wv] = wn;
-        }
-        if (lane == 0) {
-            wsum[0][wave] = wmax;
-            wsum[1][wave] = wmin;
-            wsum[2][wave] = lgw ? 1 : 0;
-        }
-        // the next tile of this chunk, or (PERSIST) the first tile of the next chunk
-        const double* nsrc = src;
-        int64_t nk = k + 1;
-        bool have_next = false;
-        if (k + 1 < k_end) {
-            have_next = interior(k + 1);
-        } else if constexpr (PERSIST) {
-            nsrc = (ch + G < nchunk) ? chunk_first(ch + G, nk) : nullptr;
-            have_next = nsrc != nullptr;
-        }
-        STAMP(0);
-        lds_barrier();
-        STAMP(1);
-        // DMA: the staging image is free again (every thread read its pieces before the
-        // barrier): the next tile streams in during this whole tile
-        if constexpr (DMA) {
-            if (have_next) STS_DMA_ISSUE(k + 1);
-        }
-        STAMP(2);
-        STAMP(3);
-
-        // ---- 2. the waves' summaries -> this wave's word tables (last valid before / first
-        //      valid after each word), the global scans for runs longer than the halos, and the
-        //      imputation of this wave's NaN positions (F back into vals IN PLACE: every (L, N)
-        //      source is a valid position, never rewritten) ----
-        {
-            // lane u < kWaves holds wave u's summary; the carries into this wave are reduced
-            // over lanes (no per-wave uniform branches)
-            const int su = lane < kWaves ? lane : 0;
-            const int Lu = wsum[0][su], Fu = wsum[1][su], Gu = wsum[2][su];
-            const bool inu = lane < kWaves;
-            const int cl = (inu && lane < wave) ? Lu : -1, cn = (inu && lane > wave) ? Fu : kBig;
-            const int al = inu ? Lu : -1, af = inu ? Fu : kBig;
-            int cinL = -1, cinN = kBig, lastValidE = -1, firstValidE = kBig, lgs = 0;
-#pragma unroll
-            for (int u = 0; u < kWaves; u++) {
-                cinL = imax(cinL, rl(cl, u));
-                cinN = imin(cinN, rl(cn, u));
-                lastValidE = imax(lastValidE, rl(al, u));
-                firstValidE = imin(firstValidE, rl(af, u));
-                lgs |= rl(Gu, u);
-            }
-            const int exl = dpp<0x138>(-1, pm);     // lane - 1's inclusive max (all lanes active)
-            const int exf = dpp<0x130>(kBig, sm);   // lane + 1's inclusive min
-            if (wok) {
-                lastBefore[wv] = imax(cinL, exl);
-                firstAfter[wv] = imin(cinN, exf);
-            }
-            const int nnan = wcnt;
-            const int rd = (int)((k + 1) & 1), wr = (int)(k & 1);
-            // slow paths: a NaN run longer than the halos (rare); the answers are cached (by tile
-            // parity) for the next tiles of this workgroup
-            int lext = -1, next = (int)T;
-            if (needL && e0 > 0 && cinL < 0 && firstValidE > qA && nnan > 0)
-                lext = (sc[rd][0] == e0) ? sc[rd][1] : (int)scan_back(src, e0, lane);
-            if (needN && e0 + EW < T && qB > qA && cinN >= kBig && lastValidE < qB - 1 && nnan > 0) {
-                const int from = e0 + EW;
-                const int cN_pos = sc[rd][2], cN = sc[rd][3];
-                next = (cN_pos >= 0 && cN_pos <= from && cN >= from) ? cN : (int)scan_fwd(src, from, T, lane);
-                if (lane == 0) {
-                    sc[wr][2] = from;
-                    sc[wr][3] = next;
-                }
-            }
-            // the last valid index before the next tile's e0 = e0 + TW, from the wave owning word
-            // TW / 64 - 1 (no valid step in the tile's words [0, TW / 64): that wave had lext)
-            if (needL && wave == (TW / 64 - 1) / WPW && lane == 0) {
-                static_assert((TW / 64 - 1) % WPW < 16, "row-0 lane: no carry");
-                const int lq = imax(cinL, __builtin_amdgcn_readlane(pm, (TW / 64 - 1) % WPW));
-                sc[wr][0] = e0 + TW;
-                sc[wr][1] = (lq >= 0) ? e0 + lq : lext;
-            }
-            double lextv = 0.0, nextv = 0.0;
-            // (global loads inside their rare wave-uniform branches: the vmcnt wait they need is
-            // not executed on the common path, where it would also wait for the prefetch)
-            if (lext >= 0) lextv = src[lext];
-            if (next < T) nextv = src[next];
-            wave_lds_sync();   // this wave's word tables, written by other lanes
-            auto impute = [&](auto long_tag) {
-            constexpr bool LONG = decltype(long_tag)::value;
-            for (int idx = lane; idx < nnan; idx += 64) {
-                // this wave's word holding NaN #idx: the number of words whose inclusive count
-                // is <= idx (wave-uniform reads of the counts: no LDS round trips) ...
-                int kw = 0, base = 0;
-#pragma unroll
-                for (int kk = 0; kk < WPW; kk++) {
-                    const int pk = rl(pcr[0], kk) + (kk >= 16 ? pcr[kk >> 4] : 0);
-                    if (idx >= pk) {
-                        kw = kk + 1;
-                        base = pk;
-                    }
-                }
-                const int w = wave * WPW + kw;
-                unsigned long long nm = wneed[w];
-                const unsigned long long m = mask[w];
-                const int lb = lastBefore[w], fa = firstAfter[w];
-                // ... and the position of its (idx - base)-th set need-bit (popcount bisection)
-                int kq = idx - base, bit = 0;
-#pragma unroll
-                for (int width = 32; width >= 1; width >>= 1) {
-                    const int c = __popcll(nm & ((1ull << width) - 1ull));
-                    if (kq >= c) { kq -= c; nm >>= width; bit += width; }
-                }
-                const int q = w * 64 + bit;
-                const int t = e0 + q;
-                const int b = bit;
-                int Lt = -1, Nt = (int)T;
-                double Lv = 0.0, Nv = 0.0;
-                if (needL) {
-                    const unsigned long long lo = m & ((1ull << b) - 1ull);
-                    const int Lq = lo ? w * 64 + 63 - __clzll(lo) : lb;
-                    if (Lq >= 0) { Lt = e0 + Lq; Lv = vals[px(Lq)]; }
-                    else { Lt = lext; Lv = lextv; }
-                }
-                if (needN) {
-                    const unsigned long long hi = (b == 63) ? 0ull : (m & (~0ull << (b + 1)));
-                    const int Nq = hi ? w * 64 + __ffsll(hi) - 1 : fa;
-                    if (Nq < kBig) { Nt = e0 + Nq; Nv = vals[px(Nq)]; }
-                    else { Nt = next; Nv = nextv; }
-                }
-                double f = __builtin_nan("");
-                switch (method) {
-                case STS_FILL_PREVIOUS:
-                    if (Lt >= 0) f = Lv;
-                    break;
-                case STS_FILL_NEXT:
-                    if (Nt < T) f = Nv;
-                    break;
-                case STS_FILL_NEAREST: {
-                    if (t == 0) break;                        // index 0 is never modified
-                    const int P = (Lt >= 1) ? Lt : -1;        // index 0 is never a previous source
-                    if (P < 0 && Nt >= T) { series_err = true; break; }
-                    f = (Nt >= T || (P >= 0 && t - P < Nt - t)) ? Lv : Nv;   // ties go to next
-                    break;
-                }
-                case STS_FILL_LINEAR: {
-                    if (Lt < 0 || Nt >= T) break;             // runs touching index 0 or n-1 stay NaN
-                    if (LONG && t - Lt > kLongRun) {
-                        // a step more than kLongRun past L: the lane holding the run's first
-                        // such step in this tile walks the chain r = r + inc through all of
-                        // them (O(run), not O(run^2)), starting from the previous tile's
-                        // carried value when the run continues from it, else replaying from L;
-                        // the other lanes (of every wave) skip theirs
-                        if (t - Lt == kLongRun + 1 || q == qA) {
-                            const double inc = (Nv - Lv) / (double)(Nt - Lt);
-                            double v;
-                            if (carry_L[rd] == Lt && carry_t[rd] == t - 1) {
-                                v = carry_r[rd];
-                            } else {
-                                v = Lv;
-                                int j = t - 1 - Lt;   // replay from L, 8 dependent adds per trip
-                                for (; j >= 8; j -= 8) {
-                                    v = v + inc; v = v + inc; v = v + inc; v = v + inc;
-                                    v = v + inc; v = v + inc; v = v + inc; v = v + inc;
-                                }
-                                for (; j > 0; j--) v = v + inc;
-                            }
-                            const int qend = (Nt - e0 < qB) ? Nt - e0 : qB;
-                            for (int qq = q; qq < qend; qq++) {
-                                v = v + inc;
-                                vals[px(qq)] = v;
-                                if (e0 + qq == t1 - 1) {
-                                    carry_L[wr] = Lt;
-                                    carry_t[wr] = t1 - 1;
-                                    carry_r[wr] = v;
-                                }
-                            }
-                        }
-                        continue;
-                    }
-                    const double inc = (Nv - Lv) / (double)(Nt - Lt);
-                    double r = Lv;
-                    for (int j = t - Lt; j > 0; j--) r = r + inc;   // sequential, as :259-261
-                    f = r;
-                    break;
-                }
-                default:
-                    break;
-                }
-                vals[px(q)] = f;
-            }
-        };
-            if (lgs) impute(std::true_type{});
-            else impute(std::false_type{});
-        }
-        STAMP(4);
-        STAMP(5);
-        STAMP(6);
-        lds_barrier();
-        STAMP(7);
-#else
         // ---- 1. prefetched registers (or a bounds-checked edge load) -> LDS; for prefetched
         //      tiles the validity ballots come straight from the registers: register j of
         //      wave v holds steps 128v + 512j + 2*lane (+1), i.e. words 2v + 8j and 2v + 8j + 1
         //      as an even/odd bit interleave ----
         if (have) {
-            if constexpr (DMA) {
-                // every wave's pieces have landed (own DMA waited, then the barrier for the others)
-                dma_wait();
-                lds_barrier();
-                STS_DMA_TAKE();
-            }
             double2* v2_ = reinterpret_cast<double2*>(vals);
             const int pst_ = opq(px2(tid));   // px2(tid + j kThreads) = px2(tid) + j PX2S
             STS_ST1(0) STS_ST1(1) STS_ST1(2) STS_ST1(3) STS_ST1(4) STS_ST1(5) STS_ST1(6) STS_ST1(7) STS_ST1(8)
@@ -845,24 +458,10 @@ __global__ __launch_bounds__(NTH, NTH == 128 ? 2 * STS_TILE_WGS : STS_TILE_WGS) 
                 vals[px(q)] = (t >= 0 && t < T) ? src[t] : __builtin_nan("");
             }
         }
-        // the next tile of this chunk, or (PERSIST) the first tile of the next chunk
-        const double* nsrc = src;
-        int64_t nk = k + 1;
-        bool have_next = false;
-        if (k + 1 < k_end) {
-            have_next = interior(k + 1);
-        } else if constexpr (PERSIST) {
-            nsrc = (ch + G < nchunk) ? chunk_first(ch + G, nk) : nullptr;
-            have_next = nsrc != nullptr;
-        }
+        const bool have_next = (k + 1 < k_end) && interior(k + 1);
         STAMP(0);
         lds_barrier();
         STAMP(1);
-        // DMA: the staging image is free again (every thread read its pieces before the
-        // barrier): the next tile streams in during this whole tile
-        if constexpr (DMA) {
-            if (have_next) STS_DMA_ISSUE(k + 1);
-        }
 
         // positions to produce: [qA, qB) (E-relative); the ACF needs REACH steps past the tile
         const int qA = kHB;
@@ -873,8 +472,9 @@ __global__ __launch_bounds__(NTH, NTH == 128 ? 2 * STS_TILE_WGS : STS_TILE_WGS) 
         // ---- 2. validity ballots from LDS for the edge tiles (wave v owns words v, v+4, ...) ----
         if (!have) {
             const int pb = opq(px(lane) + PXW * wave);   // px(64 w + lane) = px(lane) + PXW w
-            // (not unrolled: unrolled, the per-trip tests w < NW were hoisted out of the tile loop
-            // as 16 wave-uniform 64-bit masks, spilled, and cost the common path 32 SGPRs)
+            // (not unrolled: unrolled, its per-trip tests w < NW were hoisted out of the tile loop
+            // as 16 wave-uniform 64-bit masks, spilled, and cost the common path 42 SGPRs of spill
+            // slots: 78 -> 36 spilled SGPRs, round 4)
 #pragma unroll 1
             for (int i = 0; i < (NW + kWaves - 1) / kWaves; i++) {
                 const int w = wave + i * kWaves;
@@ -1105,7 +705,6 @@ __global__ __launch_bounds__(NTH, NTH == 128 ? 2 * STS_TILE_WGS : STS_TILE_WGS) 
         STAMP(6);
         lds_barrier();
         STAMP(7);
-#endif
 
         // ---- 5. filled output + lag matrix (16-B stores), then y = F - F(0) in place
         //      (0 past the series end) for the MFMA phase; start the next tile's loads ----
@@ -1183,12 +782,8 @@ __global__ __launch_bounds__(NTH, NTH == 128 ? 2 * STS_TILE_WGS : STS_TILE_WGS) 
             // the look-back range as y = 0
             if (SHIFTED && NT > 0 && e0 < 0 && tid < kHB / 2) v2[px2(tid)] = make_double2(0.0, 0.0);
         }
-        if constexpr (DMA) {
-            STS_CLEAR();
-        } else {
-            if (have_next) STS_ISSUE_AT(nsrc, nk);   // in flight during the MFMA phase of tile k
-            else STS_CLEAR();
-        }
+        if (have_next) STS_ISSUE(k + 1);   // in flight during the MFMA phase of tile k
+        else STS_CLEAR();
         // lag matrix (fill only; S/Lag.scala:62-77): column c - init holds x[r + max_lag - c] at
         // row r.  Each column's rows of this tile go out as 16-B pairs aligned on the column's
         // own address (one wave instruction = 1 KB of one column; round 3 stored the two halves
@@ -1232,14 +827,6 @@ __global__ __launch_bounds__(NTH, NTH == 128 ? 2 * STS_TILE_WGS : STS_TILE_WGS) 
         STAMP(11);
     }
 #undef STS_ISSUE
-#undef STS_ISSUE_AT
-#undef STS_Q2
-#if STS_TILE_WSCAN
-#undef STS_EDGE1
-#endif
-#undef STS_DMA_ISSUE
-#undef STS_DMA_TAKE
-#undef STS_TK1
 #undef STS_LD1
 #undef STS_ST1
 #undef STS_CLEAR
@@ -1312,14 +899,6 @@ __global__ __launch_bounds__(NTH, NTH == 128 ? 2 * STS_TILE_WGS : STS_TILE_WGS) 
             }
         }
     }
-    if constexpr (!PERSIST) {
-        break;
-    } else {
-        ch += G;
-        if (ch >= nchunk) break;
-        lds_barrier();   // vals (the diagonal scratch) and the word tables are reused
-    }
-    }   // chunk loop
 }
 
 // One wave per series: combine the chunk partials in chunk order (deterministic) and form
@@ -1383,47 +962,39 @@ hipError_t launch_acf_shift(const double* in, int64_t S, int64_t T, int64_t ld, 
     return hipGetLastError();
 }
 
+// one launch of tile_kernel<TW, NT, SHIFTED, NTH, method>
+template <int TW, int NT, bool SHIFTED, int NTH>
+hipError_t launch_m(int method, dim3 grid, const TileArgs& a, hipStream_t st) {
+    const dim3 block(NTH);
+    switch (method) {
+    case STS_FILL_NONE: hipLaunchKernelGGL((tile_kernel<TW, NT, SHIFTED, NTH, STS_FILL_NONE>), grid, block, 0, st, a); break;
+    case STS_FILL_LINEAR: hipLaunchKernelGGL((tile_kernel<TW, NT, SHIFTED, NTH, STS_FILL_LINEAR>), grid, block, 0, st, a); break;
+    case STS_FILL_NEAREST: hipLaunchKernelGGL((tile_kernel<TW, NT, SHIFTED, NTH, STS_FILL_NEAREST>), grid, block, 0, st, a); break;
+    case STS_FILL_NEXT: hipLaunchKernelGGL((tile_kernel<TW, NT, SHIFTED, NTH, STS_FILL_NEXT>), grid, block, 0, st, a); break;
+    case STS_FILL_PREVIOUS: hipLaunchKernelGGL((tile_kernel<TW, NT, SHIFTED, NTH, STS_FILL_PREVIOUS>), grid, block, 0, st, a); break;
+    default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
 hipError_t launch_tile(int method, int tw, const TileArgs& a, hipStream_t st) {
     const int64_t nchunk = a.S * a.chunks_per_series;
     if (nchunk <= 0) return hipSuccess;
     if (nchunk > 0x7fffffffLL) return hipErrorInvalidValue;
-    dim3 grid((unsigned)nchunk), block(kThreads);
-    if (tw == 512 && a.K == 0) {
-        hipLaunchKernelGGL((tile_kernel<512, 0, false, kThreads>), grid, block, 0, st, a, method);
+    dim3 grid((unsigned)nchunk);
+    if (tw == 512 && a.K == 0) return launch_m<512, 0, false, kThreads>(method, grid, a, st);
 #ifdef STS_AB
-    } else if (tw == 2048 && a.K > 0 && a.K <= 60) {   // 2-wave workgroups (A/B build: STS_TILE_W=2048)
-        if (a.K <= 24) hipLaunchKernelGGL((tile_kernel<2048, 2, true, kThreads / 2>), grid, dim3(kThreads / 2), 0, st, a, method);
-        else hipLaunchKernelGGL((tile_kernel<2048, 4, true, kThreads / 2>), grid, dim3(kThreads / 2), 0, st, a, method);
-#endif
-#if STS_TILE_PERSIST
-    } else if (tw == 4096 && a.K <= 60) {   // variant build: resident workgroups sweep the chunks
-        static int ncu = 0;
-        if (ncu <= 0) {
-            int dev = 0, v = 0;
-            if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0) v = 256;
-            ncu = v;
-        }
-        const int64_t g = nchunk < 4 * ncu ? nchunk : 4 * ncu;
-        dim3 pg((unsigned)g);
-        if (a.K == 0) hipLaunchKernelGGL((tile_kernel<4096, 0, false, kThreads, false, true>), pg, block, 0, st, a, method);
-        else if (a.K <= 24) hipLaunchKernelGGL((tile_kernel<4096, 2, true, kThreads, false, true>), pg, block, 0, st, a, method);
-        else hipLaunchKernelGGL((tile_kernel<4096, 4, true, kThreads, false, true>), pg, block, 0, st, a, method);
-#endif
-#if STS_TILE_DMA
-    } else if (tw == 2048 && a.K > 0 && a.K <= 60) {   // variant build: LDS-DMA prefetch, 4-wave workgroups
-        if (a.K <= 24) hipLaunchKernelGGL((tile_kernel<2048, 2, true, kThreads, true>), grid, block, 0, st, a, method);
-        else hipLaunchKernelGGL((tile_kernel<2048, 4, true, kThreads, true>), grid, block, 0, st, a, method);
-#endif
-    } else if (tw == 4096) {
-        if (a.K == 0) hipLaunchKernelGGL((tile_kernel<4096, 0, false, kThreads>), grid, block, 0, st, a, method);
-        else if (a.K <= 24) hipLaunchKernelGGL((tile_kernel<4096, 2, true, kThreads>), grid, block, 0, st, a, method);
-        else if (a.K <= 60) hipLaunchKernelGGL((tile_kernel<4096, 4, true, kThreads>), grid, block, 0, st, a, method);
-        else if (a.K <= 63) hipLaunchKernelGGL((tile_kernel<4096, 5, false, kThreads>), grid, block, 0, st, a, method);
-        else return hipErrorInvalidValue;
-    } else {
-        return hipErrorInvalidValue;
+    if (tw == 2048 && a.K > 0 && a.K <= 60) {   // 2-wave workgroups (A/B build: STS_TILE_W=2048)
+        if (a.K <= 24) return launch_m<2048, 2, true, kThreads / 2>(method, grid, a, st);
+        return launch_m<2048, 4, true, kThreads / 2>(method, grid, a, st);
     }
-    return hipGetLastError();
+#endif
+    if (tw != 4096) return hipErrorInvalidValue;
+    if (a.K == 0) return launch_m<4096, 0, false, kThreads>(method, grid, a, st);
+    if (a.K <= 24) return launch_m<4096, 2, true, kThreads>(method, grid, a, st);
+    if (a.K <= 60) return launch_m<4096, 4, true, kThreads>(method, grid, a, st);
+    if (a.K <= 63) return launch_m<4096, 5, false, kThreads>(method, grid, a, st);
+    return hipErrorInvalidValue;
 }
 
 #ifdef STS_STAMPS

@@ -1,6 +1,6 @@
 """Per wave-tile SQ instruction counts and wave-cycle split of tools/r3_sqcases.sh output.
 
-    python tools/sq_cases.py OUT.json "what"   (reads gpurun_out/sqcases/ and gpurun_out/sqcases.log)
+    python tools/sq_cases.py OUT.json "what" [SUFFIX]   (reads gpurun_out/sqcases<SUFFIX>/ and .log)
 
 Dispatches are matched to kbench cases in order (one warm-up + --reps calls per case; the
 counters of one call are reported).  SQ_WAVE_CYCLES / SQ_WAIT_ANY / SQ_ACTIVE_INST_ANY count
@@ -16,13 +16,14 @@ OUT = os.path.join(ROOT, "gpurun_out")
 
 
 def main():
-    rows = list(csv.DictReader(open(os.path.join(OUT, "sqcases", "run_counter_collection.csv"))))
+    suf = sys.argv[3] if len(sys.argv) > 3 else ""
+    rows = list(csv.DictReader(open(os.path.join(OUT, "sqcases" + suf, "run_counter_collection.csv"))))
     d = collections.OrderedDict()
     for r in rows:
         if "tile_kernel" not in r["Kernel_Name"]:
             continue
         d.setdefault(int(r["Dispatch_Id"]), {})[r["Counter_Name"]] = float(r["Counter_Value"])
-    cases = [json.loads(l) for l in open(os.path.join(OUT, "sqcases.log")) if l.startswith('{"case"')]
+    cases = [json.loads(l) for l in open(os.path.join(OUT, "sqcases" + suf + ".log")) if l.startswith('{"case"')]
     disp = sorted(d)
     per = len(disp) // max(1, len(cases))
     res = []
