@@ -45,6 +45,9 @@
 // are not in this source: their records are in DESIGN.md §5.2 / profiles/INDEX.md and their code
 // at commit bd59bf8 (tools/var_rev.sh builds a library from any revision for same-box A/B).
 
+#ifndef STS_FILL_PRIO
+#define STS_FILL_PRIO 2   // wave priority outside the MFMA phase (s_setprio; r04_v8 A/B: 41.0 vs 41.4-41.6 ms on C3)
+#endif
 #ifndef STS_TILE_WGS
 #define STS_TILE_WGS 4    // workgroups per CU the register budget is sized for (128 VGPRs; LDS 40.5 KB x 4 fits)
 #endif
@@ -818,8 +821,12 @@ __global__ __launch_bounds__(NTH, STS_TILE_WGS) void tile_kernel(TileArgs a) {
         if constexpr (NT > 0) {
             lds_barrier();
             STAMP(9);
-            // ---- 6. lag products on MFMA ----
+            // ---- 6. lag products on MFMA, at wave priority 0; the rest of the tile loop runs at
+            //      STS_FILL_PRIO, so a SIMD's arbiter favours the waves of workgroups in their fill
+            //      and store phases (memory issue) over the MFMA stream of the others ----
+            __builtin_amdgcn_s_setprio(0);
             mfma_group(std::integral_constant<int, 0>{}, std::integral_constant<int, CPW>{}, vals, k, t0, t1);
+            __builtin_amdgcn_s_setprio(STS_FILL_PRIO);
         }
         have = have_next;
         STAMP(10);
