@@ -252,7 +252,9 @@ __global__ __launch_bounds__(64) void ar_fit_kernel(ArArgs a, int NT) {
 // pass).  No LDS beyond the head/tail terms; the block loads/stores are 16 B per lane.
 // The lag products P_0..P_p are lane-local FP64 FMAs: for p <= 8 the 16 x 16 MFMA tile
 // would compute >= 24 lags to use p + 1 of them, and on MI355X the FP64 VALU and FP64
-// MFMA peaks are equal (profiles/r01_ubench_fp64.jsonl).  The (p+1) x (p+1) Gram and the
+// MFMA peaks are equal (profiles/r01_ubench_fp64.jsonl).  Measured in round 4 (commit
+// history: STS_AR_MFMA): P_d from v_mfma_f64_16x16x4f64 on the LDS block, 2 MFMAs per 64
+// steps, parity green, C4 5.51 ms against 4.11 (profiles/r04_v8_ab_c4_ar_mfma.jsonl).  The (p+1) x (p+1) Gram and the
 // Cholesky run uniformly in every lane (ar_normal_chol).  Same algebra as ar_fit_kernel: centred
 // data, Gram from lag products minus head/tail terms, Cholesky + one step of refinement
 // against an exact residual pass (corrected semi-normal equations: Householder-QR accuracy).
@@ -457,33 +459,6 @@ __global__ __launch_bounds__(64 * NWV, STS_AR_WAVES_PER_EU) void ar_fit_blk_kern
 #pragma unroll
     for (int d = 0; d <= P; d++) Pd[d] = 0.0;
     double sy = 0.0;
-#if STS_AR_MFMA
-    if (hd_blk && dma) {
-        // A/B: P_d on FP64 MFMA from the raw series still in the LDS block (rows of 16 steps,
-        // U0 = within-row pairs, U1 = pairs crossing into the next row, as in ar_fit_kernel)
-        typedef double d4 __attribute__((ext_vector_type(4)));
-        d4 U0 = {0, 0, 0, 0}, U1 = {0, 0, 0, 0};
-        for (int j0 = 0; j0 < T; j0 += 64) {
-            const int ia = j0 + lane, ib = j0 + 16 + lane;
-            const double av = ia < T ? buf[ia] - mu : 0.0;
-            const double bv = ib < T ? buf[ib] - mu : 0.0;
-            U0 = __builtin_amdgcn_mfma_f64_16x16x4f64(av, av, U0, 0, 0, 0);
-            U1 = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, U1, 0, 0, 0);
-        }
-#pragma unroll
-        for (int j = 0; j < B; j++) sy += Y(j);
-        const int col = lane & 15;
-#pragma unroll
-        for (int r = 0; r < 4; r++) {
-            const int row = (lane >> 4) + 4 * r;
-#pragma unroll
-            for (int d = 0; d <= P; d++) {
-                Pd[d] += (col - row == d) ? U0[r] : 0.0;
-                Pd[d] += (col + 16 - row == d) ? U1[r] : 0.0;
-            }
-        }
-    } else
-#endif
     {
         double win[P + 1];                    // win[k] = y_{t-k}: a rolling window, no arrays of B
 #pragma unroll

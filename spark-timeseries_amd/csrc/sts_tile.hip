@@ -46,7 +46,8 @@
 // at commit bd59bf8 (tools/var_rev.sh builds a library from any revision for same-box A/B).
 
 #ifndef STS_FILL_PRIO
-#define STS_FILL_PRIO 2   // wave priority outside the MFMA phase (s_setprio; r04_v8 A/B: 41.0 vs 41.4-41.6 ms on C3)
+#define STS_FILL_PRIO 2   // wave priority outside the MFMA phase (s_setprio; same-box A/B on C3, profiles/r04_v8_ab_c3_prio.jsonl:
+                          // 41.36-41.55 ms against 41.98-42.12 without priorities, 41.60-41.63 when raised from the second tile on)
 #endif
 #ifndef STS_TILE_WGS
 #define STS_TILE_WGS 4    // workgroups per CU the register budget is sized for (128 VGPRs; LDS 40.5 KB x 4 fits)
@@ -188,6 +189,7 @@ __device__ __forceinline__ int px2_(int q2) { return PAD ? q2 + ((q2 >> 4) << 1)
 template <int TW, int NT, bool SHIFTED, int NTH, int M>
 __global__ __launch_bounds__(NTH, STS_TILE_WGS) void tile_kernel(TileArgs a) {
     constexpr int method = M;
+    if constexpr (NT > 0) __builtin_amdgcn_s_setprio(STS_FILL_PRIO);   // see the MFMA phase below
     constexpr int kThreads = NTH;          // 256 (4 waves) or 128 (2 waves, TW = 2048)
     constexpr int kWaves = NTH / 64;
     static_assert(TW / 64 % kWaves == 0, "whole 64-step chunks per wave");
