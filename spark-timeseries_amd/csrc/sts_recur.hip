@@ -16,6 +16,7 @@
 // shape (1M series x 390 steps): 64-step row segments beat 32 (1.68 vs 1.98 ms) and 128
 // (2.86 ms); the series count per wave (16 / 32 / 64) hardly matters.
 #include "sts_internal.hpp"
+#include "sts_dma.hpp"
 
 #include <hip/hip_runtime.h>
 
@@ -214,6 +215,219 @@ __global__ __launch_bounds__(64) void recur_kernel(RecurArgs a) {
     }
 }
 
+// ---------------------------------------------------------------------------------------
+// Whole rows, 16 LANES per series (4 series per wave; T <= 16 B, C2: T = 390, B = 26): lane
+// r of a row of 16 holds the steps [rB, rB + B) in registers (16-B loads straight from the row,
+// no LDS), and the sequential recurrences run lane-parallel yet bit-exact:
+//  * fillPrevious: the carry into a lane is the last valid value of the nearest lower lane of
+//    its row that has one (ballot + one bpermute); inside the block the reference's carry loop;
+//  * differencesAtLag(lag <= H): the previous lane's last H filled values by DPP row shift;
+//  * EWMA add: e_t = s d_t + (1 - s) e_{t-1} is affine in e_{t-1}.  Each lane composes its
+//    block's map (A, B); a scan of the maps along the row (DPP row_shr 1, 2, 4, 8) gives every
+//    lane a GUESS of its incoming state; one pass of the reference's own step from the guess
+//    gives each lane's outgoing state, which becomes the next lane's incoming state; a second
+//    pass computes and stores the outputs and is verified: a lane's incoming state must equal,
+//    bit for bit, the previous lane's outgoing state as computed from that lane's incoming
+//    state.  Mismatching lanes take their predecessor's value and run (and store) again.  The
+//    first lane of a row starts exactly (e_0 = d_0), so after k rounds lanes 0..k are exact and
+//    the loop ends after at most 16 rounds; with a block's contraction (1 - s)^B (0.8^26 = 3e-3
+//    for C2) it ends after the first almost always.  The outputs are the sequential loop's bits.
+// Only the fused C2 pipeline and EWMA add take this kernel (the maps of in-place EWMA remove
+// expand by (1 - s) / s, and AR add's state is a p-vector).
+#ifndef STS_RECUR_ROWSCAN
+#define STS_RECUR_ROWSCAN 1
+#endif
+#ifndef STS_RECUR_ROWSCAN_IO
+#define STS_RECUR_ROWSCAN_IO 1
+#endif
+
+template <int CTRL>
+__device__ __forceinline__ double dpp_row(double v) {   // row_shr:k; lanes shifted in from outside the row get 0
+    const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)(unsigned)u, CTRL, 0xf, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(unsigned)(u >> 32), CTRL, 0xf, 0xf, false);
+    return __builtin_bit_cast(double, ((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
+}
+__device__ __forceinline__ unsigned long long dbits(double v) { return __builtin_bit_cast(unsigned long long, v); }
+
+// IO: the wave's four rows move as one contiguous span (ld == T, T even) through a per-wave LDS
+// block: in by LDS-DMA (1 KB of consecutive doubles per instruction), out by 16-B LDS reads and
+// coalesced 16-B stores; each lane reads / writes its block in LDS.  Without IO every load / store
+// instruction touches 16 B per lane at a 8B-byte lane stride (64 cache lines per instruction).
+template <int OP, int H, int B, bool IO>
+__global__ __launch_bounds__(256) void recur_row_kernel(RecurArgs a) {
+    static_assert(B % 2 == 0 && H <= B, "lane blocks of whole 16-B pairs, history inside one block");
+    constexpr int WD = 64 * B;   // doubles per wave block: four rows of up to 16 B steps
+    __shared__ __attribute__((aligned(16))) double blk_mem[IO ? 4 * WD : 2];
+    const int lane = threadIdx.x & 63;
+    const int rl = lane & 15;
+    const int wave = threadIdx.x >> 6;
+    const int64_t s0 = ((int64_t)blockIdx.x * 4 + wave) * 4;   // the wave's first series
+    if (s0 >= a.S) return;                                     // wave-uniform
+    const int64_t s = s0 + (lane >> 4);
+    const bool live = s < a.S;
+    const int64_t sc = live ? s : a.S - 1;   // a dead row computes on a copy and stores nothing
+    const int T = (int)a.T;
+    const int t0 = rl * B;
+    const double* src = a.in + sc * a.ld_in;
+    double* dst = a.out + sc * a.ld_out;
+    const double sm = a.sm[sc];
+    const double oms = 1.0 - sm;
+    const bool even = (T & 1) == 0;   // uniform
+    double* blk = blk_mem + (IO ? wave * WD : 0);
+    const int nrow = (a.S - s0 < 4) ? (int)(a.S - s0) : 4;
+    const int span = nrow * T;                       // doubles of the wave's rows (even)
+    const int lo = (lane >> 4) * T + t0;             // this lane's block in the LDS span
+
+    // clamped addresses, no branches: steps past the row read some other valid step; they only
+    // feed lanes past the row and the row's last lane's own steps past T, never a store
+    double v[B];
+    if constexpr (IO) {
+        const double* g = a.in + s0 * a.ld_in;      // ld == T: the rows are one span
+        const unsigned lb = lds_addr(blk);
+#pragma unroll
+        for (int i = 0; i < WD / 128; i++) {
+            const int u = 128 * i + 2 * lane;
+            if (128 * i < span) glds16(g + (u < span ? u : span - 2), lb + i * 1024);
+        }
+        dma_wait();
+        wave_lds_sync();
+#pragma unroll
+        for (int j = 0; j < B; j += 2) {
+            const double2 p = *reinterpret_cast<const double2*>(blk + lo + j);
+            v[j] = p.x;
+            v[j + 1] = p.y;
+        }
+        wave_lds_sync();   // every lane has its block: the span's LDS takes the outputs
+    } else if (even) {
+#pragma unroll
+        for (int j = 0; j < B; j += 2) {
+            const int t = (t0 + j < T - 2) ? t0 + j : T - 2;
+            const double2 p = *reinterpret_cast<const double2*>(src + t);
+            v[j] = p.x;
+            v[j + 1] = p.y;
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < B; j++) v[j] = src[(t0 + j < T - 1) ? t0 + j : T - 1];
+    }
+
+    double d0;   // d at the block's first step (the EWMA's e_0 when t0 == 0)
+    if constexpr (OP == kFillDiffEwma) {
+        // ---- fillPrevious (S/UnivariateTimeSeries.scala:186-204) ----
+        double lastv = __builtin_nan("");
+#pragma unroll
+        for (int j = 0; j < B; j++) lastv = (v[j] != v[j]) ? lastv : v[j];
+        const unsigned long long below =
+            __ballot(!(lastv != lastv)) & ((1ull << lane) - 1ull) & (0xffffull << (lane & 48));
+        const double cin = __shfl(lastv, below ? 63 - __builtin_clzll(below) : lane);
+        double carry = below ? cin : __builtin_nan("");
+#pragma unroll
+        for (int j = 0; j < B; j++) {
+            carry = (v[j] != v[j]) ? carry : v[j];
+            v[j] = carry;
+        }
+        // ---- differencesAtLag(lag, start = lag) of the FILLED values (:356-376), in place from
+        //      the block's end ----
+        double pv[H + 1];   // pv[k]: the filled value at t0 - k (row lane 0: never read, t < lag)
+        pv[0] = 0.0;
+#pragma unroll
+        for (int k = 1; k <= H; k++) pv[k] = dpp_row<0x111>(v[B - k]);
+        if constexpr (H == 1) {
+#pragma unroll
+            for (int j = B - 1; j >= 1; j--) v[j] = v[j] - v[j - 1];
+            v[0] = (t0 == 0) ? v[0] : v[0] - pv[1];
+        } else {
+            const int L = a.lag;   // 1 <= L <= H
+#pragma unroll
+            for (int j = B - 1; j >= 0; j--) {
+                double hl = 0.0;
+#pragma unroll
+                for (int k = 1; k <= H; k++) hl = (k == L) ? (j >= k ? v[j - k] : pv[k - j]) : hl;
+                v[j] = (j < H && t0 + j < L) ? v[j] : v[j] - hl;
+            }
+        }
+    }
+    d0 = v[0];
+    // sm * d once per step: the reference's step is then one product and one sum,
+    // e = (s d) + ((1 - s) e), rounded in the same order
+#pragma unroll
+    for (int j = 0; j < B; j++) v[j] = sm * v[j];
+    const bool first = (t0 == 0);
+    auto enter = [&](double ein) -> double { return first ? d0 : v[0] + oms * ein; };
+
+    // ---- EWMA add (S/models/EWMA.scala:135-142): the guess ----
+    double Bm = first ? d0 : v[0];   // e_out = A e_in + Bm over the block (FMAs: a guess only)
+#pragma unroll
+    for (int j = 1; j < B; j++) Bm = __builtin_fma(oms, Bm, v[j]);
+    double A = 1.0, pw = oms;   // oms^B by squaring
+#pragma unroll
+    for (int b = B; b > 0; b >>= 1) {
+        if (b & 1) A *= pw;
+        pw *= pw;
+    }
+    A = first ? 0.0 : A;
+#define STS_ROWSCAN_STEP(K)                                                                  \
+    {                                                                                        \
+        const double Ap = dpp_row<0x110 + K>(A), Bp = dpp_row<0x110 + K>(Bm);                \
+        if (rl >= K) {                                                                       \
+            Bm = __builtin_fma(A, Bp, Bm);                                                   \
+            A = A * Ap;                                                                      \
+        }                                                                                    \
+    }
+    STS_ROWSCAN_STEP(1) STS_ROWSCAN_STEP(2) STS_ROWSCAN_STEP(4) STS_ROWSCAN_STEP(8)
+#undef STS_ROWSCAN_STEP
+    double ein = dpp_row<0x111>(Bm);   // the row's inclusive prefix ends at the state entering this lane
+    // one pass of the reference's step from the guess; its outgoing state is the next guess
+    {
+        double e = enter(ein);
+#pragma unroll
+        for (int j = 1; j < B; j++) e = v[j] + oms * e;
+        const double nx = dpp_row<0x111>(e);
+        ein = (rl > 0) ? nx : ein;
+    }
+
+    // ---- outputs from the reference's step, stored, verified lane by lane ----
+    const bool act = live && t0 < T;
+    bool dirty = true;
+    for (int round = 0; round < 16; round++) {
+        double e = enter(ein);
+        double ep = e;
+#pragma unroll
+        for (int j = 1; j < B; j++) {
+            e = v[j] + oms * e;
+            if (j & 1) {
+                const int t = t0 + j - 1;
+                if (act && dirty) {
+                    if (IO) {
+                        if (t < T) *reinterpret_cast<double2*>(blk + lo + j - 1) = make_double2(ep, e);
+                    } else if (even) {
+                        if (t < T) *reinterpret_cast<double2*>(dst + t) = make_double2(ep, e);
+                    } else {
+                        if (t + 1 < T) *reinterpret_cast<double2*>(dst + t) = make_double2(ep, e);
+                        else if (t < T) dst[t] = ep;
+                    }
+                }
+            }
+            ep = e;
+        }
+        const double eprev = dpp_row<0x111>(e);
+        const bool redo = rl > 0 && t0 < T && dbits(eprev) != dbits(ein);
+        if (!__ballot(redo)) break;
+        ein = redo ? eprev : ein;
+        dirty = redo;
+    }
+    if constexpr (IO) {   // the span out in 1-KB coalesced pieces
+        wave_lds_sync();
+        double* g = a.out + s0 * a.ld_out;
+#pragma unroll
+        for (int i = 0; i < WD / 128; i++) {
+            const int u = 128 * i + 2 * lane;
+            if (u < span) *reinterpret_cast<double2*>(g + u) = *reinterpret_cast<const double2*>(blk + u);
+        }
+    }
+}
+
 // Fallbacks for histories longer than 32 steps (correct, not tuned):
 // in-place differencing decomposes into `lag` independent chains t = r, r+lag, ...
 __global__ __launch_bounds__(256) void diff_chain_kernel(double* x, int64_t S, int64_t T, int64_t ld, int lag,
@@ -257,6 +471,36 @@ inline bool rows16(const RecurArgs& a) {
 
 template <int OP>
 hipError_t launch_h(const RecurArgs& a, int need, hipStream_t st) {
+    if constexpr (OP == kFillDiffEwma || OP == kEwmaAdd) {
+        if (STS_RECUR_ROWSCAN && need <= 8 && rows16(a) && a.T <= 16 * 32) {   // whole rows, 16 lanes per series
+            dim3 g((unsigned)((a.S + 15) / 16)), b(256);
+            const int B = (int)(((a.T + 15) / 16 + 1) & ~1);   // even, >= 2
+            const bool h1 = OP == kEwmaAdd || need <= 1;
+            if (!h1 && need > B) goto chunks;                   // the lag reaches past the previous lane
+            // one contiguous span per wave through LDS (in place too: a wave reads and rewrites
+            // only its own span)
+            const bool io = STS_RECUR_ROWSCAN_IO && a.ld_in == a.T && a.ld_out == a.T && (a.T & 1) == 0;
+#define STS_ROW_B(BB)                                                                          \
+            case BB:                                                                           \
+                if (io) {                                                                      \
+                    if (h1) hipLaunchKernelGGL((recur_row_kernel<OP, 1, BB, true>), g, b, 0, st, a); \
+                    else hipLaunchKernelGGL((recur_row_kernel<OP, (OP == kEwmaAdd ? 1 : (BB < 8 ? BB : 8)), BB, true>), g, b, 0, st, a); \
+                } else {                                                                       \
+                    if (h1) hipLaunchKernelGGL((recur_row_kernel<OP, 1, BB, false>), g, b, 0, st, a); \
+                    else hipLaunchKernelGGL((recur_row_kernel<OP, (OP == kEwmaAdd ? 1 : (BB < 8 ? BB : 8)), BB, false>), g, b, 0, st, a); \
+                }                                                                              \
+                break;
+            switch (B) {
+                STS_ROW_B(2) STS_ROW_B(4) STS_ROW_B(6) STS_ROW_B(8) STS_ROW_B(10) STS_ROW_B(12) STS_ROW_B(14)
+                STS_ROW_B(16) STS_ROW_B(18) STS_ROW_B(20) STS_ROW_B(22) STS_ROW_B(24) STS_ROW_B(26) STS_ROW_B(28)
+                STS_ROW_B(30) STS_ROW_B(32)
+            default: return hipErrorInvalidValue;
+            }
+#undef STS_ROW_B
+            return hipGetLastError();
+        }
+    }
+chunks:
     if (need <= 8 && rows16(a)) {   // the C2 shape: 16 series x 128-step chunks, 16-B accesses
         dim3 g((unsigned)((a.S + kSpw - 1) / kSpw)), b(64);
         if (need <= 1) hipLaunchKernelGGL((recur_kernel<OP, 1, kSpw, kCh, true>), g, b, 0, st, a);

@@ -1,6 +1,7 @@
 """Bit-exact parity of the recurrence kernels (recur_kernel: one lane per series, 16 series x
 128-step chunks through LDS with 16-B accesses when rows are 16-B aligned, 64 x 32 with 8-B
-accesses otherwise) with the oracle, through the C ABI.  Shapes cover partial chunks and
+accesses otherwise; recur_row_kernel for EWMA add and the fused C2 pipeline on 16-B aligned rows
+of T <= 1 024: one wave per series) with the oracle, through the C ABI.  Shapes cover partial chunks and
 partial series groups (S, T not multiples of 16 / 128), padded row strides (ld > T, different
 in and out strides, odd padding that forces the 8-B kernel) and the in-place operators
 (reference aliasing).  Needs an MI355X.
@@ -143,11 +144,10 @@ def test_recur_fill_diff_ewma(torch, S, T, lag):
     assert_bits(host(out, T), np.array(ref), "fill_diff_ewma")
 
 
-# Row-contiguous panels (ld == T, T even, 8+ series per 75-KB batch) take rows_kernel: whole-row
-# batches by LDS-DMA, double-buffered, one persistent workgroup per CU.  Batch edges (S not a
-# multiple of the batch, odd S: the smoothing piece's dword clamp), the smallest / largest rows it
-# takes (T = 2, T = 1200: 8 series per batch) and the first row it does not (T = 1202), and more
-# batches than workgroups (S = 20 000 at T = 390: 834 batches over <= 256 CUs).
+# Row-contiguous panels (ld == T, 16-B aligned rows): the shapes of the round-4 whole-row batch
+# variant (batch edges, T = 2 .. 1202, more batches than CUs); with T <= 1 024 they now take
+# recur_row_kernel (one wave per series, lane blocks of 8 / 16 steps, bit-exact affine-scan guess
+# verified lane by lane), T = 1 200 / 1 202 the chunk kernel.
 @pytest.mark.parametrize("S,T", [(1, 2), (5, 2), (300, 390), (301, 390), (24, 390), (25, 390), (17, 1200),
                                  (9, 1202), (20_000, 390), (777, 64)])
 @pytest.mark.parametrize("lag", [1, 8])
@@ -169,3 +169,39 @@ def test_recur_fill_diff_ewma_rows(torch, S, T, lag):
     for r, v in zip(x, s):
         ref.append(oracle.ewma_add(oracle.differences_at_lag(oracle.fill_previous(r), lag), v))
     assert_bits(out.cpu().numpy(), np.array(ref), "fill_diff_ewma rows")
+
+
+# recur_row_kernel edges: lane-block boundaries (T around 64 x 8 and 64 x 16, odd T: the scalar
+# tail), smoothing extremes (s = 1: every map constant; s = 1e-6: a block contracts by only
+# 1 - 8e-6, so the scan's guess is verified over more rounds), NaN runs across many lane blocks,
+# infinities, and series whose EWMA crosses zero (cancellation in the guess, not in the result).
+@pytest.mark.parametrize("T", [1, 2, 3, 7, 9, 15, 63, 64, 65, 390, 511, 512, 513, 1023, 1024, 1025])
+@pytest.mark.parametrize("lag", [1, 3, 5, 8])
+def test_recur_row_scan_edges(torch, T, lag):
+    from sparkts import _native
+    lib = _native.lib()
+    S = 11
+    rng = np.random.default_rng(31 * T + lag)
+    x = 100 + rng.standard_normal((S, T)).cumsum(axis=1)
+    x[rng.random((S, T)) < 0.1] = NaN
+    x[1, T // 8: T // 2 + 1] = NaN                  # a run over many lane blocks
+    x[2, :] = NaN
+    x[3, : T - 1] = NaN                             # only the last step valid
+    x[4] = rng.standard_normal(T) * 1e-3            # zero-mean: the EWMA of its diffs crosses 0
+    x[5, T // 3:T // 3 + 2] = np.inf
+    x[6, T // 2] = -np.inf
+    s = np.array([1.0, 1e-6, 0.999999, 0.5, 0.2, 0.2, 0.2, 1e-3, 0.97, 0.3, 0.05])
+    xd = torch.as_tensor(x, device="cuda:0")
+    out = torch.full_like(xd, 7.0)
+    assert lib.sts_fill_diff_ewma(xd.data_ptr(), out.data_ptr(), S, T, T, T, 3, lag,
+                                  dvec(torch, s).data_ptr(), None, None) == 0
+    ref = np.array([oracle.ewma_add(oracle.differences_at_lag(oracle.fill_previous(r), lag), v) for r, v in zip(x, s)])
+    assert_bits(out.cpu().numpy(), ref, "fill_diff_ewma row kernel")
+    # EWMA add alone, raw values (NaN / inf in the chain)
+    out2 = torch.full_like(xd, 7.0)
+    assert lib.sts_ewma_add(xd.data_ptr(), out2.data_ptr(), S, T, T, T, dvec(torch, s).data_ptr(), None) == 0
+    assert_bits(out2.cpu().numpy(), np.array([oracle.ewma_add(r, v) for r, v in zip(x, s)]), "ewma add row kernel")
+    # in place (the reference's dest eq ts is safe for add)
+    ip = torch.as_tensor(x, device="cuda:0").clone()
+    assert lib.sts_ewma_add(ip.data_ptr(), ip.data_ptr(), S, T, T, T, dvec(torch, s).data_ptr(), None) == 0
+    assert_bits(ip.cpu().numpy(), np.array([oracle.ewma_add(r, v) for r, v in zip(x, s)]), "ewma add in place")
