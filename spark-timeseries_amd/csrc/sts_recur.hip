@@ -1,5 +1,5 @@
-// sts_recur.hip -- first-order and p-th order recurrences along time, one LANE per
-// series, bit-exact by construction (the reference's own sequential order):
+// sts_recur.hip -- first-order and p-th order recurrences along time, bit-exact by
+// construction (the reference's own sequential order):
 //   EWMAModel.addTimeDependentEffects     S/models/EWMA.scala:135-142
 //   EWMAModel.removeTimeDependentEffects  S/models/EWMA.scala:125-133 (dest eq ts)
 //   ARModel.addTimeDependentEffects       S/models/Autoregression.scala:75-88 (IIR)
@@ -7,14 +7,13 @@
 //   differencesAtLag                      S/UnivariateTimeSeries.scala:356-376 (dest eq ts)
 //   C2 pipeline fillPrevious -> differencesAtLag(lag) -> EWMA add, fused (one HBM pass)
 //
-// A wave owns SPW series (64 by default; 32 for the fused C2 pipeline).  Time is processed
-// in chunks of CH steps: the wave loads an SPW x CH block through LDS (each load
-// instruction covers 64 consecutive steps of one series, 512 contiguous bytes; the next
-// chunk's loads are in flight while the current chunk runs), transposes it (row stride
-// CH+1 doubles: the per-lane row reads hit distinct banks), runs each lane's recurrence
-// over the chunk in registers, and stores the block back the same way.  Measured on the C2
-// shape (1M series x 390 steps): 64-step row segments beat 32 (1.68 vs 1.98 ms) and 128
-// (2.86 ms); the series count per wave (16 / 32 / 64) hardly matters.
+// Two kernels:
+//  * recur_row_kernel (C2 and EWMA add on 16-B aligned rows of <= 512 steps): whole rows, 16
+//    lanes per series, the sequential pieces made lane-parallel (carry by ballot, lag by DPP,
+//    EWMA by an affine-map scan whose guess is verified bit for bit lane by lane);
+//  * recur_kernel (everything else): one LANE per series; a wave owns SPW series and moves
+//    SPW x CH blocks through LDS (the next chunk's loads in flight while the current one runs),
+//    transposed so each lane runs its series' recurrence over the chunk in registers.
 #include "sts_internal.hpp"
 #include "sts_dma.hpp"
 

@@ -494,8 +494,12 @@ __global__ __launch_bounds__(NTH, STS_TILE_WGS) void tile_kernel(TileArgs a) {
         STAMP(3);
 
         // ---- 3. word scans (wave 0; lane l: words 2l, 2l+1): last valid position up to each
-        //      word, first valid from each word, and the NaN-list offset of each word ----
+        //      word, first valid from each word, and the NaN-list offset of each word.  The
+        //      workgroup's other waves wait at the barrier, so with the MFMA phase wave 0 runs at
+        //      the top priority (same-box A/B on C3, profiles/r04_v8_ab_c3_prio.jsonl: 5 of 5
+        //      rounds faster, 0.03-0.5 ms) ----
         if (wave == 0) {
+            if constexpr (NT > 0) __builtin_amdgcn_s_setprio(3);
             // opaque: recomputed per tile (two VALU ops) instead of hoisted out of the tile loop,
             // where the derived LDS addresses were spilled to scratch and reloaded behind a
             // vmcnt(0) on wave 0's critical path
@@ -593,6 +597,7 @@ __global__ __launch_bounds__(NTH, STS_TILE_WGS) void tile_kernel(TileArgs a) {
                 if (lane == 0) sh_d[2] = v;
             }
         }
+        if constexpr (NT > 0) __builtin_amdgcn_s_setprio(STS_FILL_PRIO);
         STAMP(4);
         lds_barrier();
         STAMP(5);

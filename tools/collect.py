@@ -37,7 +37,7 @@ FP64_COUNTERS = ["SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VAL
 FP64_KERNELS = {"c3": "tile_kernel", "c4": "ar_fit_blk_kernel"}
 # dominant kernel per workload (the c3 passes are of the default `python bench.py` command;
 # c3 directories keep their round-1 names pmc_fetch_c3 / pmc_write_c3 / prof_c3)
-TRAFFIC_KERNELS = {"c3": "tile_kernel", "c1": "short_fill_acf_kernel", "c2": "recur_kernel", "c4": "ar_fit_blk_kernel",
+TRAFFIC_KERNELS = {"c3": "tile_kernel", "c1": "short_fill_acf_kernel", "c2": "recur_row_kernel", "c4": "ar_fit_blk_kernel",
                    "c5": "tile_kernel"}
 
 
