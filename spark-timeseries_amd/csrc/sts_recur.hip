@@ -24,6 +24,10 @@
 #define STS_FDE_CH 128   // 8 x 128 1.42, 32 x 128 1.50-1.52, 32 x 64 1.59-1.67, 16 x 192 2.35, 16 x 256 2.24)
 #endif
 
+#ifndef STS_ROW_LPS
+#define STS_ROW_LPS 16   // lanes per series in recur_row_kernel
+#endif
+
 #ifndef STS_RECUR_V2
 #define STS_RECUR_V2 1   // 16-B global accesses in the C2 recurrence kernel (A/B: 1.673 vs 1.687 ms on C2)
 #endif
@@ -32,6 +36,7 @@ namespace sts {
 namespace {
 
 constexpr int kSpw = STS_FDE_SPW, kCh = STS_FDE_CH;
+constexpr int kRowLps = STS_ROW_LPS;
 
 // One lane's recurrence state and step, shared by the chunk and row kernels (the
 // reference's statement order; -ffp-contract=off keeps every product / sum separate).
@@ -229,7 +234,7 @@ __global__ __launch_bounds__(64) void recur_kernel(RecurArgs a) {
 //    bit for bit, the previous lane's outgoing state as computed from that lane's incoming
 //    state.  Mismatching lanes take their predecessor's value and run (and store) again.  The
 //    first lane of a row starts exactly (e_0 = d_0), so after k rounds lanes 0..k are exact and
-//    the loop ends after at most 16 rounds; with a block's contraction (1 - s)^B (0.8^26 = 3e-3
+//    the loop ends after at most 15 rounds; with a block's contraction (1 - s)^B (0.8^26 = 3e-3
 //    for C2) it ends after the first almost always.  The outputs are the sequential loop's bits.
 // Only the fused C2 pipeline and EWMA add take this kernel (the maps of in-place EWMA remove
 // expand by (1 - s) / s, and AR add's state is a p-vector).
@@ -248,22 +253,32 @@ __device__ __forceinline__ double dpp_row(double v) {   // row_shr:k; lanes shif
     return __builtin_bit_cast(double, ((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
 }
 __device__ __forceinline__ unsigned long long dbits(double v) { return __builtin_bit_cast(unsigned long long, v); }
+__device__ __forceinline__ double lane_get(double v, int l) {   // v_readlane: lane l's value, uniform
+    const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
+    const unsigned lo = __builtin_amdgcn_readlane((unsigned)u, l);
+    const unsigned hi = __builtin_amdgcn_readlane((unsigned)(u >> 32), l);
+    return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
+}
 
 // IO: the wave's four rows move as one contiguous span (ld == T, T even) through a per-wave LDS
 // block: in by LDS-DMA (1 KB of consecutive doubles per instruction), out by 16-B LDS reads and
 // coalesced 16-B stores; each lane reads / writes its block in LDS.  Without IO every load / store
 // instruction touches 16 B per lane at a 8B-byte lane stride (64 cache lines per instruction).
-template <int OP, int H, int B, bool IO>
+// LPS: lanes per series (16: one DPP row; 32: two rows, joined by readlanes), 64 / LPS series
+// per wave.
+template <int OP, int H, int B, bool IO, int LPS>
 __global__ __launch_bounds__(256) void recur_row_kernel(RecurArgs a) {
     static_assert(B % 2 == 0 && H <= B, "lane blocks of whole 16-B pairs, history inside one block");
-    constexpr int WD = 64 * B;   // doubles per wave block: four rows of up to 16 B steps
+    static_assert(LPS == 16 || LPS == 32, "one or two DPP rows per series");
+    constexpr int SPW = 64 / LPS;  // series per wave
+    constexpr int WD = 64 * B;     // doubles per wave block: SPW rows of up to LPS B steps
     __shared__ __attribute__((aligned(16))) double blk_mem[IO ? 4 * WD : 2];
     const int lane = threadIdx.x & 63;
-    const int rl = lane & 15;
+    const int rl = lane & (LPS - 1);
     const int wave = threadIdx.x >> 6;
-    const int64_t s0 = ((int64_t)blockIdx.x * 4 + wave) * 4;   // the wave's first series
-    if (s0 >= a.S) return;                                     // wave-uniform
-    const int64_t s = s0 + (lane >> 4);
+    const int64_t s0 = ((int64_t)blockIdx.x * 4 + wave) * SPW;   // the wave's first series
+    if (s0 >= a.S) return;                                       // wave-uniform
+    const int64_t s = s0 + lane / LPS;
     const bool live = s < a.S;
     const int64_t sc = live ? s : a.S - 1;   // a dead row computes on a copy and stores nothing
     const int T = (int)a.T;
@@ -274,9 +289,9 @@ __global__ __launch_bounds__(256) void recur_row_kernel(RecurArgs a) {
     const double oms = 1.0 - sm;
     const bool even = (T & 1) == 0;   // uniform
     double* blk = blk_mem + (IO ? wave * WD : 0);
-    const int nrow = (a.S - s0 < 4) ? (int)(a.S - s0) : 4;
+    const int nrow = (a.S - s0 < SPW) ? (int)(a.S - s0) : SPW;
     const int span = nrow * T;                       // doubles of the wave's rows (even)
-    const int lo = (lane >> 4) * T + t0;             // this lane's block in the LDS span
+    const int lo = (lane / LPS) * T + t0;            // this lane's block in the LDS span
 
     // clamped addresses, no branches: steps past the row read some other valid step; they only
     // feed lanes past the row and the row's last lane's own steps past T, never a store
@@ -318,7 +333,7 @@ __global__ __launch_bounds__(256) void recur_row_kernel(RecurArgs a) {
 #pragma unroll
         for (int j = 0; j < B; j++) lastv = (v[j] != v[j]) ? lastv : v[j];
         const unsigned long long below =
-            __ballot(!(lastv != lastv)) & ((1ull << lane) - 1ull) & (0xffffull << (lane & 48));
+            __ballot(!(lastv != lastv)) & ((1ull << lane) - 1ull) & (((1ull << LPS) - 1ull) << (lane & (64 - LPS)));
         const double cin = __shfl(lastv, below ? 63 - __builtin_clzll(below) : lane);
         double carry = below ? cin : __builtin_nan("");
 #pragma unroll
@@ -331,7 +346,7 @@ __global__ __launch_bounds__(256) void recur_row_kernel(RecurArgs a) {
         double pv[H + 1];   // pv[k]: the filled value at t0 - k (row lane 0: never read, t < lag)
         pv[0] = 0.0;
 #pragma unroll
-        for (int k = 1; k <= H; k++) pv[k] = dpp_row<0x111>(v[B - k]);
+        for (int k = 1; k <= H; k++) pv[k] = dpp_row<0x138>(v[B - k]);
         if constexpr (H == 1) {
 #pragma unroll
             for (int j = B - 1; j >= 1; j--) v[j] = v[j] - v[j - 1];
@@ -369,27 +384,35 @@ __global__ __launch_bounds__(256) void recur_row_kernel(RecurArgs a) {
 #define STS_ROWSCAN_STEP(K)                                                                  \
     {                                                                                        \
         const double Ap = dpp_row<0x110 + K>(A), Bp = dpp_row<0x110 + K>(Bm);                \
-        if (rl >= K) {                                                                       \
+        if ((lane & 15) >= K) {                                                              \
             Bm = __builtin_fma(A, Bp, Bm);                                                   \
             A = A * Ap;                                                                      \
         }                                                                                    \
     }
     STS_ROWSCAN_STEP(1) STS_ROWSCAN_STEP(2) STS_ROWSCAN_STEP(4) STS_ROWSCAN_STEP(8)
 #undef STS_ROWSCAN_STEP
-    double ein = dpp_row<0x111>(Bm);   // the row's inclusive prefix ends at the state entering this lane
+    if constexpr (LPS == 32) {   // the second row of a series continues from its first row's total
+        const double a0 = lane_get(A, 15), b0 = lane_get(Bm, 15), a1 = lane_get(A, 47), b1 = lane_get(Bm, 47);
+        const double Ap = lane < 32 ? a0 : a1, Bp = lane < 32 ? b0 : b1;
+        if (rl >= 16) {
+            Bm = __builtin_fma(A, Bp, Bm);
+            A = A * Ap;
+        }
+    }
+    double ein = dpp_row<0x138>(Bm);   // the inclusive prefix of the lane before: the state entering this one
     // one pass of the reference's step from the guess; its outgoing state is the next guess
     {
         double e = enter(ein);
 #pragma unroll
         for (int j = 1; j < B; j++) e = v[j] + oms * e;
-        const double nx = dpp_row<0x111>(e);
+        const double nx = dpp_row<0x138>(e);
         ein = (rl > 0) ? nx : ein;
     }
 
     // ---- outputs from the reference's step, stored, verified lane by lane ----
     const bool act = live && t0 < T;
     bool dirty = true;
-    for (int round = 0; round < 16; round++) {
+    for (int round = 0; round < LPS; round++) {   // round r: lanes 0..r+1 of the series exact
         double e = enter(ein);
         double ep = e;
 #pragma unroll
@@ -410,7 +433,7 @@ __global__ __launch_bounds__(256) void recur_row_kernel(RecurArgs a) {
             }
             ep = e;
         }
-        const double eprev = dpp_row<0x111>(e);
+        const double eprev = dpp_row<0x138>(e);
         const bool redo = rl > 0 && t0 < T && dbits(eprev) != dbits(ein);
         if (!__ballot(redo)) break;
         ein = redo ? eprev : ein;
@@ -471,9 +494,9 @@ inline bool rows16(const RecurArgs& a) {
 template <int OP>
 hipError_t launch_h(const RecurArgs& a, int need, hipStream_t st) {
     if constexpr (OP == kFillDiffEwma || OP == kEwmaAdd) {
-        if (STS_RECUR_ROWSCAN && need <= 8 && rows16(a) && a.T <= 16 * 32) {   // whole rows, 16 lanes per series
-            dim3 g((unsigned)((a.S + 15) / 16)), b(256);
-            const int B = (int)(((a.T + 15) / 16 + 1) & ~1);   // even, >= 2
+        if (STS_RECUR_ROWSCAN && need <= 8 && rows16(a) && a.T <= kRowLps * 32) {   // whole rows, kRowLps lanes per series
+            dim3 g((unsigned)((a.S + 4 * (64 / kRowLps) - 1) / (4 * (64 / kRowLps)))), b(256);
+            const int B = (int)(((a.T + kRowLps - 1) / kRowLps + 1) & ~1);   // even, >= 2
             const bool h1 = OP == kEwmaAdd || need <= 1;
             if (!h1 && need > B) goto chunks;                   // the lag reaches past the previous lane
             // one contiguous span per wave through LDS (in place too: a wave reads and rewrites
@@ -482,11 +505,11 @@ hipError_t launch_h(const RecurArgs& a, int need, hipStream_t st) {
 #define STS_ROW_B(BB)                                                                          \
             case BB:                                                                           \
                 if (io) {                                                                      \
-                    if (h1) hipLaunchKernelGGL((recur_row_kernel<OP, 1, BB, true>), g, b, 0, st, a); \
-                    else hipLaunchKernelGGL((recur_row_kernel<OP, (OP == kEwmaAdd ? 1 : (BB < 8 ? BB : 8)), BB, true>), g, b, 0, st, a); \
+                    if (h1) hipLaunchKernelGGL((recur_row_kernel<OP, 1, BB, true, kRowLps>), g, b, 0, st, a); \
+                    else hipLaunchKernelGGL((recur_row_kernel<OP, (OP == kEwmaAdd ? 1 : (BB < 8 ? BB : 8)), BB, true, kRowLps>), g, b, 0, st, a); \
                 } else {                                                                       \
-                    if (h1) hipLaunchKernelGGL((recur_row_kernel<OP, 1, BB, false>), g, b, 0, st, a); \
-                    else hipLaunchKernelGGL((recur_row_kernel<OP, (OP == kEwmaAdd ? 1 : (BB < 8 ? BB : 8)), BB, false>), g, b, 0, st, a); \
+                    if (h1) hipLaunchKernelGGL((recur_row_kernel<OP, 1, BB, false, kRowLps>), g, b, 0, st, a); \
+                    else hipLaunchKernelGGL((recur_row_kernel<OP, (OP == kEwmaAdd ? 1 : (BB < 8 ? BB : 8)), BB, false, kRowLps>), g, b, 0, st, a); \
                 }                                                                              \
                 break;
             switch (B) {
