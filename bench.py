@@ -231,8 +231,8 @@ def main():
     kernel = {"c3": "sts::tile_kernel<4096,4,shifted> (fill linear + ACF partials, FP64 MFMA)",
               "c1": "sts::short_fill_acf_kernel<40,20> (one wave per series in one-wave workgroups: series in by LDS-DMA, linear fill run by run in LDS, lag products as register FMAs, fused ACF finalize)",
               "c5": "sts::tile_kernel<4096,0> (fill nearest + lag-matrix columns)",
-              "c2": "sts::recur_row_kernel<kFillDiffEwma,1,26,io> (fillPrevious -> differencesAtLag(1) -> EWMA add; whole rows through LDS, 16 lanes per series, bit-exact verified affine-scan EWMA)",
-              "stage_c2": "sts::recur_row_kernel<kFillDiffEwma,1,26,io> (fillPrevious -> differencesAtLag(1) -> EWMA add; whole rows through LDS, 16 lanes per series)",
+              "c2": "sts::recur_row_kernel<kFillDiffEwma,1,14,io,32> (fillPrevious -> differencesAtLag(1) -> EWMA add; whole rows through LDS, 32 lanes per series, bit-exact verified affine-scan EWMA)",
+              "stage_c2": "sts::recur_row_kernel<kFillDiffEwma,1,14,io,32> (fillPrevious -> differencesAtLag(1) -> EWMA add; whole rows through LDS, 32 lanes per series)",
               "c4": "sts::ar_fit_blk_kernel<5,40,4,dma> (AR(5): series in by LDS-DMA, lane-blocked register lag products, normal equations / Cholesky uniform in every lane + refinement, fused remove out through LDS)",
               "stats": "sts::stats_fast_kernel<64,16> (StatCounter.merge per lane, LDS-staged series block, division off the step chain)",
               "nan_instants": "sts::nan_instants16_kernel + sts::gather_instants_kernel (wave per row)",

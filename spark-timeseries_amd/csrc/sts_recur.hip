@@ -8,7 +8,7 @@
 //   C2 pipeline fillPrevious -> differencesAtLag(lag) -> EWMA add, fused (one HBM pass)
 //
 // Two kernels:
-//  * recur_row_kernel (C2 and EWMA add on 16-B aligned rows of <= 512 steps): whole rows, 16
+//  * recur_row_kernel (C2 and EWMA add on 16-B aligned rows of <= 1 024 steps): whole rows, 32
 //    lanes per series, the sequential pieces made lane-parallel (carry by ballot, lag by DPP,
 //    EWMA by an affine-map scan whose guess is verified bit for bit lane by lane);
 //  * recur_kernel (everything else): one LANE per series; a wave owns SPW series and moves
@@ -25,7 +25,8 @@
 #endif
 
 #ifndef STS_ROW_LPS
-#define STS_ROW_LPS 16   // lanes per series in recur_row_kernel
+#define STS_ROW_LPS 32   // lanes per series in recur_row_kernel (C2 A/B, profiles/r04_v9_ab_c2_lps.jsonl:
+                         // 16 / 32 / 64 lanes 1.176-1.185 / 1.162-1.170 / 1.173-1.177 ms)
 #endif
 
 #ifndef STS_RECUR_V2
@@ -220,22 +221,23 @@ __global__ __launch_bounds__(64) void recur_kernel(RecurArgs a) {
 }
 
 // ---------------------------------------------------------------------------------------
-// Whole rows, 16 LANES per series (4 series per wave; T <= 16 B, C2: T = 390, B = 26): lane
-// r of a row of 16 holds the steps [rB, rB + B) in registers (16-B loads straight from the row,
-// no LDS), and the sequential recurrences run lane-parallel yet bit-exact:
+// Whole rows, LPS lanes per series (64 / LPS series per wave; T <= LPS B; C2 with LPS = 32:
+// B = 14, two series per wave): lane r of a series holds the steps [rB, rB + B) in registers,
+// and the sequential recurrences run lane-parallel yet bit-exact:
 //  * fillPrevious: the carry into a lane is the last valid value of the nearest lower lane of
-//    its row that has one (ballot + one bpermute); inside the block the reference's carry loop;
-//  * differencesAtLag(lag <= H): the previous lane's last H filled values by DPP row shift;
+//    its series that has one (ballot + one bpermute); inside the block the reference's carry loop;
+//  * differencesAtLag(lag <= H): the previous lane's last H filled values by DPP wave shift;
 //  * EWMA add: e_t = s d_t + (1 - s) e_{t-1} is affine in e_{t-1}.  Each lane composes its
-//    block's map (A, B); a scan of the maps along the row (DPP row_shr 1, 2, 4, 8) gives every
-//    lane a GUESS of its incoming state; one pass of the reference's own step from the guess
-//    gives each lane's outgoing state, which becomes the next lane's incoming state; a second
-//    pass computes and stores the outputs and is verified: a lane's incoming state must equal,
-//    bit for bit, the previous lane's outgoing state as computed from that lane's incoming
-//    state.  Mismatching lanes take their predecessor's value and run (and store) again.  The
-//    first lane of a row starts exactly (e_0 = d_0), so after k rounds lanes 0..k are exact and
-//    the loop ends after at most 15 rounds; with a block's contraction (1 - s)^B (0.8^26 = 3e-3
-//    for C2) it ends after the first almost always.  The outputs are the sequential loop's bits.
+//    block's map (A, B); a scan of the maps (DPP row_shr 1, 2, 4, 8 inside rows of 16, readlanes
+//    across rows) gives every lane a GUESS of its incoming state; one pass of the reference's own
+//    step from the guess gives each lane's outgoing state, which becomes the next lane's incoming
+//    state; a second pass computes and stores the outputs and is verified: a lane's incoming
+//    state must equal, bit for bit, the previous lane's outgoing state as computed from that
+//    lane's incoming state.  Mismatching lanes take their predecessor's value and run (and
+//    store) again.  A series' first lane starts exactly (e_0 = d_0), so after round r lanes
+//    0..r+1 are exact and the loop ends after at most LPS - 1 rounds; with a block's contraction
+//    (1 - s)^B (0.8^14 = 0.04 for C2) it ends after the first almost always.  The outputs are the
+//    sequential loop's bits.
 // Only the fused C2 pipeline and EWMA add take this kernel (the maps of in-place EWMA remove
 // expand by (1 - s) / s, and AR add's state is a p-vector).
 #ifndef STS_RECUR_ROWSCAN
@@ -253,25 +255,26 @@ __device__ __forceinline__ double dpp_row(double v) {   // row_shr:k; lanes shif
     return __builtin_bit_cast(double, ((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
 }
 __device__ __forceinline__ unsigned long long dbits(double v) { return __builtin_bit_cast(unsigned long long, v); }
-__device__ __forceinline__ double lane_get(double v, int l) {   // v_readlane: lane l's value, uniform
+[[maybe_unused]] __device__ __forceinline__ double lane_get(double v, int l) {   // v_readlane: lane l's value, uniform
     const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
     const unsigned lo = __builtin_amdgcn_readlane((unsigned)u, l);
     const unsigned hi = __builtin_amdgcn_readlane((unsigned)(u >> 32), l);
     return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
 }
 
-// IO: the wave's four rows move as one contiguous span (ld == T, T even) through a per-wave LDS
+// IO: the wave's rows move as one contiguous span (ld == T, T even) through a per-wave LDS
 // block: in by LDS-DMA (1 KB of consecutive doubles per instruction), out by 16-B LDS reads and
 // coalesced 16-B stores; each lane reads / writes its block in LDS.  Without IO every load / store
-// instruction touches 16 B per lane at a 8B-byte lane stride (64 cache lines per instruction).
-// LPS: lanes per series (16: one DPP row; 32: two rows, joined by readlanes), 64 / LPS series
-// per wave.
+// instruction touches 16 B per lane at an 8B-byte lane stride (up to 64 cache lines per
+// instruction).  LPS: lanes per series (16: one DPP row; 32 / 64: two / four rows, joined by
+// readlanes).
 template <int OP, int H, int B, bool IO, int LPS>
 __global__ __launch_bounds__(256) void recur_row_kernel(RecurArgs a) {
     static_assert(B % 2 == 0 && H <= B, "lane blocks of whole 16-B pairs, history inside one block");
-    static_assert(LPS == 16 || LPS == 32, "one or two DPP rows per series");
+    static_assert(LPS == 16 || LPS == 32 || LPS == 64, "one, two or four DPP rows per series");
     constexpr int SPW = 64 / LPS;  // series per wave
     constexpr int WD = 64 * B;     // doubles per wave block: SPW rows of up to LPS B steps
+    constexpr unsigned long long kGroup = LPS == 64 ? ~0ull : (1ull << (LPS % 64)) - 1ull;   // a series' lanes
     __shared__ __attribute__((aligned(16))) double blk_mem[IO ? 4 * WD : 2];
     const int lane = threadIdx.x & 63;
     const int rl = lane & (LPS - 1);
@@ -333,7 +336,7 @@ __global__ __launch_bounds__(256) void recur_row_kernel(RecurArgs a) {
 #pragma unroll
         for (int j = 0; j < B; j++) lastv = (v[j] != v[j]) ? lastv : v[j];
         const unsigned long long below =
-            __ballot(!(lastv != lastv)) & ((1ull << lane) - 1ull) & (((1ull << LPS) - 1ull) << (lane & (64 - LPS)));
+            __ballot(!(lastv != lastv)) & ((1ull << lane) - 1ull) & (kGroup << (lane & (64 - LPS)));
         const double cin = __shfl(lastv, below ? 63 - __builtin_clzll(below) : lane);
         double carry = below ? cin : __builtin_nan("");
 #pragma unroll
@@ -398,6 +401,13 @@ __global__ __launch_bounds__(256) void recur_row_kernel(RecurArgs a) {
             Bm = __builtin_fma(A, Bp, Bm);
             A = A * Ap;
         }
+    } else if constexpr (LPS == 64) {   // rows 1..3 continue from the state at the end of the row before
+        const double E0 = lane_get(Bm, 15);   // row 0 holds t = 0: its prefix is a constant
+        const double E1 = __builtin_fma(lane_get(A, 31), E0, lane_get(Bm, 31));
+        const double E2 = __builtin_fma(lane_get(A, 47), E1, lane_get(Bm, 47));
+        const int row = lane >> 4;
+        const double Ein = row == 1 ? E0 : (row == 2 ? E1 : E2);
+        Bm = row == 0 ? Bm : __builtin_fma(A, Ein, Bm);
     }
     double ein = dpp_row<0x138>(Bm);   // the inclusive prefix of the lane before: the state entering this one
     // one pass of the reference's step from the guess; its outgoing state is the next guess
