@@ -1,5 +1,5 @@
 // sts_lanes.hpp -- cross-lane moves of doubles without the LDS crossbar, for the kernels whose
-// reductions / broadcasts sit on dependency chains (sts_ar.hip, sts_seg.hip).
+// reductions / broadcasts sit on dependency chains (sts_ar.hip, sts_seg.hip), and the XCD remap.
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -39,5 +39,15 @@ __device__ __forceinline__ double row_sum_dpp(double v) {
 }
 // lane l - 1's value (wave_shr:1; lane 0 gets 0)
 __device__ __forceinline__ double lane_prev(double v) { return dpp_d<0x138>(v); }
+
+// Bijective XCD-aware remap of a workgroup id (cdna_hip_programming.md §5 "XCD swizzle must be
+// bijective"): workgroups go to the 8 XCDs round-robin (b % 8); this hands XCD x one contiguous
+// range of ids, so each XCD streams one contiguous part of the panel (tile kernel: neighbour
+// tiles of a series share the L2 that holds their overlapping halos; row kernels: C2 1.17 ->
+// 1.07 ms, profiles/r04_v10_ab_c2_shape.jsonl).
+__device__ __forceinline__ int64_t xcd_remap(int64_t b, int64_t n) {
+    int64_t q = n / 8, r = n % 8, x = b % 8;
+    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
+}
 
 }  // namespace sts

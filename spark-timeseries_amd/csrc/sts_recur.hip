@@ -16,17 +16,13 @@
 //    transposed so each lane runs its series' recurrence over the chunk in registers.
 #include "sts_internal.hpp"
 #include "sts_dma.hpp"
+#include "sts_lanes.hpp"
 
 #include <hip/hip_runtime.h>
 
 #ifndef STS_FDE_SPW
 #define STS_FDE_SPW 16   // series per wave (A/B on C2, 1M x 390: 16 x 128 1.40 ms, 24 x 128 1.41-1.43,
 #define STS_FDE_CH 128   // 8 x 128 1.42, 32 x 128 1.50-1.52, 32 x 64 1.59-1.67, 16 x 192 2.35, 16 x 256 2.24)
-#endif
-
-#ifndef STS_ROW_LPS
-#define STS_ROW_LPS 32   // lanes per series in recur_row_kernel (C2 A/B, profiles/r04_v9_ab_c2_lps.jsonl:
-                         // 16 / 32 / 64 lanes 1.176-1.185 / 1.162-1.170 / 1.173-1.177 ms)
 #endif
 
 #ifndef STS_RECUR_V2
@@ -37,7 +33,12 @@ namespace sts {
 namespace {
 
 constexpr int kSpw = STS_FDE_SPW, kCh = STS_FDE_CH;
-constexpr int kRowLps = STS_ROW_LPS;
+// recur_row_kernel's launch shape (C2 A/B, profiles/r04_v9_ab_c2_lps.jsonl, r04_v10_ab_c2_shape.jsonl):
+// 16 / 32 / 64 lanes per series 1.176-1.185 / 1.162-1.170 / 1.173-1.177 ms; 1 / 2 / 4 waves per
+// workgroup 1.248-1.252 / 1.202-1.204 / 1.170-1.174 ms; XCD-contiguous spans 1.068-1.070 against
+// 1.160-1.170 ms without
+constexpr int kRowLps = 32;
+constexpr int kRowWpg = 4;
 
 // One lane's recurrence state and step, shared by the chunk and row kernels (the
 // reference's statement order; -ffp-contract=off keeps every product / sum separate).
@@ -269,17 +270,18 @@ __device__ __forceinline__ unsigned long long dbits(double v) { return __builtin
 // instruction).  LPS: lanes per series (16: one DPP row; 32 / 64: two / four rows, joined by
 // readlanes).
 template <int OP, int H, int B, bool IO, int LPS>
-__global__ __launch_bounds__(256) void recur_row_kernel(RecurArgs a) {
+__global__ __launch_bounds__(64 * kRowWpg) void recur_row_kernel(RecurArgs a) {
     static_assert(B % 2 == 0 && H <= B, "lane blocks of whole 16-B pairs, history inside one block");
     static_assert(LPS == 16 || LPS == 32 || LPS == 64, "one, two or four DPP rows per series");
     constexpr int SPW = 64 / LPS;  // series per wave
     constexpr int WD = 64 * B;     // doubles per wave block: SPW rows of up to LPS B steps
     constexpr unsigned long long kGroup = LPS == 64 ? ~0ull : (1ull << (LPS % 64)) - 1ull;   // a series' lanes
-    __shared__ __attribute__((aligned(16))) double blk_mem[IO ? 4 * WD : 2];
+    __shared__ __attribute__((aligned(16))) double blk_mem[IO ? kRowWpg * WD : 2];
     const int lane = threadIdx.x & 63;
     const int rl = lane & (LPS - 1);
     const int wave = threadIdx.x >> 6;
-    const int64_t s0 = ((int64_t)blockIdx.x * 4 + wave) * SPW;   // the wave's first series
+    const int64_t bid = xcd_remap(blockIdx.x, gridDim.x);   // XCD x streams one contiguous range of spans
+    const int64_t s0 = (bid * kRowWpg + wave) * SPW;   // the wave's first series
     if (s0 >= a.S) return;                                       // wave-uniform
     const int64_t s = s0 + lane / LPS;
     const bool live = s < a.S;
@@ -505,7 +507,7 @@ template <int OP>
 hipError_t launch_h(const RecurArgs& a, int need, hipStream_t st) {
     if constexpr (OP == kFillDiffEwma || OP == kEwmaAdd) {
         if (STS_RECUR_ROWSCAN && need <= 8 && rows16(a) && a.T <= kRowLps * 32) {   // whole rows, kRowLps lanes per series
-            dim3 g((unsigned)((a.S + 4 * (64 / kRowLps) - 1) / (4 * (64 / kRowLps)))), b(256);
+            dim3 g((unsigned)((a.S + kRowWpg * (64 / kRowLps) - 1) / (kRowWpg * (64 / kRowLps)))), b(64 * kRowWpg);
             const int B = (int)(((a.T + kRowLps - 1) / kRowLps + 1) & ~1);   // even, >= 2
             const bool h1 = OP == kEwmaAdd || need <= 1;
             if (!h1 && need > B) goto chunks;                   // the lag reaches past the previous lane

@@ -81,7 +81,7 @@ __global__ __launch_bounds__(64 * kShortWaves, 2) void short_fill_acf_kernel(Til
     __shared__ __attribute__((aligned(16))) double buf_mem[kShortWaves * BUFD];
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int64_t s = (int64_t)blockIdx.x * kShortWaves + wave;
+    const int64_t s = (int64_t)blockIdx.x * kShortWaves + wave;   // (an XCD-contiguous remap: 0.1025-0.1029 vs 0.1028-0.1030 ms, round 4)
     if (s >= a.S) return;
     double* buf = buf_mem + wave * BUFD;
     const int T = (int)a.T;

@@ -32,6 +32,7 @@
 // v_mfma_f64_16x16x4_f64, so both operands are contiguous LDS reads.  A finalize
 // kernel (sts_acf_finalize) combines the tiles in a fixed order (deterministic).
 #include "sts_internal.hpp"
+#include "sts_lanes.hpp"
 #include "sts_acf.hpp"
 #include "sts_scan.hpp"
 
@@ -90,14 +91,6 @@ __device__ unsigned long long g_stamps[16];
     do {         \
     } while (0)
 #endif
-
-// Bijective XCD-aware remap (cdna_hip_programming.md §5 "XCD swizzle must be
-// bijective"): consecutive tile ids -> one XCD, so neighbour tiles of one series
-// share the L2 that holds their overlapping halos.
-__device__ __forceinline__ int64_t xcd_remap(int64_t b, int64_t n) {
-    int64_t q = n / 8, r = n % 8, x = b % 8;
-    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
-}
 
 // Interleave two 32-step validity ballots into one 64-step word: bit i of ev -> bit 2i,
 // bit i of od -> bit 2i + 1.  s_bitreplicate_b64_b32 doubles every bit (i -> 2i, 2i + 1)
