@@ -241,12 +241,6 @@ __global__ __launch_bounds__(64) void recur_kernel(RecurArgs a) {
 //    sequential loop's bits.
 // Only the fused C2 pipeline and EWMA add take this kernel (the maps of in-place EWMA remove
 // expand by (1 - s) / s, and AR add's state is a p-vector).
-#ifndef STS_RECUR_ROWSCAN
-#define STS_RECUR_ROWSCAN 1
-#endif
-#ifndef STS_RECUR_ROWSCAN_IO
-#define STS_RECUR_ROWSCAN_IO 1
-#endif
 
 template <int CTRL>
 __device__ __forceinline__ double dpp_row(double v) {   // row_shr:k; lanes shifted in from outside the row get 0
@@ -506,14 +500,14 @@ inline bool rows16(const RecurArgs& a) {
 template <int OP>
 hipError_t launch_h(const RecurArgs& a, int need, hipStream_t st) {
     if constexpr (OP == kFillDiffEwma || OP == kEwmaAdd) {
-        if (STS_RECUR_ROWSCAN && need <= 8 && rows16(a) && a.T <= kRowLps * 32) {   // whole rows, kRowLps lanes per series
+        if (need <= 8 && rows16(a) && a.T <= kRowLps * 32) {   // whole rows, kRowLps lanes per series
             dim3 g((unsigned)((a.S + kRowWpg * (64 / kRowLps) - 1) / (kRowWpg * (64 / kRowLps)))), b(64 * kRowWpg);
             const int B = (int)(((a.T + kRowLps - 1) / kRowLps + 1) & ~1);   // even, >= 2
             const bool h1 = OP == kEwmaAdd || need <= 1;
             if (!h1 && need > B) goto chunks;                   // the lag reaches past the previous lane
             // one contiguous span per wave through LDS (in place too: a wave reads and rewrites
             // only its own span)
-            const bool io = STS_RECUR_ROWSCAN_IO && a.ld_in == a.T && a.ld_out == a.T && (a.T & 1) == 0;
+            const bool io = a.ld_in == a.T && a.ld_out == a.T && (a.T & 1) == 0;
 #define STS_ROW_B(BB)                                                                          \
             case BB:                                                                           \
                 if (io) {                                                                      \
