@@ -243,7 +243,7 @@ __global__ __launch_bounds__(64) void recur_kernel(RecurArgs a) {
 // expand by (1 - s) / s, and AR add's state is a p-vector).
 
 template <int CTRL>
-__device__ __forceinline__ double dpp_row(double v) {   // row_shr:k; lanes shifted in from outside the row get 0
+__device__ __forceinline__ double dpp_shift(double v) {   // row_shr:k (0x110 + k) or wave_shr:1 (0x138); lanes without a source get 0
     const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
     const int lo = __builtin_amdgcn_update_dpp(0, (int)(unsigned)u, CTRL, 0xf, 0xf, false);
     const int hi = __builtin_amdgcn_update_dpp(0, (int)(unsigned)(u >> 32), CTRL, 0xf, 0xf, false);
@@ -345,7 +345,7 @@ __global__ __launch_bounds__(64 * kRowWpg) void recur_row_kernel(RecurArgs a) {
         double pv[H + 1];   // pv[k]: the filled value at t0 - k (row lane 0: never read, t < lag)
         pv[0] = 0.0;
 #pragma unroll
-        for (int k = 1; k <= H; k++) pv[k] = dpp_row<0x138>(v[B - k]);
+        for (int k = 1; k <= H; k++) pv[k] = dpp_shift<0x138>(v[B - k]);
         if constexpr (H == 1) {
 #pragma unroll
             for (int j = B - 1; j >= 1; j--) v[j] = v[j] - v[j - 1];
@@ -382,7 +382,7 @@ __global__ __launch_bounds__(64 * kRowWpg) void recur_row_kernel(RecurArgs a) {
     A = first ? 0.0 : A;
 #define STS_ROWSCAN_STEP(K)                                                                  \
     {                                                                                        \
-        const double Ap = dpp_row<0x110 + K>(A), Bp = dpp_row<0x110 + K>(Bm);                \
+        const double Ap = dpp_shift<0x110 + K>(A), Bp = dpp_shift<0x110 + K>(Bm);                \
         if ((lane & 15) >= K) {                                                              \
             Bm = __builtin_fma(A, Bp, Bm);                                                   \
             A = A * Ap;                                                                      \
@@ -405,13 +405,13 @@ __global__ __launch_bounds__(64 * kRowWpg) void recur_row_kernel(RecurArgs a) {
         const double Ein = row == 1 ? E0 : (row == 2 ? E1 : E2);
         Bm = row == 0 ? Bm : __builtin_fma(A, Ein, Bm);
     }
-    double ein = dpp_row<0x138>(Bm);   // the inclusive prefix of the lane before: the state entering this one
+    double ein = dpp_shift<0x138>(Bm);   // the inclusive prefix of the lane before: the state entering this one
     // one pass of the reference's step from the guess; its outgoing state is the next guess
     {
         double e = enter(ein);
 #pragma unroll
         for (int j = 1; j < B; j++) e = v[j] + oms * e;
-        const double nx = dpp_row<0x138>(e);
+        const double nx = dpp_shift<0x138>(e);
         ein = (rl > 0) ? nx : ein;
     }
 
@@ -439,7 +439,7 @@ __global__ __launch_bounds__(64 * kRowWpg) void recur_row_kernel(RecurArgs a) {
             }
             ep = e;
         }
-        const double eprev = dpp_row<0x138>(e);
+        const double eprev = dpp_shift<0x138>(e);
         const bool redo = rl > 0 && t0 < T && dbits(eprev) != dbits(ein);
         if (!__ballot(redo)) break;
         ein = redo ? eprev : ein;
