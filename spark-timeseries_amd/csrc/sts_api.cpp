@@ -139,6 +139,11 @@ int method_ok(int method, bool allow_none, const char* name) {
 
 int tile_width(int64_t T) { return T <= 512 ? 512 : 4096; }
 constexpr int64_t kTilesPerChunk = 16;  // tiles per workgroup (prefetch pipeline depth 1)
+// without the ACF (fill only, fill + lag matrix: C5) one tile per workgroup: the denser sweep
+// beats the prefetch pipeline (C5: 1.527-1.534 vs 1.647-1.659 ms same box, and 1.83 vs 2.03-2.07 on
+// a box in its slow state, profiles/r04_v11_ab_c5_tpc.jsonl; fill only on the C3 shard 31.2-31.6 vs
+// 33.3 ms, r04_v2_ab_tiles_per_chunk.jsonl)
+constexpr int64_t kTilesPerChunkFill = 1;
 
 // Measurement hook (bench.py): HIP events recorded on the launch stream around every
 // tile-kernel launch of this thread while profiling is on.
@@ -207,7 +212,8 @@ int run_tile(const double* in, double* out, double* lagmat, int64_t S, int64_t T
     // STS_TILES_PER_CHUNK: tiles per tile-kernel workgroup, for A/B runs only
     const char* tpc_env = seg ? nullptr : sts::ab_knob("STS_TILES_PER_CHUNK");
     const int seg_knob = seg_env ? std::atoi(seg_env) : 0, tpc_knob = tpc_env ? std::atoi(tpc_env) : 0;
-    const int64_t per_chunk = seg ? (seg_knob > 0 ? seg_knob : sts::kSegTiles) : (tpc_knob > 0 ? tpc_knob : kTilesPerChunk);
+    const int64_t per_chunk = seg ? (seg_knob > 0 ? seg_knob : sts::kSegTiles)
+                                  : (tpc_knob > 0 ? tpc_knob : (K > 0 ? kTilesPerChunk : kTilesPerChunkFill));
     a.tiles_per_chunk = a.tiles_per_series < per_chunk ? a.tiles_per_series : per_chunk;
     a.chunks_per_series = (a.tiles_per_series + a.tiles_per_chunk - 1) / a.tiles_per_chunk;
     a.K = K;
