@@ -205,3 +205,30 @@ def test_recur_row_scan_edges(torch, T, lag):
     ip = torch.as_tensor(x, device="cuda:0").clone()
     assert lib.sts_ewma_add(ip.data_ptr(), ip.data_ptr(), S, T, T, T, dvec(torch, s).data_ptr(), None) == 0
     assert_bits(ip.cpu().numpy(), np.array([oracle.ewma_add(r, v) for r, v in zip(x, s)]), "ewma add in place")
+
+
+# recur_row_kernel's direct-access form on odd T (16-B aligned rows need an even stride: ld = T + 1
+# or T + 3), where the last pair of a row is a single step (8-B loads from clamped addresses).
+@pytest.mark.parametrize("T", [1, 3, 9, 65, 391, 1023])
+@pytest.mark.parametrize("extra", [1, 3])
+def test_recur_row_scan_odd_rows(torch, T, extra):
+    from sparkts import _native
+    lib = _native.lib()
+    S = 9
+    ld = T + extra
+    rng = np.random.default_rng(17 * T + extra)
+    x = 100 + rng.standard_normal((S, T)).cumsum(axis=1)
+    x[rng.random((S, T)) < 0.15] = NaN
+    x[1, :] = NaN
+    s = rng.uniform(0.05, 0.95, S)
+    xi = padded(torch, x, ld)
+    out = padded(torch, np.zeros((S, T)), ld)
+    assert lib.sts_fill_diff_ewma(xi.data_ptr(), out.data_ptr(), S, T, ld, ld, 3, 1,
+                                  dvec(torch, s).data_ptr(), None, None) == 0
+    ref = np.array([oracle.ewma_add(oracle.differences_at_lag(oracle.fill_previous(r), 1), v) for r, v in zip(x, s)])
+    assert_bits(host(out, T), ref, "fill_diff_ewma odd rows")
+    assert (out[:, T:].cpu().numpy() == 7.0).all(), "wrote into the row padding"
+    out2 = padded(torch, np.zeros((S, T)), ld)
+    assert lib.sts_ewma_add(xi.data_ptr(), out2.data_ptr(), S, T, ld, ld, dvec(torch, s).data_ptr(), None) == 0
+    assert_bits(host(out2, T), np.array([oracle.ewma_add(r, v) for r, v in zip(x, s)]), "ewma add odd rows")
+    assert (out2[:, T:].cpu().numpy() == 7.0).all(), "wrote into the row padding"
