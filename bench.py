@@ -32,9 +32,19 @@ WORKLOADS = {
            "C3 shard: fill('linear') + autocorr(60), 12,500 series x 982,800 steps per GPU "
            "(N=8 -> C3's 100k x 982,800, 786 GB)"),
     "c1": (10_000, 2_520, 0.05, 1, "C1: fill('linear') + autocorr(20), 10,000 series x 2,520 steps"),
+    "c1_rule3": (10_000, 2_520, 0.05, 1,
+                 "ACF rule-3 worst case at the C1 shape: every series the constant 100.1 with 5 % NaN (a suspended "
+                 "instrument), fill('linear') + autocorr(20); every series flagged, every lag from the reference's "
+                 "two-pass loop (sts_acf.hpp acf_exact_lag)"),
+    "c3_rule3": (1_000, 982_800, 0.05, 3,
+                 "ACF rule-3 worst case at the C3 length: 1,000 series of the constant 100.1 with 5 % NaN, "
+                 "fill('linear') + autocorr(60); every series flagged (two-pass loop per lag)"),
     "c2": (1_000_000, 390, 0.05, 2,
            "C2: fillPrevious -> differencesAtLag(1) -> EWMA(0.2).add, 1,000,000 series x 390 steps"),
     "c4": (500_000, 2_520, 0.0, 4, "C4: AR(5) fit + removeTimeDependentEffects, 500,000 series x 2,520 steps"),
+    "c4_levels": (500_000, 2_520, 0.0, 4,
+                  "C4 shape on price levels (AR rule worst case): 1e4 + 0.01 x the C4 panel, every series flagged "
+                  "and fitted with the reference's Householder-QR order (sts_ar_qr.hip), 500,000 series x 2,520 steps"),
     "stage_c2": (1_000_000, 390, 0.05, 2,
                  "C2 (fillPrevious -> differencesAtLag(1) -> EWMA(0.2).add, 1,000,000 series x 390 steps) from "
                  "HOST-resident panels through the _host entry points' pinned staging pipeline; value = the "
@@ -91,12 +101,14 @@ def main():
         _native.use_library(os.environ["STS_HIP_LIB"])
     _native.ensure_device(local)
     lib = _native.lib()
+    global LIB_SHA16
+    LIB_SHA16 = lib_sha16(lib._name)
 
     S, T, nan_p, seed, desc = WORKLOADS[args.workload]
     if args.series:
         S = args.series
     K, p_ar = 60, 5
-    if args.workload == "c1":
+    if args.workload in ("c1", "c1_rule3"):
         K = 20
     s0 = rank * S                      # this rank's partition of the keyed panel
     stream = torch.cuda.current_stream(dev)
@@ -108,15 +120,19 @@ def main():
     err = torch.zeros(S, dtype=torch.int32, device=dev)
     if args.workload in ("stage_c2",):
         pass
-    if args.workload == "c4":
+    if args.workload in ("c4", "c4_levels"):
         cgen = torch.empty(S, dtype=torch.float64, device=dev)
         pgen = torch.empty((S, p_ar), dtype=torch.float64, device=dev)
         raise_for_status(lib.sts_gen_ar_panel(x.data_ptr(), cgen.data_ptr(), pgen.data_ptr(), s0, S, T, T, seed, p_ar,
                                               sp), "gen")
+        if args.workload == "c4_levels":
+            x.mul_(0.01).add_(1e4)
         c_fit = torch.empty(S, dtype=torch.float64, device=dev)
         coef_fit = torch.empty((S, p_ar), dtype=torch.float64, device=dev)
     else:
         raise_for_status(lib.sts_gen_panel(x.data_ptr(), s0, S, T, T, seed, nan_p, sp), "gen")
+        if args.workload in ("c1_rule3", "c3_rule3"):
+            x.masked_fill_(~torch.isnan(x), 100.1)
     smooth = torch.full((S,), 0.2, dtype=torch.float64, device=dev)
     if args.workload == "ewma_fit":
         smooth = torch.empty((S,), dtype=torch.float64, device=dev)
@@ -152,7 +168,7 @@ def main():
         gather = ResultGather(S, (3,), torch.float64, dev)
     elif world > 1 and args.workload == "ewma_fit":
         gather = ResultGather(S, (1,), torch.float64, dev)
-    elif world > 1 and args.workload == "c4":
+    elif world > 1 and args.workload in ("c4", "c4_levels"):
         gather = ResultGather(S, (1 + p_ar,), torch.float64, dev)
 
     # the headline step: one fused fill + ACF launch over the rank's shard, then the all-gather
@@ -162,7 +178,7 @@ def main():
         "fill_autocorr"), acf, gather)
 
     def step():
-        if args.workload in ("c3", "c1"):
+        if args.workload in ("c3", "c1", "c1_rule3", "c3_rule3"):
             fill_acf()
         elif args.workload in ("c2", "stage_c2"):
             raise_for_status(lib.sts_fill_diff_ewma(x.data_ptr(), out.data_ptr(), S, T, T, T, 3, 1, smooth.data_ptr(),
@@ -200,7 +216,7 @@ def main():
                              "EWMA.fitModel")
             if world > 1:
                 gather(smooth[:, None])
-        elif args.workload == "c4":
+        elif args.workload in ("c4", "c4_levels"):
             raise_for_status(lib.sts_ar_fit_remove(x.data_ptr(), out.data_ptr(), S, T, T, T, p_ar, 0,
                                                    c_fit.data_ptr(), coef_fit.data_ptr(), err.data_ptr(), sp),
                              "ar_fit_remove")
@@ -229,10 +245,13 @@ def main():
     if args.workload == "nan_instants":  # flag pass reads everything; the gather reads + writes kept values
         bytes_per_step = 8.0 * S * T + 16.0 * S * n_keep
     kernel = {"c3": "sts::tile_kernel<4096,4,shifted> (fill linear + ACF partials, FP64 MFMA)",
+              "c1_rule3": "sts::short_fill_acf_kernel<40,20> with rule 3 firing on every series (acf_exact_lag per lag)",
+              "c3_rule3": "sts::tile_kernel<4096,4,shifted> + acf_finalize_kernel with rule 3 firing on every series",
               "c1": "sts::short_fill_acf_kernel<40,20> (one wave per series in one-wave workgroups: series in by LDS-DMA, linear fill run by run in LDS, lag products as register FMAs, fused ACF finalize)",
               "c5": "sts::tile_kernel<4096,0> (fill nearest + lag-matrix columns)",
               "c2": "sts::recur_row_kernel<kFillDiffEwma,1,14,io,32> (fillPrevious -> differencesAtLag(1) -> EWMA add; whole rows through LDS, 32 lanes per series, bit-exact verified affine-scan EWMA)",
               "stage_c2": "sts::recur_row_kernel<kFillDiffEwma,1,14,io,32> (fillPrevious -> differencesAtLag(1) -> EWMA add; whole rows through LDS, 32 lanes per series)",
+              "c4_levels": "sts::ar_fit_blk_kernel<5,40,4,dma> + sts::ar_qr_lane_kernel<5,true> (every series flagged: the reference's Householder-QR order, one series per lane, reflections replayed per row)",
               "c4": "sts::ar_fit_blk_kernel<5,40,4,dma> (AR(5): series in by LDS-DMA, lane-blocked register lag products, normal equations / Cholesky uniform in every lane + refinement, fused remove out through LDS)",
               "stats": "sts::stats_fast_kernel<64,16> (StatCounter.merge per lane, LDS-staged series block, division off the step chain)",
               "nan_instants": "sts::nan_instants16_kernel + sts::gather_instants_kernel (wave per row)",
@@ -251,7 +270,7 @@ def main():
         achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9
         roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                     "frac": round(achieved / HBM_PEAK_GBPS, 4),
-                    "traffic": measured_traffic(args.workload, S, T), "kernel": kernel,
+                    "traffic": measured_traffic(args.workload, S, T), "kernel": kernel, "lib_sha16": LIB_SHA16,
                     "avg_kernel_ms": round(avg_ms, 4), "bytes_per_launch": bytes_per_launch,
                     "kernel_launches_timed": int(launches[0])}
         fp = measured_fp64(args.workload, S, T, avg_ms)
@@ -261,7 +280,8 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.workload != "stage_c2":   # the CPU leg is an N = 1 report
         cpu = cpu_baseline(args, S, T, K, seed, nan_p, out, acf, p_ar, smooth,
-                           gpar if args.workload == "garch_fit" else None)
+                           gpar if args.workload == "garch_fit" else None,
+                           (c_fit, coef_fit) if args.workload in ("c4", "c4_levels") else None)
 
     line = result_line(args.workload, value, world, args.steps, args.warmup, ms_per_step, desc, S, T, K, nan_p,
                        roofline, cpu)
@@ -324,7 +344,8 @@ def timed_region(step, steps, warmup, world, sync, reduce_device, on_start=None,
     return wall, elapsed
 
 
-FILL_OF = {"c3": "linear", "c1": "linear", "c2": "previous", "stage_c2": "previous", "c4": None, "c5": "nearest",
+FILL_OF = {"c3": "linear", "c1": "linear", "c1_rule3": "linear", "c3_rule3": "linear", "c2": "previous", "stage_c2": "previous", "c4": None, "c4_levels": None,
+           "c5": "nearest",
            "ewma_fit": None, "garch_fit": None, "stats": None, "nan_instants": None, "to_instants": None,
            "wire_decode": None}
 
@@ -338,7 +359,7 @@ def result_line(workload, value, world, steps, warmup, ms_per_step, desc, S, T, 
         "vs_baseline": None, "dtype": "f64",
         "data": "synthetic: Philox4x32-10 counter-based panel generated in HBM (SURVEY.md 8(d)), %g NaN" % nan_p,
         "config": {"workload": desc, "series_per_gpu": S, "steps_per_series": T,
-                   "numLags": K if workload in ("c3", "c1") else None,
+                   "numLags": K if workload in ("c3", "c1", "c1_rule3", "c3_rule3") else None,
                    "fill": FILL_OF[workload],
                    "parallelism": "dp%d (series sharded by key, one process per GPU)" % world},
         "roofline": roofline,
@@ -409,11 +430,21 @@ def staging_leg(args, lib, x, out, smooth, S, T):
     return res
 
 
+LIB_SHA16 = None   # sha256[:16] of the libsts_hip.so this process loaded (main)
+
+
+def lib_sha16(path):
+    import hashlib
+    with open(path, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()[:16]
+
+
 def measured_traffic(workload, S, T):
     """HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC passes
     (profiles/<round>_<workload>_traffic.json, written by tools/collect.py from separate
     FETCH_SIZE / WRITE_SIZE passes over this same workload at its default shape); None when no
-    pass covers it."""
+    pass covers it, or when the newest pass was taken on a different build of libsts_hip.so
+    (its lib_sha16 is not the loaded library's)."""
     import glob
     if workload not in WORKLOADS or (S, T) != WORKLOADS[workload][:2]:
         return None
@@ -427,6 +458,8 @@ def measured_traffic(workload, S, T):
         return None
     with open(files[-1]) as f:
         rec = json.load(f)
+    if rec.get("lib_sha16") is None or rec.get("lib_sha16") != LIB_SHA16:
+        return None
     return rec.get("traffic_bytes_per_launch")
 
 
@@ -450,6 +483,8 @@ def measured_fp64(workload, S, T, avg_ms):
         return None
     with open(files[-1]) as f:
         rec = json.load(f)
+    if rec.get("lib_sha16") is None or rec.get("lib_sha16") != LIB_SHA16:
+        return None
     sec = avg_ms * 1e-3
     return {"source": os.path.basename(files[-1]),
             "tflops": round(rec["fp64_flops_per_launch"] / sec / 1e12, 2),
@@ -470,7 +505,7 @@ def cpu_threads():
     return max(1, n)
 
 
-def cpu_baseline(args, S, T, K, seed, nan_p, out, acf, p_ar, smooth=None, gpar_ref=None):
+def cpu_baseline(args, S, T, K, seed, nan_p, out, acf, p_ar, smooth=None, gpar_ref=None, ar_model=None):
     """The oracle (CPU restatement of the reference loops, oracle/) on a bounded sample of
     the same workload, one series per thread like Spark local[N].  The sample series are
     the rank-0 series 0..n-1, so their GPU results are also checked here."""
@@ -483,16 +518,21 @@ def cpu_baseline(args, S, T, K, seed, nan_p, out, acf, p_ar, smooth=None, gpar_r
         threads, per_round = 1, 4096     # single-threaded restatements (one partition)
     done, elapsed, s_next = 0, 0.0, 0
     worst_rel, exact = 0.0, True
+    ar_check = None
     while elapsed < args.cpu_seconds and s_next < S:
         n = min(per_round, S - s_next)
-        if args.workload == "c4":
+        if args.workload in ("c4", "c4_levels"):
             xs = oracle.gen_ar_panel(seed, n, T, p_ar, s0=s_next)
+            if args.workload == "c4_levels":
+                xs = xs * 0.01 + 1e4        # the same two roundings as the device's mul_ / add_
         else:
             xs = oracle.gen_panel(seed, n, T, nan_p, s0=s_next)
+            if args.workload in ("c1_rule3", "c3_rule3"):
+                xs[~np.isnan(xs)] = 100.1
         if args.workload == "wire_decode":
             wire_bytes = oracle.wire_records(["k%07d" % i for i in range(n)], xs)
         t0 = time.perf_counter()
-        if args.workload in ("c3", "c1"):
+        if args.workload in ("c3", "c1", "c1_rule3", "c3_rule3"):
             rf, racf, _ = oracle.panel_fill_autocorr(xs, "linear", K, threads=threads)
         elif args.workload == "c2":
             rf = oracle.panel_fill_diff_ewma(xs, 0.2, threads=threads)
@@ -523,14 +563,31 @@ def cpu_baseline(args, S, T, K, seed, nan_p, out, acf, p_ar, smooth=None, gpar_r
                     np.frombuffer(wire_bytes, dtype=">f8", count=vn, offset=pos + 8 + kl).astype(np.float64)
                     pos += 8 + kl + 8 * vn
         else:
-            rf, _, _ = oracle.panel_ar_fit_remove(xs, p_ar, threads=threads)
+            rf, rc, rcoef = oracle.panel_ar_fit_remove(xs, p_ar, threads=threads)
         elapsed += time.perf_counter() - t0
         if s_next == 0 and rf is not None:
             g = {"ewma_fit": smooth, "garch_fit": gpar_ref}.get(args.workload, out)[:n].cpu().numpy()
-            if args.workload != "c4":
+            if args.workload not in ("c4", "c4_levels"):
                 exact = bool(np.array_equal(np.isnan(g), np.isnan(rf)) and
                              np.array_equal(np.nan_to_num(g), np.nan_to_num(rf)))
-            if args.workload in ("c3", "c1"):
+            else:
+                # the model: c, phi within 1e-10 elementwise of the reference (bit-identical where the AR
+                # rule flags the series); the residuals bit-exact given the device's own model
+                gc = ar_model[0][:n].cpu().numpy()
+                gph = ar_model[1][:n].cpu().numpy()
+                beta_d = np.column_stack([gc, gph])
+                beta_r = np.column_stack([rc, rcoef])
+                big = np.abs(beta_r) > 1e-6 * np.linalg.norm(beta_r, axis=1, keepdims=True)
+                rel = np.where(big, np.abs(beta_d - beta_r) / np.where(big, np.abs(beta_r), 1.0), 0.0)
+                worst_rel = float(rel.max())
+                own = np.array([oracle.ar_remove(xs[i], gc[i], gph[i]) for i in range(min(n, 64))])
+                exact = bool(np.array_equal(own.view(np.uint64), g[:own.shape[0]].view(np.uint64)))
+                ar_check = {"model_max_rel_err_elementwise": worst_rel,
+                            "model_bit_identical_series": int(np.sum(np.all(beta_d.view(np.uint64) ==
+                                                                            beta_r.view(np.uint64), axis=1))),
+                            "series_checked": int(n),
+                            "residuals_bit_exact_given_device_model": exact}
+            if args.workload in ("c3", "c1", "c1_rule3", "c3_rule3"):
                 ga = acf[:n].cpu().numpy()
                 fin = ~np.isnan(racf)
                 if fin.any():
@@ -548,7 +605,7 @@ def cpu_baseline(args, S, T, K, seed, nan_p, out, acf, p_ar, smooth=None, gpar_r
             "sample": "%d of the rank-0 series x %d steps (%.1f s of CPU work), oracle/sts_oracle.c restatement of "
                       "the reference loops, one series per thread (Spark local[%d] analogue); the JVM reference "
                       "cannot run here" % (done, T, elapsed, threads),
-            "sample_check": {"filled_bit_exact": exact, "acf_max_rel_err": worst_rel}}
+            "sample_check": ar_check if ar_check is not None else {"filled_bit_exact": exact, "acf_max_rel_err": worst_rel}}
 
 
 if __name__ == "__main__":

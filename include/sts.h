@@ -257,9 +257,16 @@ int sts_csv_parse(const char* text, int64_t len, int64_t max_records, int64_t* n
 
 /* ---- a11: Autoregression.fitModel(ts, p, noIntercept) (S/models/Autoregression.scala:38-53).
  * c[s] and coef[s*p + j] receive the model; 1 <= p <= 31.  T - p < p + 1 ->
- * STS_ERR_NOT_ENOUGH_DATA.  1e-10 relative to a Householder-QR OLS. */
+ * STS_ERR_NOT_ENOUGH_DATA.  1e-10 relative to commons-math3's Householder-QR OLS: a series
+ * the fast fit flags as ill-conditioned ("AR rule": level / spread, collinear lags, fragile
+ * coefficients), and every noIntercept series, is fitted with the reference's own QR
+ * operation order -- bit-identical to it. */
 int sts_ar_fit(const double* in, int64_t S, int64_t T, int64_t ld, int p, int no_intercept,
                double* c, double* coef, int32_t* err_per_series, void* stream);
+/* Diagnostic: how many of the S series the AR rule sends to the reference-order QR for
+ * sts_ar_fit(in, S, T, ld, p, no_intercept, ...) (synchronous; noIntercept: all S). */
+int sts_ar_rule_count(const double* in, int64_t S, int64_t T, int64_t ld, int p, int no_intercept,
+                      int64_t* count, void* stream);
 
 /* ---- f1b: ARIMA.fitModel(p, d, 0, ts, includeIntercept) -- the AR-only path
  * (S/models/ARIMA.scala:80-90): differencesOfOrderD(ts, d) (S/UnivariateTimeSeries.scala:

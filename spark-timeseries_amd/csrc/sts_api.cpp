@@ -594,6 +594,41 @@ int sts_ar_fit(const double* in, int64_t S, int64_t T, int64_t ld, int p, int no
     return ar_fit_common(in, nullptr, S, T, ld, ld, p, no_intercept, c, coef, err_per_series, stream, "ar_fit");
 }
 
+int sts_ar_rule_count(const double* in, int64_t S, int64_t T, int64_t ld, int p, int no_intercept, int64_t* count,
+                      void* stream) {
+    int r;
+    const char* name = "ar_rule_count";
+    if ((r = check_panel(in, S, T, ld, name))) return r;
+    if (!count) return fail(STS_ERR_BAD_ARG, "%s: null count", name);
+    if (p < 1 || p > 31) return fail(STS_ERR_BAD_ARG, "%s: AR order %d outside [1, 31]", name, p);
+    if (T - p < (int64_t)p + 1)
+        return fail(STS_ERR_NOT_ENOUGH_DATA, "%s: not enough data (%lld rows) for the number of predictors (%d)", name,
+                    (long long)(T - p), p);
+    *count = 0;
+    if (S == 0) return STS_OK;
+    if (no_intercept) {
+        *count = S;
+        return STS_OK;
+    }
+    if ((r = ensure_device())) return r;
+    hipStream_t st = as_stream(stream);
+    Scratch sc(st);
+    const size_t S8 = (size_t)S * sizeof(double);
+    HIP_TRY(sc.alloc(S8 * (size_t)(p + 1) + S * sizeof(int32_t) + 64), "hipMallocAsync(ar_rule_count)");
+    char* base = static_cast<char*>(sc.p);
+    sts::ArArgs a{};
+    a.in = in; a.out = nullptr; a.c = reinterpret_cast<double*>(base); a.coef = a.c + S;
+    a.err = reinterpret_cast<int32_t*>(base + S8 * (size_t)(p + 1));
+    a.S = S; a.T = T; a.ld_in = ld; a.ld_out = ld; a.p = p; a.no_intercept = 0;
+    uint32_t* dcount = reinterpret_cast<uint32_t*>(base + S8 * (size_t)(p + 1) + S * sizeof(int32_t));
+    HIP_TRY(sts::launch_ar_rule_count(a, dcount, st), name);
+    uint32_t h = 0;
+    HIP_TRY(hipMemcpyAsync(&h, dcount, sizeof(h), hipMemcpyDeviceToHost, st), name);
+    HIP_TRY(hipStreamSynchronize(st), name);
+    *count = (int64_t)h;
+    return STS_OK;
+}
+
 int sts_ar_fit_remove(const double* in, double* out, int64_t S, int64_t T, int64_t ld_in, int64_t ld_out, int p,
                       int no_intercept, double* c, double* coef, int32_t* err_per_series, void* stream) {
     if (!out) return fail(STS_ERR_BAD_ARG, "ar_fit_remove: null output");

@@ -29,6 +29,31 @@ typedef double d4 __attribute__((ext_vector_type(4)));
 constexpr int kPMax = 31;
 constexpr int kLd = kPMax + 2;   // row stride of the (p+1) x (p+1) Gram in LDS
 
+// ---- AR rule: which series the reference's own arithmetic must fit ----
+// commons-math3's Householder QR on the uncentred lag design drifts from the exact least-
+// squares solution with the level / spread ratio of the lag columns, with their collinearity,
+// and (in c) with how small the intercept is against the level it is the difference of.  The
+// fast kernels land ~1e-13 from exact; where the reference may sit farther than ~1e-11 from
+// exact the series is flagged and sts_ar_qr.hip recomputes it with the reference's operation
+// order (bit-exact to oracle/sts_oracle.c).  Thresholds from tools/ar_flag_study.py (11,240
+// series: walks, integrated walks, AR(1), noise, trends, sines at levels 0 .. 1e7, T 300 /
+// 2,520 / 6,000, p 1 / 2 / 5 / 8): inside all three bounds the reference is within 7e-14
+// (normwise) and 8.8e-12 (elementwise, over coefficients down to 1e-6 of the vector) of exact.
+// C4 panels sit at ratio 4.2, kappa 1.1, level 1.4: no C4 series is flagged.
+constexpr double kRuleRatio2 = 256.0;   // (|mean| / centred column rms)^2 < 16^2
+constexpr double kRuleKappa = 100.0;    // 1 / (scaled Cholesky pivot)^2 < 100
+constexpr double kRuleLevel = 100.0;    // |mean| / |c| < 100
+
+// the intercept half of the rule on a finished fit
+__device__ __forceinline__ bool ar_rule_level(double c, double mu) {
+    return !(__builtin_fabs(mu) < kRuleLevel * __builtin_fabs(c));
+}
+
+__device__ __forceinline__ void ar_rule_append(const ArArgs& a, int64_t s) {
+    const uint32_t i = atomicAdd(a.qr_count, 1u);
+    a.qr_list[i] = s;
+}
+
 template <bool STAGED, int PB>
 __global__ __launch_bounds__(64) void ar_fit_kernel(ArArgs a, int NT) {
     extern __shared__ __attribute__((aligned(16))) double lds[];
@@ -128,6 +153,7 @@ __global__ __launch_bounds__(64) void ar_fit_kernel(ArArgs a, int NT) {
     const bool intercept = !a.no_intercept;
     const double fm = (double)m;
     const bool bad = __builtin_isnan(sy) || __builtin_isnan(part);
+    bool illc = false;   // AR rule, conditioning half (lane 0)
     if (lane == 0 && !bad) {
         int status = STS_OK;
         if (intercept) {
@@ -136,10 +162,13 @@ __global__ __launch_bounds__(64) void ar_fit_kernel(ArArgs a, int NT) {
                 G[0 * kLd + j] -= cs[0] * cs[j] / fm;
             }
         }
+        const double mu2m = mu * mu * fm;
         // Cholesky in place on the lower triangle of the 1-based p x p block
         for (int j = 1; j <= p && status == STS_OK; j++) {
-            double d = G[j * kLd + j];
+            const double dg = G[j * kLd + j];   // centred column j's sum of squares
+            double d = dg;
             for (int k = 1; k < j; k++) d -= G[j * kLd + k] * G[j * kLd + k];
+            illc = illc || !(mu2m < kRuleRatio2 * dg) || !(d * kRuleKappa > dg);
             if (!(d > 0.0)) { status = STS_ERR_SINGULAR; break; }
             const double l = __builtin_sqrt(d);
             G[j * kLd + j] = l;
@@ -219,6 +248,12 @@ __global__ __launch_bounds__(64) void ar_fit_kernel(ArArgs a, int NT) {
             // un-shift: y = x - mu  =>  c = c' + mu * (1 - sum phi)
             sol[0] = intercept ? (sol[0] + dc / fm) + mu * (1.0 - sphi) : 0.0;
         }
+    }
+    if (lane == 0 && !bad && a.qr_list) {
+        // AR rule: a singular Cholesky, an ill-conditioned design or a fragile coefficient
+        // vector -> the reference's QR decides (sts_ar_qr.hip)
+        const bool flag = status != STS_OK || illc || ar_rule_level(sol[0], mu);
+        if (flag) ar_rule_append(a, s);
     }
     if (lane == 0) {
         if (bad || status != STS_OK) {
@@ -315,11 +350,13 @@ struct ArWaveLds {
 // is Y, rows / columns 1..p the lags; cs = the design's column sums; centring eliminates the
 // intercept; the Cholesky factor of the 1..p block overwrites A's lower triangle; phi = the
 // centred right-hand side A[1..p][0].  Returns false when a pivot is not positive (or NaN).
+// illc: the conditioning half of the AR rule (kRuleRatio2 on mu2m = mean^2 * m against each
+// centred column, kRuleKappa on each scaled pivot).
 template <int P>
 __device__ __forceinline__ bool ar_normal_chol(const double (&Pd)[P + 1], double sy, const double (&hd)[P],
                                                const double (&tl)[P], bool intercept, double ifm,
                                                double (&A)[P + 1][P + 1], double (&cs)[P + 1],
-                                               double (&phi)[P + 1]) {
+                                               double (&phi)[P + 1], double mu2m, bool& illc) {
 #pragma unroll
     for (int i = 1; i <= P; i++) {
 #pragma unroll
@@ -348,11 +385,16 @@ __device__ __forceinline__ bool ar_normal_chol(const double (&Pd)[P + 1], double
 #pragma unroll
             for (int k = 0; k <= i; k++) A[i][k] -= cs[i] * cs[k] * ifm;
     }
+    double dg[P + 1];
+#pragma unroll
+    for (int j = 1; j <= P; j++) dg[j] = A[j][j];
     bool ok = true;
+    illc = false;
 #pragma unroll
     for (int j = 1; j <= P; j++) {
         const double djj = A[j][j];
         ok = ok && (djj > 0.0);
+        illc = illc || !(mu2m < kRuleRatio2 * dg[j]) || !(djj * kRuleKappa > dg[j]);
         const double l = __builtin_sqrt(djj);
         A[j][j] = l;
 #pragma unroll
@@ -509,7 +551,8 @@ __global__ __launch_bounds__(64 * NWV, STS_AR_WAVES_PER_EU) void ar_fit_blk_kern
     const double ifm = 1.0 / fm;   // the fit is a 1e-10-tolerance path: multiply, no division chains
     const bool bad = __builtin_isnan(sy) || __builtin_isnan(part);
     double A[P + 1][P + 1], cs[P + 1], phi[P + 1];
-    const bool ok = ar_normal_chol<P>(Pd, sy, hd, tl, intercept, ifm, A, cs, phi);
+    bool illc;
+    const bool ok = ar_normal_chol<P>(Pd, sy, hd, tl, intercept, ifm, A, cs, phi, mu * mu * fm, illc);
     auto Lu = [&](int i, int k) -> double { return A[i][k]; };
     // reciprocals of L's diagonal once: the two solves' substitutions are chains of P steps,
     // and a division per step was ~10 instructions of dependent latency
@@ -613,6 +656,10 @@ __global__ __launch_bounds__(64 * NWV, STS_AR_WAVES_PER_EU) void ar_fit_blk_kern
 #pragma unroll
         for (int j = 0; j < P; j++) a.coef[s * P + j] = phi[1 + j];
         if (a.err) a.err[s] = status;
+        // AR rule (uniform in every lane; lane 0 appends): the reference's QR decides
+        if (!bad && a.qr_list &&
+            (!ok || illc || ar_rule_level(cpr, mu)))
+            ar_rule_append(a, s);
     }
     if (!a.out) return;
 
@@ -675,219 +722,6 @@ __global__ __launch_bounds__(64 * NWV, STS_AR_WAVES_PER_EU) void ar_fit_blk_kern
 #endif
 }
 
-// ---------------------------------------------------------------------------------------
-// noIntercept = true (Autoregression.fitModel(ts, maxLag, noIntercept = true)).  Without an
-// intercept the data cannot be centred, and on a price-level series (level L, steps sigma)
-// the lag columns are nearly collinear: cond(X) ~ L / sigma, so the normal equations lose
-// cond^2 (1e-4 relative at L / sigma = 1e6) and one refinement step does not recover it.
-// This kernel solves the same least-squares problem in the unimodular "difference basis":
-//   X beta = theta_1 x_{t-1} - sum_{j=1}^{p-1} theta_{j+1} d_{t-j},  d_u = x_u - x_{u-1},
-//   theta_m = sum_{j >= m} beta_j,
-// i.e. it regresses d_t = x_t - x_{t-1} on [x_{t-1}, d_{t-1}, .., d_{t-p+1}] (rows
-// t = p .. T-1, exactly the reference's rows) and maps back:
-//   beta_1 = alpha + gamma_1,  beta_j = gamma_j - gamma_{j-1},  beta_p = -gamma_{p-1},
-// with alpha = 1 + (coefficient of x_{t-1}), gamma_j = coefficient of d_{t-j}.  The level
-// now lives in one column only; the difference columns carry no level and are nearly
-// orthogonal to it, so the column-scaled Gram is well conditioned.  On a level series the
-// differences are exact (Sterbenz: x_u, x_{u-1} within a factor 2), so no information is
-// lost.  Gram entries are full-range lag products (d x d, x_{t-1} x d) minus at most p head /
-// tail terms, as in the kernels above; lane-0 Cholesky, then two refinement steps against
-// exact residual passes.  One wave per series, operands read through the L1 / L2 (this is
-// not a bench path: C4 fits with an intercept).
-template <int PB>
-__global__ __launch_bounds__(64) void ar_fit_noint_kernel(ArArgs a) {
-    __shared__ double G[(kPMax + 1) * kLd];   // [v0 = d_t | v1 = x_{t-1} | v2.. = d_{t-1}..]
-    __shared__ double sol[kPMax + 2];
-    __shared__ double zz[kPMax + 2];
-    __shared__ int stat;
-    const int lane = threadIdx.x;
-    const int64_t s = blockIdx.x;
-    const int64_t T = a.T;
-    const int p = a.p;
-    const double* xg = a.in + s * a.ld_in;
-    auto X = [&](int64_t u) -> double { return xg[u]; };
-    auto D = [&](int64_t u) -> double { return xg[u] - xg[u - 1]; };   // u >= 1
-
-    // ---- full-range sums: Q_k = sum_{u=1+k}^{T-1} d_u d_{u-k},
-    //      R_b = sum_{t=1+b}^{T-1} x_{t-1} d_{t-b}, X2 = sum_{u=p-1}^{T-2} x_u^2 ----
-    double Q[PB], R[PB], x2 = 0.0, nanchk = 0.0;
-#pragma unroll
-    for (int k = 0; k < PB; k++) Q[k] = R[k] = 0.0;
-    for (int64_t u = 1 + lane; u < T; u += 64) {
-        const double du = D(u);
-        const double xm = X(u - 1);
-        nanchk += du;
-        if (u - 1 >= p - 1 && u - 1 <= T - 2) x2 = __builtin_fma(xm, xm, x2);
-#pragma unroll
-        for (int k = 0; k < PB; k++) {
-            if (k < p && u - k >= 1) {
-                const double dk = D(u - k);
-                Q[k] = __builtin_fma(du, dk, Q[k]);
-                R[k] = __builtin_fma(xm, dk, R[k]);
-            }
-        }
-    }
-    nanchk += X(0);
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) {
-        x2 += __shfl_xor(x2, d);
-        nanchk += __shfl_xor(nanchk, d);
-    }
-#pragma unroll
-    for (int k = 0; k < PB; k++) {
-#pragma unroll
-        for (int d = 32; d >= 1; d >>= 1) {
-            Q[k] += __shfl_xor(Q[k], d);
-            R[k] += __shfl_xor(R[k], d);
-        }
-    }
-    const bool bad = __builtin_isnan(nanchk) || __builtin_isnan(x2);
-
-    // ---- Gram of v = [d_t, x_{t-1}, d_{t-1}, .., d_{t-p+1}] over rows t = p .. T-1 ----
-    // index i -> (is_x, d lag): i = 1 is x_{t-1}; i = 0 is lag 0; i >= 2 is lag i - 1
-    const int np1 = p + 1;
-    const int npair = np1 * (np1 + 1) / 2;
-    for (int idx = lane; idx < npair; idx += 64) {
-        int i = 0, rem = idx;
-        while (rem >= np1 - i) { rem -= np1 - i; i++; }
-        const int j = i + rem;                 // i <= j
-        double g;
-        if (i == 1 && j == 1) {
-            g = x2;
-        } else if (i == 1 || j == 1) {         // x_{t-1} x d_{t-lam}
-            const int o = (i == 1) ? j : i;
-            const int lam = o == 0 ? 0 : o - 1;
-            double r = 0.0;
-#pragma unroll
-            for (int k = 0; k < PB; k++)
-                if (k == lam) r = R[k];
-            for (int64_t t = 1 + lam; t <= p - 1; t++) r -= X(t - 1) * D(t - lam);   // head rows
-            g = r;
-        } else {                               // d_{t-la} x d_{t-lb}
-            int la = i == 0 ? 0 : i - 1, lb = j == 0 ? 0 : j - 1;
-            if (la > lb) { const int tmp = la; la = lb; lb = tmp; }
-            const int k = lb - la;
-            double q = 0.0;
-#pragma unroll
-            for (int kk = 0; kk < PB; kk++)
-                if (kk == k) q = Q[kk];
-            for (int64_t u = 1 + k; u <= p - la - 1; u++) q -= D(u) * D(u - k);        // head
-            for (int64_t u = T - la; u <= T - 1; u++) q -= D(u) * D(u - k);             // tail
-            g = q;
-        }
-        G[i * kLd + j] = g;
-        G[j * kLd + i] = g;
-    }
-    __syncthreads();
-
-    // ---- Cholesky of the 1..p block (lane 0); rhs = row 0 ----
-    if (lane == 0) {
-        int status = STS_OK;
-        if (!bad) {
-            for (int j = 1; j <= p && status == STS_OK; j++) {
-                double d = G[j * kLd + j];
-                for (int k = 1; k < j; k++) d -= G[j * kLd + k] * G[j * kLd + k];
-                if (!(d > 0.0)) { status = STS_ERR_SINGULAR; break; }
-                const double l = __builtin_sqrt(d);
-                G[j * kLd + j] = l;
-                for (int i = j + 1; i <= p; i++) {
-                    double v = G[i * kLd + j];
-                    for (int k = 1; k < j; k++) v -= G[i * kLd + k] * G[j * kLd + k];
-                    G[i * kLd + j] = v / l;
-                }
-            }
-            if (status == STS_OK) {
-                for (int i = 1; i <= p; i++) sol[i] = G[0 * kLd + i];
-            }
-        }
-        stat = status;
-    }
-    __syncthreads();
-    auto solve_lane0 = [&](double* z) {
-        for (int i = 1; i <= p; i++) {
-            double v = z[i];
-            for (int k = 1; k < i; k++) v -= G[i * kLd + k] * z[k];
-            z[i] = v / G[i * kLd + i];
-        }
-        for (int i = p; i >= 1; i--) {
-            double v = z[i];
-            for (int k = i + 1; k <= p; k++) v -= G[k * kLd + i] * z[k];
-            z[i] = v / G[i * kLd + i];
-        }
-    };
-    const int status = stat;
-    const bool ok = !bad && status == STS_OK;
-    if (ok && lane == 0) solve_lane0(sol);
-    __syncthreads();
-
-    // ---- refinement: e_t = d_t - sum_i sol_i v_i(t); g_i = sum e_t v_i(t) ----
-    for (int it = 0; it < 2 && ok; it++) {
-        double g[PB + 1];
-#pragma unroll
-        for (int k = 0; k <= PB; k++) g[k] = 0.0;
-        for (int64_t t = p + lane; t < T; t += 64) {
-            const double xm = X(t - 1);
-            double e = D(t) - sol[1] * xm;
-#pragma unroll
-            for (int k = 1; k < PB; k++)
-                if (k < p) e -= sol[k + 1] * D(t - k);
-            g[1] = __builtin_fma(e, xm, g[1]);
-#pragma unroll
-            for (int k = 1; k < PB; k++)
-                if (k < p) g[k + 1] = __builtin_fma(e, D(t - k), g[k + 1]);
-        }
-#pragma unroll
-        for (int k = 1; k <= PB; k++) {
-            if (k <= p) {
-#pragma unroll
-                for (int d = 32; d >= 1; d >>= 1) g[k] += __shfl_xor(g[k], d);
-                if (lane == 0) zz[k] = g[k];
-            }
-        }
-        __syncthreads();
-        if (lane == 0) {
-            solve_lane0(zz);
-            for (int k = 1; k <= p; k++) sol[k] += zz[k];
-        }
-        __syncthreads();
-    }
-
-    // ---- back to the lag basis ----
-    if (lane == 0) {
-        double beta[kPMax + 1];
-        if (ok) {
-            // alpha = 1 + sol[1]; gamma_j = sol[j + 1] (j = 1 .. p-1)
-            if (p == 1) {
-                beta[1] = 1.0 + sol[1];
-            } else {
-                beta[1] = (1.0 + sol[1]) + sol[2];
-                for (int j = 2; j <= p - 1; j++) beta[j] = sol[j + 1] - sol[j];
-                beta[p] = -sol[p];
-            }
-        } else {
-            for (int j = 1; j <= p; j++) beta[j] = __builtin_nan("");
-        }
-        a.c[s] = ok ? 0.0 : __builtin_nan("");
-        for (int j = 1; j <= p; j++) {
-            a.coef[s * p + j - 1] = beta[j];
-            sol[j] = beta[j];
-        }
-        sol[0] = ok ? 0.0 : __builtin_nan("");
-        if (a.err) a.err[s] = bad ? STS_OK : status;
-    }
-    if (!a.out) return;
-    __syncthreads();
-
-    // ---- fused removeTimeDependentEffects (bit-exact order, c = 0) ----
-    const double c = sol[0];
-    double* dst = a.out + s * a.ld_out;
-    for (int64_t t = lane; t < T; t += 64) {
-        double d = X(t) - c;
-        for (int j = 0; j < p && t - j - 1 >= 0; j++) d -= X(t - j - 1) * sol[1 + j];
-        dst[t] = d;
-    }
-}
-
 }  // namespace
 
 #ifdef STS_STAMPS
@@ -898,14 +732,82 @@ extern "C" int sts_debug_ar_stamps(unsigned long long* out16) {
 }
 #endif
 
-hipError_t launch_ar_fit(const ArArgs& a, hipStream_t st) {
-    if (a.S <= 0) return hipSuccess;
-    if (a.p < 1 || a.p > kPMax) return hipErrorInvalidValue;
-    if (a.no_intercept) {   // difference-basis solve (see ar_fit_noint_kernel)
-        if (a.p <= 8) hipLaunchKernelGGL((ar_fit_noint_kernel<8>), dim3((unsigned)a.S), dim3(64), 0, st, a);
-        else hipLaunchKernelGGL((ar_fit_noint_kernel<kPMax>), dim3((unsigned)a.S), dim3(64), 0, st, a);
-        return hipGetLastError();
+// scratch of the one-wave-per-series QR form (p > 8): slots of m x ldc doubles, at most
+// 2,048 slots and 1 GiB
+static int ar_qr_slots(const ArArgs& a, int64_t n) {
+    const size_t slot = ar_qr_wave_slot_elems(a.T, a.p, a.no_intercept) * sizeof(double);
+    int64_t k = (int64_t)((size_t(1) << 30) / (slot ? slot : 1));
+    if (k > 2048) k = 2048;
+    if (k > n) k = n;
+    return (int)(k < 1 ? 1 : k);
+}
+
+static hipError_t launch_ar_fast(const ArArgs& a, hipStream_t st);
+
+hipError_t launch_ar_fit(const ArArgs& a0, hipStream_t st) {
+    if (a0.S <= 0) return hipSuccess;
+    if (a0.p < 1 || a0.p > kPMax) return hipErrorInvalidValue;
+    ArArgs a = a0;
+    // A/B build only: the one-wave-per-series QR form for every p (its parity tests)
+    const bool force_wave = ab_knob("STS_AR_QR_WAVE") != nullptr;
+    const bool wave = force_wave || !ar_qr_lane_ok(a.p);
+    hipError_t e;
+    if (a.no_intercept) {
+        // noIntercept: every series through the reference's QR: without the
+        // intercept the lag columns keep the level, and no fast basis tracks the reference's
+        // rounding closely enough on price levels
+        double* scr = nullptr;
+        int slots = 0;
+        if (wave) {
+            slots = ar_qr_slots(a, a.S);
+            e = hipMallocAsync(reinterpret_cast<void**>(&scr),
+                               (size_t)slots * ar_qr_wave_slot_elems(a.T, a.p, 1) * sizeof(double), st);
+            if (e != hipSuccess) return e;
+        }
+        e = launch_ar_qr(a, nullptr, nullptr, a.S, scr, slots, force_wave, st);
+        if (scr) (void)hipFreeAsync(scr, st);
+        return e;
     }
+    // intercept: the fast fit, the rule's list of flagged series, the reference's QR on the list
+    void* buf = nullptr;
+    const size_t list_bytes = ((size_t)a.S * sizeof(int64_t) + 255) & ~size_t(255);
+    e = hipMallocAsync(&buf, list_bytes + 256, st);
+    if (e != hipSuccess) return e;
+    a.qr_list = static_cast<int64_t*>(buf);
+    a.qr_count = reinterpret_cast<uint32_t*>(static_cast<char*>(buf) + list_bytes);
+    e = hipMemsetAsync(a.qr_count, 0, sizeof(uint32_t), st);
+    if (e == hipSuccess) e = launch_ar_fast(a, st);
+    double* scr = nullptr;
+    int slots = 0;
+    if (e == hipSuccess && wave) {
+        slots = ar_qr_slots(a, a.S);
+        e = hipMallocAsync(reinterpret_cast<void**>(&scr),
+                           (size_t)slots * ar_qr_wave_slot_elems(a.T, a.p, 0) * sizeof(double), st);
+    }
+    if (e == hipSuccess) e = launch_ar_qr(a, a.qr_list, a.qr_count, 0, scr, slots, force_wave, st);
+    if (scr) (void)hipFreeAsync(scr, st);
+    (void)hipFreeAsync(buf, st);
+    return e;
+}
+
+hipError_t launch_ar_rule_count(const ArArgs& a0, uint32_t* count, hipStream_t st) {
+    if (a0.S <= 0 || a0.no_intercept) return hipSuccess;
+    if (a0.p < 1 || a0.p > kPMax) return hipErrorInvalidValue;
+    ArArgs a = a0;
+    a.out = nullptr;
+    void* buf = nullptr;
+    hipError_t e = hipMallocAsync(&buf, (size_t)a.S * sizeof(int64_t), st);
+    if (e != hipSuccess) return e;
+    a.qr_list = static_cast<int64_t*>(buf);
+    a.qr_count = count;
+    e = hipMemsetAsync(count, 0, sizeof(uint32_t), st);
+    if (e == hipSuccess) e = launch_ar_fast(a, st);
+    (void)hipFreeAsync(buf, st);
+    return e;
+}
+
+// the fast fit kernels (intercept)
+static hipError_t launch_ar_fast(const ArArgs& a, hipStream_t st) {
     // register path: p <= 8, T <= 64 * 40 (lane blocks of B steps, B in {8, 16, 24, 32, 40})
     if (a.p <= kRegPB && a.T <= 64 * 40 && !ab_knob("STS_AR_STAGED")) {
         constexpr int NWV = kRegWaves;

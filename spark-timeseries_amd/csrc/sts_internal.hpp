@@ -134,8 +134,20 @@ struct ArArgs {
     int32_t* err;
     int64_t S, T, ld_in, ld_out;
     int p, no_intercept;
+    // AR rule (sts_ar.hip / sts_ar_qr.hip): series the fast fit flags, appended by the fit
+    // kernels (set by launch_ar_fit, not by callers)
+    int64_t* qr_list;
+    uint32_t* qr_count;
 };
 hipError_t launch_ar_fit(const ArArgs& a, hipStream_t st);
+// the fast fit kernels only, flagged series counted into *count (device; AR rule diagnostic)
+hipError_t launch_ar_rule_count(const ArArgs& a, uint32_t* count, hipStream_t st);
+// the reference's Householder QR on the listed series (list == nullptr: series 0 .. n_direct-1;
+// otherwise list[0 .. *count-1]); scratch = slots x ar_qr_wave_slot_elems doubles for p > 8
+bool ar_qr_lane_ok(int p);
+size_t ar_qr_wave_slot_elems(int64_t T, int p, int no_intercept);
+hipError_t launch_ar_qr(const ArArgs& a, const int64_t* list, const uint32_t* count, int64_t n_direct,
+                        double* scratch, int slots, bool force_wave, hipStream_t st);
 
 // EWMA.fitModel and EWMAModel.sse / gradient (sts_ewma_fit.hip)
 struct EwmaFitArgs {

@@ -440,7 +440,8 @@ __global__ __launch_bounds__(64 * kRowWpg) void recur_row_kernel(RecurArgs a) {
             ep = e;
         }
         const double eprev = dpp_shift<0x138>(e);
-        const bool redo = rl > 0 && t0 < T && dbits(eprev) != dbits(ein);
+        // dead rows (past S) never redo: their garbage NaN patterns must not force rounds
+        const bool redo = act && rl > 0 && dbits(eprev) != dbits(ein);
         if (!__ballot(redo)) break;
         ein = redo ? eprev : ein;
         dirty = redo;

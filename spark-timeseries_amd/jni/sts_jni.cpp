@@ -27,6 +27,8 @@
 
 #include <cstdint>
 #include <cstring>
+#include <memory>
+#include <new>
 #include <vector>
 
 #include "sts.h"
@@ -38,7 +40,7 @@ struct Cls {
     jclass cls = nullptr;
     jmethodID ctor = nullptr;
 };
-Cls g_iae, g_uoe, g_npe, g_rte;              // java.lang.*(String)
+Cls g_iae, g_uoe, g_npe, g_rte, g_oome;      // java.lang.*(String)
 Cls g_singular;                               // commons-math3 SingularMatrixException()
 Cls g_tme, g_tmi;                             // TooManyEvaluations / TooManyIterationsException(Number)
 Cls g_miae;                                   // MathIllegalArgumentException(Localizable, Object...)
@@ -150,19 +152,26 @@ struct PinBuf {
 };
 thread_local PinBuf t_in, t_out;
 
+// The heap fallback of a call buffer, allocated without exceptions (a std::bad_alloc out of a
+// JNIEXPORT function would abort the JVM): a failure becomes a pending
+// java.lang.OutOfMemoryError and a null buffer; every native returns as soon as it sees the
+// pending exception.
+double* heap_buf(JNIEnv* env, std::unique_ptr<double[]>& own, size_t n) {
+    own.reset(n <= SIZE_MAX / sizeof(double) ? new (std::nothrow) double[n] : nullptr);
+    if (!own) throw_string(env, g_oome.cls ? g_oome : g_rte, "sts_jni: cannot allocate the partition buffer");
+    return own.get();
+}
+
 // One call's panel buffer: the thread's pinned buffer, or -- when pinned memory cannot be had
 // -- the heap (the staging pipeline handles pageable memory too, at a lower PCIe rate).
 struct CallBuf {
     PinBuf* pb;
-    std::vector<double> own;
+    std::unique_ptr<double[]> own;
     double* p = nullptr;
-    CallBuf(PinBuf* b, int64_t count) : pb(b) {
+    CallBuf(JNIEnv* env, PinBuf* b, int64_t count) : pb(b) {
         const size_t n = (size_t)(count > 0 ? count : 1);
         p = pb->get(n * sizeof(double));
-        if (!p) {
-            own.resize(n);
-            p = own.data();
-        }
+        if (!p) p = heap_buf(env, own, n);
     }
     ~CallBuf() { pb->trim(); }
 };
@@ -184,21 +193,18 @@ struct Region {
     JNIEnv* env;
     jdoubleArray arr;
     jsize n;
-    std::vector<double> own;
+    std::unique_ptr<double[]> own;
     double* p = nullptr;
     PinBuf* pb_ = nullptr;
     // pinned: use the thread's pinned buffer `pb` (the panel); copy_in: read the array
     Region(JNIEnv* e, jdoubleArray a, int64_t count, bool copy_in, PinBuf* pb = nullptr)
         : env(e), arr(a), n((jsize)count), pb_(pb) {
         if (pb) p = pb->get((size_t)(count > 0 ? count : 1) * sizeof(double));
-        if (!p) {
-            own.resize((size_t)(count > 0 ? count : 1));
-            p = own.data();
-        }
-        if (copy_in && count > 0) env->GetDoubleArrayRegion(arr, 0, n, p);
+        if (!p) p = heap_buf(env, own, (size_t)(count > 0 ? count : 1));
+        if (p && copy_in && count > 0) env->GetDoubleArrayRegion(arr, 0, n, p);
     }
     void copy_out() {
-        if (n > 0 && !env->ExceptionCheck()) env->SetDoubleArrayRegion(arr, 0, n, p);
+        if (p && n > 0 && !env->ExceptionCheck()) env->SetDoubleArrayRegion(arr, 0, n, p);
     }
     ~Region() {
         if (pb_) pb_->trim();
@@ -288,6 +294,7 @@ JNIEXPORT jint JNICALL JNI_OnLoad(JavaVM* vm, void*) {
     g_iae = resolve(env, "java/lang/IllegalArgumentException", "(Ljava/lang/String;)V");
     g_uoe = resolve(env, "java/lang/UnsupportedOperationException", "(Ljava/lang/String;)V");
     g_npe = resolve(env, "java/lang/NullPointerException", "(Ljava/lang/String;)V");
+    g_oome = resolve(env, "java/lang/OutOfMemoryError", "(Ljava/lang/String;)V");
     g_singular = resolve(env, "org/apache/commons/math3/linear/SingularMatrixException", "()V");
     g_tme = resolve(env, "org/apache/commons/math3/exception/TooManyEvaluationsException", "(Ljava/lang/Number;)V");
     g_tmi = resolve(env, "org/apache/commons/math3/exception/TooManyIterationsException", "(Ljava/lang/Number;)V");
@@ -327,6 +334,7 @@ JNIEXPORT void JNICALL Java_com_cloudera_sparkts_StsNative_fill(JNIEnv* env, jcl
         !check_len(env, out, n, "fill: dest array shorter than S * T"))
         return;
     Region ri(env, in, n, true, &t_in), ro(env, out, n, false, &t_out);
+    if (env->ExceptionCheck()) return;
     const int st = sts_fill_host(ri.p, ro.p, S, T, T, code, nullptr);
     if (st == STS_OK) ro.copy_out();
     throw_for(env, st);
@@ -341,6 +349,7 @@ JNIEXPORT void JNICALL Java_com_cloudera_sparkts_StsNative_autocorr(JNIEnv* env,
         !check_len(env, acf, na, "autocorr: result array shorter than S * numLags"))
         return;
     Region ri(env, in, n, true, &t_in), ra(env, acf, na, false);
+    if (env->ExceptionCheck()) return;
     const int st = sts_autocorr_host(ri.p, S, T, T, numLags, ra.p);
     if (st == STS_OK) ra.copy_out();
     throw_for(env, st);
@@ -362,6 +371,7 @@ JNIEXPORT void JNICALL Java_com_cloudera_sparkts_StsNative_fillAutocorr(JNIEnv* 
         !check_len(env, acf, na, "fillAutocorr: result array shorter than S * numLags"))
         return;
     Region ri(env, in, n, true, &t_in), rf(env, filled, n, false, &t_out), ra(env, acf, na, false);
+    if (env->ExceptionCheck()) return;
     const int st = sts_fill_autocorr_host(ri.p, rf.p, S, T, T, code, numLags, ra.p, nullptr);
     if (st == STS_OK) {
         rf.copy_out();
@@ -381,11 +391,13 @@ JNIEXPORT void JNICALL Java_com_cloudera_sparkts_StsNative_differencesAtLag(JNIE
     int st;
     if (env->IsSameObject(in, dest)) {
         Region r(env, in, n, true, &t_in);
+        if (env->ExceptionCheck()) return;
         st = sts_diff_at_lag_host(r.p, r.p, S, T, T, lag, start);
         if (st == STS_OK) r.copy_out();
     } else {
         // dest is read as well (lag 0 leaves it untouched): copy it in too
         Region ri(env, in, n, true, &t_in), ro(env, dest, n, true, &t_out);
+        if (env->ExceptionCheck()) return;
         st = sts_diff_at_lag_host(ri.p, ro.p, S, T, T, lag, start);
         if (st == STS_OK) ro.copy_out();
     }
@@ -403,6 +415,7 @@ JNIEXPORT void JNICALL Java_com_cloudera_sparkts_StsNative_lag(JNIEnv* env, jcla
         !check_len(env, out, no, "lag: result array shorter than S * (T - maxLag) * (maxLag + inc)"))
         return;
     Region ri(env, in, n, true, &t_in), ro(env, out, no, false, &t_out);
+    if (env->ExceptionCheck()) return;
     const int st = sts_lag_matrix_host(ri.p, ro.p, S, T, T, maxLag, includeOriginal ? 1 : 0);
     if (st == STS_OK) ro.copy_out();
     throw_for(env, st);
@@ -419,13 +432,16 @@ JNIEXPORT void JNICALL Java_com_cloudera_sparkts_StsNative_ewma(JNIEnv* env, jcl
         !check_len(env, smoothing, S, "EWMA: smoothing array shorter than S"))
         return;
     Region rs(env, smoothing, S, true);
+    if (env->ExceptionCheck()) return;
     int st;
     if (env->IsSameObject(in, dest)) {
         Region r(env, in, n, true, &t_in);
+        if (env->ExceptionCheck()) return;
         st = add ? sts_ewma_add_host(r.p, r.p, S, T, T, rs.p) : sts_ewma_remove_host(r.p, r.p, S, T, T, rs.p);
         if (st == STS_OK) r.copy_out();
     } else {
         Region ri(env, in, n, true, &t_in), ro(env, dest, n, false, &t_out);
+        if (env->ExceptionCheck()) return;
         st = add ? sts_ewma_add_host(ri.p, ro.p, S, T, T, rs.p) : sts_ewma_remove_host(ri.p, ro.p, S, T, T, rs.p);
         if (st == STS_OK) ro.copy_out();
     }
@@ -448,6 +464,7 @@ JNIEXPORT void JNICALL Java_com_cloudera_sparkts_StsNative_fillDiffEwma(JNIEnv* 
         !check_len(env, smoothing, S, "fillDiffEwma: smoothing array shorter than S"))
         return;
     Region ri(env, in, n, true, &t_in), ro(env, out, n, false, &t_out), rs(env, smoothing, S, true);
+    if (env->ExceptionCheck()) return;
     const int st = sts_fill_diff_ewma_host(ri.p, ro.p, S, T, T, code, lag, rs.p, nullptr);
     if (st == STS_OK) ro.copy_out();
     throw_for(env, st);
@@ -461,6 +478,7 @@ JNIEXPORT void JNICALL Java_com_cloudera_sparkts_StsNative_ewmaFit(JNIEnv* env, 
         !check_len(env, smoothing, S, "ewmaFit: result array shorter than S"))
         return;
     Region ri(env, in, n, true, &t_in), rs(env, smoothing, S, false);
+    if (env->ExceptionCheck()) return;
     const int st = sts_ewma_fit_host(ri.p, S, T, T, rs.p, nullptr);
     if (st == STS_OK) rs.copy_out();
     throw_for(env, st);
@@ -474,6 +492,7 @@ JNIEXPORT void JNICALL Java_com_cloudera_sparkts_StsNative_garchFit(JNIEnv* env,
         !check_len(env, params, prod(S, 3), "garchFit: result array shorter than 3 S"))
         return;
     Region ri(env, in, n, true, &t_in), rp(env, params, prod(S, 3), false);
+    if (env->ExceptionCheck()) return;
     const int st = sts_garch_fit_host(ri.p, S, T, T, rp.p, nullptr);
     if (st == STS_OK) rp.copy_out();
     throw_for(env, st);
@@ -490,6 +509,7 @@ JNIEXPORT void JNICALL Java_com_cloudera_sparkts_StsNative_argarchFit(JNIEnv* en
         !check_len(env, params, prod(S, 3), "argarchFit: params array shorter than 3 S"))
         return;
     Region ri(env, in, n, true, &t_in), rc(env, c, S, false), rf(env, phi, S, false), rp(env, params, prod(S, 3), false);
+    if (env->ExceptionCheck()) return;
     const int st = sts_argarch_fit_host(ri.p, S, T, T, rc.p, rf.p, rp.p, nullptr);
     if (st == STS_OK) {
         rc.copy_out();
@@ -508,6 +528,7 @@ JNIEXPORT void JNICALL Java_com_cloudera_sparkts_StsNative_arFit(JNIEnv* env, jc
         !check_len(env, coef, prod(S, p), "arFit: coefficient array shorter than S * maxLag"))
         return;
     Region ri(env, in, n, true, &t_in), rc(env, c, S, false), rk(env, coef, prod(S, p), false);
+    if (env->ExceptionCheck()) return;
     const int st = sts_ar_fit_host(ri.p, S, T, T, p, noIntercept ? 1 : 0, rc.p, rk.p, nullptr);
     if (st == STS_OK) {
         rc.copy_out();
@@ -530,6 +551,7 @@ JNIEXPORT void JNICALL Java_com_cloudera_sparkts_StsNative_arFitRemove(JNIEnv* e
         return;
     Region ri(env, in, n, true, &t_in), ro(env, out, n, false, &t_out), rc(env, c, S, false),
         rk(env, coef, prod(S, p), false);
+    if (env->ExceptionCheck()) return;
     const int st = sts_ar_fit_remove_host(ri.p, ro.p, S, T, T, p, noIntercept ? 1 : 0, rc.p, rk.p, nullptr);
     if (st == STS_OK) {
         ro.copy_out();
@@ -549,13 +571,16 @@ JNIEXPORT void JNICALL Java_com_cloudera_sparkts_StsNative_ar(JNIEnv* env, jclas
         (p > 0 && !check_len(env, coef, prod(S, p), "AR: coefficient array shorter than S * p")))
         return;
     Region rc(env, c, S, true), rk(env, coef, p > 0 ? prod(S, p) : 0, p > 0);
+    if (env->ExceptionCheck()) return;
     int st;
     if (env->IsSameObject(in, dest)) {
         Region r(env, in, n, true, &t_in);
+        if (env->ExceptionCheck()) return;
         st = add ? sts_ar_add_host(r.p, r.p, S, T, T, rc.p, rk.p, p) : sts_ar_remove_host(r.p, r.p, S, T, T, rc.p, rk.p, p);
         if (st == STS_OK) r.copy_out();
     } else {
         Region ri(env, in, n, true, &t_in), ro(env, dest, n, false, &t_out);
+        if (env->ExceptionCheck()) return;
         st = add ? sts_ar_add_host(ri.p, ro.p, S, T, T, rc.p, rk.p, p)
                  : sts_ar_remove_host(ri.p, ro.p, S, T, T, rc.p, rk.p, p);
         if (st == STS_OK) ro.copy_out();
@@ -575,7 +600,8 @@ JNIEXPORT jobjectArray JNICALL Java_com_cloudera_sparkts_StsNative_fillRecords(J
     const int code = method_code(env, method);
     if (code < 0) return nullptr;
     const int64_t n = prod(S, T);
-    CallBuf bin(&t_in, n), bout(&t_out, n);
+    CallBuf bin(env, &t_in, n), bout(env, &t_out, n);
+    if (env->ExceptionCheck()) return nullptr;
     double *in = bin.p, *out = bout.p;
     if (!gather_records(env, recs, S, T, in)) return nullptr;
     const int st = sts_fill_host(in, out, S, T, T, code, nullptr);
@@ -593,10 +619,12 @@ JNIEXPORT jobjectArray JNICALL Java_com_cloudera_sparkts_StsNative_fillDiffEwmaR
     if (!check_len(env, smoothing, S, "fillDiffEwmaRecords: smoothing array shorter than the record count"))
         return nullptr;
     const int64_t n = prod(S, T);
-    CallBuf bin(&t_in, n), bout(&t_out, n);
+    CallBuf bin(env, &t_in, n), bout(env, &t_out, n);
+    if (env->ExceptionCheck()) return nullptr;
     double *in = bin.p, *out = bout.p;
     if (!gather_records(env, recs, S, T, in)) return nullptr;
     Region rs(env, smoothing, S, true);
+    if (env->ExceptionCheck()) return nullptr;
     const int st = sts_fill_diff_ewma_host(in, out, S, T, T, code, lag, rs.p, nullptr);
     if (st != STS_OK) return throw_for(env, st), nullptr;
     return scatter_records(env, out, S, T);
@@ -613,10 +641,12 @@ JNIEXPORT jobjectArray JNICALL Java_com_cloudera_sparkts_StsNative_arFitRemoveRe
         !check_len(env, coef, prod(S, p), "arFitRemoveRecords: coefficient array shorter than S * maxLag"))
         return nullptr;
     const int64_t n = prod(S, T);
-    CallBuf bin(&t_in, n), bout(&t_out, n);
+    CallBuf bin(env, &t_in, n), bout(env, &t_out, n);
+    if (env->ExceptionCheck()) return nullptr;
     double *in = bin.p, *out = bout.p;
     if (!gather_records(env, recs, S, T, in)) return nullptr;
     Region rc(env, c, S, false), rk(env, coef, prod(S, p), false);
+    if (env->ExceptionCheck()) return nullptr;
     const int st = sts_ar_fit_remove_host(in, out, S, T, T, p, noIntercept ? 1 : 0, rc.p, rk.p, nullptr);
     if (st != STS_OK) return throw_for(env, st, (jint)(T - p), p), nullptr;
     rc.copy_out();

@@ -366,6 +366,18 @@ int main() {
           "records longer than T -> IllegalArgumentException");
     env->ExceptionClear();
 
+    // ---- an oversized partition: no pinned or heap buffer can be had -> OutOfMemoryError, not an
+    //      abort (std::bad_alloc must not leave a JNIEXPORT function) ----
+    const jlong huge = jlong(1) << 40;   // 8 TB of doubles for one record
+    check(!Java_com_cloudera_sparkts_StsNative_fillRecords(env, cls, recs, huge, new_string("linear")) &&
+              pending_class() == "java/lang/OutOfMemoryError",
+          "oversized partition -> OutOfMemoryError");
+    env->ExceptionClear();
+    check(!Java_com_cloudera_sparkts_StsNative_arFitRemoveRecords(env, cls, recs, huge, 2, 0, jc, jk) &&
+              pending_class() == "java/lang/OutOfMemoryError",
+          "oversized AR partition -> OutOfMemoryError");
+    env->ExceptionClear();
+
     // ---- the panel form still works (one shared array in, one out) ----
     std::vector<double> flat;
     for (int s = 0; s < S; s++) flat.insert(flat.end(), data[s].begin(), data[s].end());

@@ -503,3 +503,41 @@ def test_gpu_autocorr_ill_conditioned(torch, request, T, K, kernel):
             assert np.array_equal(filled.view(np.uint64), rf.view(np.uint64)), "fill not bit-exact"
         e = rel_err(got, ref)
         assert e <= RTOL, "rel err %.3g (T=%d K=%d %s %s)" % (e, T, K, method, kernel)
+
+
+def returns_rows(T, seed):
+    """White noise and differenced random walks (returns): every correlation is O(1 / sqrt(T))
+    and some lags land near 0 -- below the reference's own rounding noise."""
+    rng = np.random.default_rng(seed)
+    walk = 100.0 + np.cumsum(rng.standard_normal(T + 1) * 0.01)
+    return np.array([rng.standard_normal(T), 1e-3 * rng.standard_normal(T) + 5e-4,
+                     np.diff(walk), np.diff(np.log(np.abs(walk)))])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("T,K", [(2520, 20), (16384 + 77, 60), (982_800, 60)])
+@pytest.mark.parametrize("method", ["linear", None])
+def test_gpu_autocorr_returns_tolerance_contract(torch, T, K, method):
+    """rule 3 does not flag a lag whose one-pass error is below the
+    reference's own rounding noise (eps sqrt(N), sts_acf.hpp acf_suspect), so on returns-like
+    rows -- white noise, differenced random walks, log returns -- the contract is explicit:
+    |acf - ref| <= 1e-10 |ref| + noise_floor(lag) (64 eps sqrt(N) sum|d1 d2| / sqrt(v1 v2), the
+    reference's own rounding level); every lag with |ref| above 100x that floor meets the plain
+    1e-10 relative bar.  T = 2 520 / K = 20 runs the short kernel (fill linear), 16 461 the
+    segment kernel, 982 800 the tile kernel."""
+    x = returns_rows(T, T + K)
+    if method is not None:
+        x = with_nans(x, np.random.default_rng(T))
+    filled, got = run_fill_acf(torch, x, method, K)
+    if method is None:
+        src, ref = x, np.array([oracle.autocorr(r, K) for r in x])
+    else:
+        src, ref, err = oracle.panel_fill_autocorr(x, method, K, threads=8)
+        assert (err == 0).all()
+        assert np.array_equal(filled.view(np.uint64), src.view(np.uint64)), "fill not bit-exact"
+    floor = np.array([noise_floor(r, K) for r in src])
+    e = within(got, ref, floor)
+    assert e <= 1.0, "error %.3g x (1e-10 rel + noise floor)" % e
+    big = np.abs(ref) > 100.0 * floor
+    assert big.mean() > 0.5
+    assert rel_err(got[big], ref[big]) <= RTOL, rel_err(got[big], ref[big])

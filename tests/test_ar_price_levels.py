@@ -1,23 +1,18 @@
-"""AR(p) fit on price-level series (VERDICT r1 "What's weak" #4).
+"""AR(p) fit on ill-conditioned series: the AR rule (sts_ar.hip + sts_ar_qr.hip).
 
 Autoregression.fitModel (S/models/Autoregression.scala:38-53) solves OLS on the uncentred
-lag matrix (+ intercept column) with commons-math3's Householder QR.  For a random walk at
-level L with step sigma the design is ill-conditioned (the intercept column and the lag
-columns are nearly collinear): the reference's own result then drifts from the exact
-least-squares solution by about 1e-16 * L / sigma (measured below: 2e-7 at L = 1e6,
-sigma = 1e-2).  The device fits on centred data (exact algebra for the intercept model) with
-a Cholesky solve plus one refinement step (spark-timeseries_amd/csrc/sts_ar.hip).
+lag matrix (+ intercept column) with commons-math3's Householder QR.  On a price level (level L
+far above the series' spread), on nearly collinear lags, or where the intercept is a small
+difference of large means, the reference itself drifts from the exact least-squares solution --
+measured below up to ~5e-8 at L = 1e6, sigma = 1e-2 (tools/ar_flag_study.py: up to 1e-5 on
+harder families).  The device cannot be "more exact" and still match: it flags such series
+(the rule's three bounds) and fits them with the reference's own operation order, bit for
+bit; the rest stay on the fast centred normal equations, where the reference is within
+~7e-14 (normwise) of exact.  Every noIntercept fit takes the reference order.
 
-So every case is measured against the EXACT least-squares solution of the same doubles
-(rational arithmetic, exact_ols below).  Relative error of a coefficient vector is normwise,
-||b - b_ref|| / ||b_ref|| (a coefficient much smaller than the vector inherits the problem's
-conditioning elementwise; the elementwise figures are recorded, not asserted), and
-  * where the reference itself is accurate (within 1e-11 of exact) the device must agree
-    with it within 1e-10;
-  * everywhere the device must be at least as close to the exact solution as the reference
-    (within a factor 2 plus 1e-12).
-Measured on MI355X: the device stays within 7e-13 of exact in every case, the
-reference drifts up to 6e-8 from it at L = 1e6, sigma = 1e-2.
+The bar: device vs oracle <= 1e-10 ELEMENTWISE on every row -- all LEVELS x
+p in {1, 5, 8} x both intercept modes x every kernel -- with the distance to the exact solution
+recorded as information only (STS_AR_LEVELS_JSON).
 """
 import json
 import os
@@ -29,6 +24,7 @@ import pytest
 import oracle
 
 LEVELS = [(1e2, 1.0), (1e3, 1.0), (1e4, 1.0), (1e4, 1e-2), (1e6, 1.0), (1e6, 1e-2)]
+ELEM_TOL = 1e-10
 
 
 def exact_ols(x, p, no_intercept=False):
@@ -67,6 +63,7 @@ def normwise(a, b):
 
 
 def elementwise(a, b):
+    """max |a_i - b_i| / |b_i| over the elements of b above 1e-6 ||b||."""
     big = np.abs(b) > 1e-6 * np.linalg.norm(b)
     return float(np.max(np.abs(a[big] - b[big]) / np.abs(b[big])))
 
@@ -80,7 +77,7 @@ def test_exact_solver_matches_lapack_on_a_well_conditioned_case():
 
 
 def test_reference_qr_error_grows_with_level_over_sigma():
-    # the premise of the GPU test below, on the oracle alone (CPU)
+    # the premise of the rule, on the oracle alone (CPU)
     errs = {}
     for level, sigma in [(1e2, 1.0), (1e6, 1e-2)]:
         x = walk(level, sigma, 1, 2520, 1)[0]
@@ -88,6 +85,56 @@ def test_reference_qr_error_grows_with_level_over_sigma():
         errs[(level, sigma)] = normwise(np.r_[c, coef], exact_ols(x, 5))
     assert errs[(1e2, 1.0)] < 1e-11 < 1e-10 < errs[(1e6, 1e-2)]
 
+
+# ---- the rule restated on the host (the device computes the same bounds from its own sums) ----
+
+def rule_flags(x, p, beta):
+    """sts_ar.hip kRule*: ratio (|mean| / centred lag-column rms) >= 16, scaled-pivot kappa
+    >= 100, |mean| / |c| >= 100."""
+    n = x.size
+    m = n - p
+    X = np.column_stack([x[p - 1 - j: n - 1 - j] for j in range(p)])
+    Xc = X - X.mean(axis=0)
+    G = Xc.T @ Xc
+    dg = np.diag(G)
+    mu = x.mean()
+    ratio = mu * mu * m >= 256.0 * dg.min()
+    d = np.sqrt(dg)
+    L = np.linalg.cholesky(G / np.outer(d, d))
+    kappa = np.any(np.diag(L) ** 2 * 100.0 <= 1.0)
+    lev = abs(mu) >= 100.0 * abs(beta[0])
+    return bool(ratio or kappa or lev)
+
+
+@pytest.mark.parametrize("family", ["ar", "noise", "walk", "trend"])
+def test_rule_bounds_hold_the_reference_near_exact(family):
+    """CPU check of the calibration (tools/ar_flag_study.py, at more seeds): wherever the rule
+    lets a series stay on the fast path, the reference is within 2e-11 elementwise of the exact
+    solution -- so the fast path (~1e-13 from exact) matches it inside 1e-10."""
+    rng = np.random.default_rng({"ar": 1, "noise": 2, "walk": 3, "trend": 4}[family])
+    kept = 0
+    for case in range(24):
+        T = int(rng.choice([120, 700, 2520]))
+        p = int(rng.choice([1, 2, 5, 8]))
+        level = float(rng.choice([0.0, 1.0, 3.0, 10.0]))
+        if family == "ar":
+            x = oracle.gen_ar_panel(50 + case, 1, T, min(p, 5))[0] + level
+        elif family == "noise":
+            x = level + rng.standard_normal(T)
+        elif family == "walk":
+            x = level + np.cumsum(rng.standard_normal(T)) * 0.05
+        else:
+            x = level + np.arange(T) / T + rng.uniform(-0.5, 0.5, T)
+        ex = exact_ols(x, p)
+        if rule_flags(x, p, ex):
+            continue
+        kept += 1
+        c, coef = oracle.ar_fit(x, p)
+        assert elementwise(np.r_[c, coef], ex) <= 2e-11, (family, case, T, p, level)
+    assert kept > 0
+
+
+# ---- GPU ----
 
 @pytest.fixture(scope="module")
 def torch():
@@ -109,19 +156,31 @@ def fit_gpu(torch, x, p, no_int):
     return np.column_stack([np.atleast_1d(c), m.coefficients.cpu().numpy().reshape(x.shape[0], p)])
 
 
+def rule_count(torch, x, p, no_int=False):
+    import ctypes
+    from sparkts import _native
+    from sparkts.errors import raise_for_status
+    t = torch.as_tensor(np.ascontiguousarray(x), device="cuda:0")
+    n = ctypes.c_int64(-1)
+    raise_for_status(_native.lib().sts_ar_rule_count(t.data_ptr(), t.shape[0], t.shape[1], t.shape[1], p, int(no_int),
+                                                     ctypes.addressof(n), None), "ar_rule_count")
+    return n.value
+
+
 @pytest.mark.gpu
-@pytest.mark.parametrize("kernel", ["register", "staged", "long"])
+@pytest.mark.parametrize("kernel", ["register", "staged", "long", "wave"])
 @pytest.mark.parametrize("p", [1, 5, 8])
 @pytest.mark.parametrize("no_int", [False, True])
 @pytest.mark.parametrize("level,sigma", LEVELS)
 def test_gpu_ar_fit_price_levels(torch, monkeypatch, kernel, p, no_int, level, sigma):
     # register: ar_fit_blk_kernel (p <= 8, T <= 2560); staged: ar_fit_kernel forced on the A/B
-    # build; long: T = 6000 takes ar_fit_kernel (MFMA Gram) in the product library
+    # build; long: T = 6000 takes ar_fit_kernel in the product library; wave: the A/B build's
+    # one-wave-per-series QR form instead of the lane form for the flagged series
     from sparkts import _native
     T = 6000 if kernel == "long" else 2520
-    if kernel == "staged":
+    if kernel in ("staged", "wave"):
         monkeypatch.setattr(_native, "_lib", _native.load_variant(_native.AB_LIB_PATH))
-        monkeypatch.setenv("STS_AR_STAGED", "1")
+        monkeypatch.setenv("STS_AR_STAGED" if kernel == "staged" else "STS_AR_QR_WAVE", "1")
     S = 4
     x = walk(level, sigma, S, T, int(level) % 97 + p * 7 + no_int)
     got = fit_gpu(torch, x, p, no_int)
@@ -133,15 +192,109 @@ def test_gpu_ar_fit_price_levels(torch, monkeypatch, kernel, p, no_int, level, s
         g = got[s]
         if no_int:
             ex, ref, g = ex[1:], ref[1:], g[1:]
-        e_ge, e_re, e_gr = normwise(g, ex), normwise(ref, ex), normwise(g, ref)
-        for k, v in (("gpu_exact", e_ge), ("ref_exact", e_re), ("gpu_ref", e_gr),
-                     ("gpu_ref_elem", elementwise(g, ref))):
+        e_el = elementwise(g, ref)
+        for k, v in (("gpu_exact", normwise(g, ex)), ("ref_exact", normwise(ref, ex)), ("gpu_ref", normwise(g, ref)),
+                     ("gpu_ref_elem", e_el)):
             worst[k] = max(worst[k], v)
-        assert e_ge <= 2.0 * e_re + 1e-12, (s, e_ge, e_re)
-        if e_re <= 1e-11:
-            assert e_gr <= 1e-10, (s, e_gr, e_re)
+        assert e_el <= ELEM_TOL, (s, e_el)
     RESULTS.append(dict(kernel=kernel, p=p, no_intercept=no_int, level=level, sigma=sigma, T=T, **worst))
     out = os.environ.get("STS_AR_LEVELS_JSON")
     if out:
         with open(out, "w") as f:
             json.dump(RESULTS, f, indent=1)
+
+
+def assert_same_bits(got, ref, what):
+    got, ref = np.asarray(got, np.float64), np.asarray(ref, np.float64)
+    bad = got.view(np.uint64) != ref.view(np.uint64)
+    assert not bad.any(), "%s: %d differ, first %s: %r vs %r" % (
+        what, int(bad.sum()), np.argwhere(bad)[0], got[bad][0], ref[bad][0])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("p", [1, 2, 5, 8, 9, 16])
+@pytest.mark.parametrize("T", [40, 700, 2520, 6000])
+def test_gpu_ar_rule_flagged_series_are_the_reference_bits(torch, p, T):
+    # price levels: every series flagged, fitted by the reference's QR order -> c, phi and the
+    # fused residuals bit-identical to the oracle's (lane form p <= 8, wave form p > 8)
+    from sparkts.models import Autoregression
+    if T <= 2 * p + 1:
+        pytest.skip("too short")
+    S = 70   # > one wave of lanes
+    x = walk(1e5, 1e-2, S, T, p * 13 + T)
+    assert rule_count(torch, x, p) == S
+    m, resid = Autoregression.fitModelAndRemove(torch.as_tensor(x, device="cuda:0"), p)
+    rr, rc, rcoef = oracle.panel_ar_fit_remove(x, p, threads=8)
+    assert_same_bits(m.c.cpu().numpy(), rc, "c")
+    assert_same_bits(m.coefficients.cpu().numpy(), rcoef, "coef")
+    assert_same_bits(resid.cpu().numpy(), rr, "residuals")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("p", [1, 3, 5, 8, 9, 17, 31])
+def test_gpu_ar_noint_is_the_reference_bits(torch, p):
+    # noIntercept: every series through the reference's QR order (C4-like and price-level rows)
+    from sparkts.models import Autoregression
+    T = 900
+    x = np.concatenate([oracle.gen_ar_panel(21, 10, T, min(p, 5)), walk(1e4, 1e-2, 10, T, p)])
+    m = Autoregression.fitModel(torch.as_tensor(x, device="cuda:0"), p, True)
+    rc = np.empty(20)
+    rcoef = np.empty((20, p))
+    for s in range(20):
+        rc[s], rcoef[s] = oracle.ar_fit(x[s], p, True)
+    assert_same_bits(m.c.cpu().numpy(), rc, "c")
+    assert_same_bits(m.coefficients.cpu().numpy(), rcoef, "coef")
+
+
+@pytest.mark.gpu
+def test_gpu_ar_rule_is_quiet_on_c4_panels(torch):
+    # the bench's C4 panel (AR(5) around c = 1, phi ~ 0.3 .. -0.05): no series flagged, so the
+    # C4 line runs the fast kernel only
+    x = oracle.gen_ar_panel(4, 20000, 2520, 5)
+    assert rule_count(torch, x, 5) == 0
+    # and the parity panels of test_parity_gpu (AR(1..5) shapes)
+    for p in (1, 2, 3, 5):
+        assert rule_count(torch, oracle.gen_ar_panel(4, 500, 2520, p), p) == 0
+
+
+@pytest.mark.gpu
+def test_gpu_ar_rule_mixed_panel(torch):
+    # flagged and unflagged rows in one call: flagged rows bit-identical to the oracle, the
+    # others within 1e-10 elementwise, the fused residuals bit-exact given each row's model
+    from sparkts.models import Autoregression
+    T, p = 2520, 5
+    x = oracle.gen_ar_panel(33, 64, T, p)
+    x[::3] = walk(1e6, 1e-2, x[::3].shape[0], T, 5)
+    m, resid = Autoregression.fitModelAndRemove(torch.as_tensor(x, device="cuda:0"), p)
+    c, coef, res = m.c.cpu().numpy(), m.coefficients.cpu().numpy(), resid.cpu().numpy()
+    for s in range(64):
+        rc, rcoef = oracle.ar_fit(x[s], p)
+        if s % 3 == 0:
+            assert_same_bits(np.r_[c[s], coef[s]], np.r_[rc, rcoef], "flagged row %d" % s)
+        else:
+            assert elementwise(np.r_[c[s], coef[s]], np.r_[rc, rcoef]) <= ELEM_TOL, s
+        assert_same_bits(res[s], oracle.ar_remove(x[s], c[s], coef[s]), "residuals row %d" % s)
+
+
+@pytest.mark.gpu
+def test_gpu_ar_rule_constant_and_near_constant_series(torch):
+    # a constant series: the fast Cholesky fails, the rule hands it to the reference's QR, whose
+    # verdict (SingularMatrixException or its finite numbers) the device then returns
+    from sparkts import _native
+    T, p = 300, 2
+    rows = [np.full(T, 100.1), np.full(T, 0.0), np.full(T, 4.0),
+            np.r_[np.full(T - 1, 7.3), 7.3000000001], walk(1e3, 1.0, 1, T, 3)[0]]
+    for x in rows:
+        xs = np.ascontiguousarray(x[None, :])
+        t = torch.as_tensor(xs, device="cuda:0")
+        c = torch.empty(1, dtype=torch.float64, device="cuda:0")
+        coef = torch.empty((1, p), dtype=torch.float64, device="cuda:0")
+        err = torch.zeros(1, dtype=torch.int32, device="cuda:0")
+        st = _native.lib().sts_ar_fit(t.data_ptr(), 1, T, T, p, 0, c.data_ptr(), coef.data_ptr(), err.data_ptr(), None)
+        assert st == 0
+        try:
+            rc, rcoef = oracle.ar_fit(x, p)
+            assert int(err.item()) == 0
+            assert_same_bits(np.r_[c.item(), coef.cpu().numpy()[0]], np.r_[rc, rcoef], "row %r" % x[:2])
+        except oracle.OracleError as e:   # the reference throws: same status on the device
+            assert int(err.item()) == e.code, (int(err.item()), e.code)

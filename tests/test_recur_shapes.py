@@ -146,8 +146,9 @@ def test_recur_fill_diff_ewma(torch, S, T, lag):
 
 # Row-contiguous panels (ld == T, 16-B aligned rows): the shapes of the round-4 whole-row batch
 # variant (batch edges, T = 2 .. 1202, more batches than CUs); with T <= 1 024 they now take
-# recur_row_kernel (one wave per series, lane blocks of 8 / 16 steps, bit-exact affine-scan guess
-# verified lane by lane), T = 1 200 / 1 202 the chunk kernel.
+# recur_row_kernel (32 lanes per series, two series per wave, lane blocks of up to 32 steps
+# (kRowLps = 32), bit-exact affine-scan guess verified lane by lane), T = 1 200 / 1 202 the chunk
+# kernel.
 @pytest.mark.parametrize("S,T", [(1, 2), (5, 2), (300, 390), (301, 390), (24, 390), (25, 390), (17, 1200),
                                  (9, 1202), (20_000, 390), (777, 64)])
 @pytest.mark.parametrize("lag", [1, 8])

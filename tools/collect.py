@@ -1,6 +1,6 @@
 """Collect one GPU session's evidence from gpurun_out/ into profiles/ (tracked).
 
-    python tools/collect.py TAG
+    python tools/collect.py TAG [DIR]      (DIR: the session's output directory, default gpurun_out)
 
 * gpurun_out/bench_<wl>.log          -> profiles/<TAG>_bench_<wl>.json   (the bench JSON line)
 * gpurun_out/prof_<wl>/*kernel_stats.csv -> profiles/<TAG>_<wl>_kernel_stats.csv (rocprofv3 --stats
@@ -18,6 +18,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUT = os.path.join(ROOT, "gpurun_out")
+LIB_SHA = None   # sha256[:16] of the libsts_hip.so the session ran (DIR/libsha.txt, tools/r5_session.sh)
 PROF = os.path.join(ROOT, "profiles")
 KERNEL = "tile_kernel"
 
@@ -60,7 +61,8 @@ def collect_fp64(tag, wl):
            "mfma_fp64_flops_per_launch": per["SQ_INSTS_VALU_MFMA_MOPS_F64"] * 512,
            "mfma_busy_frac": per["SQ_VALU_MFMA_BUSY_CYCLES"] / (1024.0 * per["GRBM_GUI_ACTIVE"] / 8.0),
            "effective_clock_note": "GRBM_GUI_ACTIVE / 8 = cycles per XCD over the launch",
-           "formula": "TOTAL_64_OPS = (2 FMA_F64 + ADD_F64 + MUL_F64) x 64 + MFMA_MOPS_F64 x 512"}
+           "formula": "TOTAL_64_OPS = (2 FMA_F64 + ADD_F64 + MUL_F64) x 64 + MFMA_MOPS_F64 x 512",
+           "lib_sha16": LIB_SHA}
     with open(os.path.join(PROF, "%s_%s_fp64.json" % (tag, wl)), "w") as f:
         json.dump(rec, f, indent=1)
     print(json.dumps(rec))
@@ -68,7 +70,13 @@ def collect_fp64(tag, wl):
 
 
 def main():
+    global OUT, LIB_SHA
     tag = sys.argv[1]
+    if len(sys.argv) > 2:
+        OUT = os.path.abspath(sys.argv[2])
+    sha = os.path.join(OUT, "libsha.txt")
+    if os.path.exists(sha):
+        LIB_SHA = open(sha).read().split()[0][:16]
     for log in glob.glob(os.path.join(OUT, "bench_*.log")):
         wl = os.path.basename(log)[len("bench_"):-len(".log")]
         lines = [ln for ln in open(log) if ln.startswith("{")]
@@ -89,7 +97,8 @@ def main():
                    "launches": [len(fetch), len(write)],
                    "read_bytes_per_launch": rd, "write_bytes_per_launch": wr,
                    "traffic_bytes_per_launch": rd + wr,
-                   "correction": "FETCH_SIZE (KiB) x 2 on gfx950, WRITE_SIZE (KiB) as is (MI355X_MICROARCH.md HBM)"}
+                   "correction": "FETCH_SIZE (KiB) x 2 on gfx950, WRITE_SIZE (KiB) as is (MI355X_MICROARCH.md HBM)",
+                   "lib_sha16": LIB_SHA}
             with open(os.path.join(PROF, "%s_%s_traffic.json" % (tag, wl)), "w") as f:
                 json.dump(rec, f, indent=1)
             print(json.dumps(rec))
