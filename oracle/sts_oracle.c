@@ -102,7 +102,12 @@ int orc_fillts(const double* x, double* r, int64_t n, int method) {
 
 /* Breeze 0.10 breeze.stats.mean over a DenseVector slice: sum left to right,
  * divide by the count (Breeze source is not vendored in /root/reference; the
- * summation order is an assumption, any other order differs by << 1e-10). */
+ * form is an ASSUMPTION -- PARITY UNPINNED).  Any summation order differs by
+ * << 1e-10 on ordinary series, but a running-mean update (mu += (y - mu) / n)
+ * would return a constant series' mean exactly and the reference's autocorr
+ * of a non-dyadic constant would then be NaN instead of 1.0.
+ * The device's one copy of this form is acf_exact_lag's first pass
+ * (spark-timeseries_amd/csrc/sts_acf.hpp). */
 static double breeze_mean(const double* v, int64_t len) {
     double sum = 0.0;
     for (int64_t k = 0; k < len; k++) sum += v[k];

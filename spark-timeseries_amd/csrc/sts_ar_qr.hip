@@ -77,6 +77,12 @@ __device__ __forceinline__ void qr_row(const double (&w)[P + 1], double (&c)[QrS
     c[NC] = w[P];
 }
 
+// raw values in flight per lane in a row sweep.  Measured on the all-flagged C4 shape
+// (bench.py --workload c4_levels): 8 values at one wave per SIMD (256 VGPRs) 49.4 ms, 4 values at
+// two waves per SIMD (251 VGPRs, __launch_bounds__(64, 2)) 57.8 ms -- the per-lane loads (64
+// series, 64 cache lines per load instruction) bound it, not latency: more waves only thrash L1
+constexpr int kQrPf = 8;
+
 template <int P, bool INT>
 __global__ __launch_bounds__(64) void ar_qr_lane_kernel(ArArgs a, const int64_t* __restrict__ list,
                                                         const uint32_t* __restrict__ count, int64_t n_direct) {
@@ -94,24 +100,24 @@ __global__ __launch_bounds__(64) void ar_qr_lane_kernel(ArArgs a, const int64_t*
         const double* xs = a.in + s * a.ld_in;
         auto ld = [&](int64_t t) -> double { return xs[t < T ? t : T - 1]; };
 
-        // sweep(r0, body): body(r, w) for r = r0 .. m-1 with w[q] = x[r + q], the next 8 raw
-        // values in flight while 8 rows are processed
+        // sweep(r0, body): body(r, w) for r = r0 .. m-1 with w[q] = x[r + q], the next kQrPf
+        // raw values in flight while kQrPf rows are processed
         auto sweep = [&](int64_t r0, auto&& body) {
             double w[P + 1];
 #pragma unroll
             for (int q = 0; q <= P; q++) w[q] = ld(r0 + q);
-            double nx[8];
+            double nx[kQrPf];
 #pragma unroll
-            for (int u = 0; u < 8; u++) nx[u] = ld(r0 + P + 1 + u);
-            for (int64_t r = r0; r < m; r += 8) {
-                double cur[8];
+            for (int u = 0; u < kQrPf; u++) nx[u] = ld(r0 + P + 1 + u);
+            for (int64_t r = r0; r < m; r += kQrPf) {
+                double cur[kQrPf];
 #pragma unroll
-                for (int u = 0; u < 8; u++) {
+                for (int u = 0; u < kQrPf; u++) {
                     cur[u] = nx[u];
-                    nx[u] = ld(r + 8 + P + 1 + u);
+                    nx[u] = ld(r + kQrPf + P + 1 + u);
                 }
 #pragma unroll
-                for (int u = 0; u < 8; u++) {
+                for (int u = 0; u < kQrPf; u++) {
                     if (r + u < m) {
                         body(r + u, w);
 #pragma unroll

@@ -35,6 +35,7 @@
 #include "sts_lanes.hpp"
 #include "sts_acf.hpp"
 #include "sts_scan.hpp"
+#include "sts_dma.hpp"
 
 #include <hip/hip_runtime.h>
 
@@ -52,6 +53,9 @@
 #endif
 #ifndef STS_TILE_WGS
 #define STS_TILE_WGS 4    // workgroups per CU the register budget is sized for (128 VGPRs; LDS 40.5 KB x 4 fits)
+#endif
+#ifndef STS_TILE_L2PF
+#define STS_TILE_L2PF 0   // ACF path: touch the lines of tile k + STS_TILE_L2PF at tile k's start (LDS-DMA into a sink)
 #endif
 
 
@@ -74,6 +78,18 @@ constexpr int kThreads = 256;
 constexpr int kBig = 1 << 30;
 
 __device__ __forceinline__ bool isnan_d(double v) { return __builtin_isnan(v); }
+
+// L2 / MALL prefetch without registers: one global_load_lds_dword per lane into a 256-B LDS
+// sink nothing reads (the line lands in L2 and the memory-side cache; the register prefetch
+// that follows hits there).  asm, so the compiler neither tracks the LDS write nor waits on it.
+__device__ __forceinline__ void l2_touch(const double* p, unsigned lds_sink) {
+    unsigned keep;
+    lds_sink = __builtin_amdgcn_readfirstlane(lds_sink);
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(p), "s"(lds_sink)
+                 : "memory");
+}
 
 // Diagnostic build only (-DSTS_STAMPS, `make stamps`): per-phase s_memtime accumulation,
 // summed over waves into a device array read back by sts_debug_stamps().  The shipped
@@ -222,6 +238,7 @@ __global__ __launch_bounds__(NTH, STS_TILE_WGS) void tile_kernel(TileArgs a) {
     // live across tiles for them): the last valid index before sh_c[0] is sh_c[1]; the first
     // valid index at or after sh_c[2] is sh_c[3]
     __shared__ int sh_c[4];
+    __shared__ __attribute__((aligned(16))) float l2pf_sink[(STS_TILE_L2PF > 0 && NT > 0) ? 64 : 1];
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -457,6 +474,21 @@ __global__ __launch_bounds__(NTH, STS_TILE_WGS) void tile_kernel(TileArgs a) {
             }
         }
         const bool have_next = (k + 1 < k_end) && interior(k + 1);
+        if constexpr (STS_TILE_L2PF > 0 && NT > 0) {
+            // the lines of tile k + D's extended range (268 x 128 B), two touches per thread
+            if (k + STS_TILE_L2PF < k_end) {
+                const int64_t pe0 = (k + STS_TILE_L2PF) * TW - kHB;
+                const unsigned sink = lds_addr(l2pf_sink);
+#pragma unroll
+                for (int j = 0; j < 2; j++) {
+                    int64_t t = pe0 + 16 * (int64_t)(tid + j * kThreads);
+                    if (j == 0 || 16 * (tid + j * kThreads) < EW) {
+                        t = t < 0 ? 0 : (t >= T ? T - 1 : t);
+                        l2_touch(src + t, sink);
+                    }
+                }
+            }
+        }
         STAMP(0);
         lds_barrier();
         STAMP(1);
@@ -837,6 +869,7 @@ __global__ __launch_bounds__(NTH, STS_TILE_WGS) void tile_kernel(TileArgs a) {
 #undef STS_LD1
 #undef STS_ST1
 #undef STS_CLEAR
+    if constexpr (STS_TILE_L2PF > 0 && NT > 0) dma_wait();   // no sink write may outlive the workgroup
     if (series_err && a.err) a.err[s] = STS_ERR_ALL_NAN;
 #ifdef STS_STAMPS
     if (lane == 0) {
@@ -994,6 +1027,12 @@ hipError_t launch_tile(int method, int tw, const TileArgs& a, hipStream_t st) {
     if (tw == 2048 && a.K > 0 && a.K <= 60) {   // 2-wave workgroups (A/B build: STS_TILE_W=2048)
         if (a.K <= 24) return launch_m<2048, 2, true, kThreads / 2>(method, grid, a, st);
         return launch_m<2048, 4, true, kThreads / 2>(method, grid, a, st);
+    }
+#endif
+#if defined(STS_ACF_TW) && STS_ACF_TW == 2048
+    if (tw == 2048 && a.K > 0 && a.K <= 60) {   // A/B builds: 4-wave workgroups on 2048-step tiles
+        if (a.K <= 24) return launch_m<2048, 2, true, kThreads>(method, grid, a, st);
+        return launch_m<2048, 4, true, kThreads>(method, grid, a, st);
     }
 #endif
     if (tw != 4096) return hipErrorInvalidValue;

@@ -48,7 +48,17 @@ for s in ${STEPS:-artests}; do
           TCP_UTCL1_STALL_UTCL2_REQ_OUT_OF_CREDITS_sum TCC_EA0_RDREQ_DRAM_CREDIT_STALL_sum TCC_EA0_WRREQ_DRAM_CREDIT_STALL_sum \
           -d $O/c5diag2_p$rep -o run --output-format csv -- python -u bench.py --workload c5 --steps 5 --warmup 1 --no-cpu-baseline
       done ;;
+    c5diag3)
+      # third set: is one L2 channel hot?  max-over-instances write stalls, tag stalls
+      for rep in 1 2 3; do
+        step c5diag3_p$rep 240 rocprofv3 --kernel-trace --pmc GRBM_GUI_ACTIVE TCC_WRREQ_STALL_max TCC_TAG_STALL_sum \
+          TCC_TOO_MANY_EA_WRREQS_STALL_sum TCC_EA0_WRREQ_STALL_sum \
+          -d $O/c5diag3_p$rep -o run --output-format csv -- python -u bench.py --workload c5 --steps 5 --warmup 1 --no-cpu-baseline
+      done ;;
+    sq_*) W=${s#sq_}; step pmc_sq_$W 200 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE \
+          -d $O/pmc_sq_$W -o run --output-format csv -- python -u bench.py --workload $W --series ${SQ_SERIES:-0} --steps 2 --warmup 0 --no-cpu-baseline ;;
     kbench) step kbench 600 env STS_HIP_LIB=spark-timeseries_amd/build/libsts_hip_ab.so python -u tools/kbench.py --series ${KB_SERIES:-12500} --reps 3 --cases ${KB_CASES:-tile:linear:60,seg:linear:60} ;;
+    ablibs) step ablibs ${AB_SECS:-900} env AB_SERIES=${AB_SERIES:-4000} bash tools/ab_libs.sh "${AB_CASES:-tile:linear:60}" $AB_LIBS ;;
     custom) step custom ${CUSTOM_SECS:-300} bash -c "$CUSTOM_CMD" ;;
   esac
 done
