@@ -54,6 +54,9 @@
 #ifndef STS_TILE_WGS
 #define STS_TILE_WGS 4    // workgroups per CU the register budget is sized for (128 VGPRs; LDS 40.5 KB x 4 fits)
 #endif
+#ifndef STS_TILE_LDS_PAD
+#define STS_TILE_LDS_PAD 0   // bytes of unused LDS per workgroup (diagnostic builds: caps workgroups per CU)
+#endif
 #ifndef STS_TILE_L2PF
 #define STS_TILE_L2PF 0   // ACF path: touch the lines of tile k + STS_TILE_L2PF at tile k's start (LDS-DMA into a sink)
 #endif
@@ -239,6 +242,14 @@ __global__ __launch_bounds__(NTH, STS_TILE_WGS) void tile_kernel(TileArgs a) {
     // valid index at or after sh_c[2] is sh_c[3]
     __shared__ int sh_c[4];
     __shared__ __attribute__((aligned(16))) float l2pf_sink[(STS_TILE_L2PF > 0 && NT > 0) ? 64 : 1];
+#if STS_TILE_LDS_PAD > 0
+    __shared__ char lds_pad[STS_TILE_LDS_PAD];
+    if (a.S < 0) {   // never taken: keeps the allocation
+        lds_pad[threadIdx.x] = 1;
+        __syncthreads();
+        a.err[threadIdx.x] = lds_pad[threadIdx.x ^ 1];
+    }
+#endif
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
