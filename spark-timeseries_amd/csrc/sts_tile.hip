@@ -93,6 +93,9 @@ __device__ __forceinline__ bool isnan_d(double v) { return __builtin_isnan(v); }
 #ifndef STS_RS_SIMD
 #define STS_RS_SIMD 1     // role split: fill / MFMA roles by SIMD (HW_ID), one of each per SIMD
 #endif
+#ifndef STS_RS_BURST
+#define STS_RS_BURST 0    // MFMA waves: 0 = operands one chunk ahead; G = bursts of G chunks (A/B)
+#endif
 #ifndef STS_RS_MPRIO
 #define STS_RS_MPRIO 0    // wave priority of the MFMA waves (A/B)
 #endif
@@ -137,13 +140,21 @@ __device__ __forceinline__ void l2_touch(const double* p, unsigned lds_sink) {
 // Diagnostic build only (-DSTS_STAMPS, `make stamps`): per-phase s_memtime accumulation,
 // summed over waves into a device array read back by sts_debug_stamps().  The shipped
 // library has no stamps.
-#ifdef STS_STAMPS
+// -DSTS_RS_MSTAMP: the role split's MFMA-wave stamps only (the fill waves run unstamped)
+#if defined(STS_STAMPS) || defined(STS_RS_MSTAMP)
 __device__ unsigned long long g_stamps[32];   // [0, 12) + 13 fill phases, 12 fill waves; [16, 21) MFMA-wave phases, 21 MFMA waves
+#ifdef STS_STAMPS
+#define STS_STAMP_FILL 1
+#else
+#define STS_STAMP_FILL 0
+#endif
 #define STAMP(i)                                                                            \
     do {                                                                                    \
-        const unsigned long long now_ = __builtin_amdgcn_s_memtime();                      \
-        st_acc[i] += now_ - st_prev;                                                        \
-        st_prev = now_;                                                                     \
+        if ((i) >= 16 || STS_STAMP_FILL) {                                                  \
+            const unsigned long long now_ = __builtin_amdgcn_s_memtime();                  \
+            st_acc[i] += now_ - st_prev;                                                    \
+            st_prev = now_;                                                                 \
+        }                                                                                   \
     } while (0)
 #else
 #define STAMP(i) \
@@ -244,7 +255,7 @@ __device__ __forceinline__ int px2_(int q2) { return PAD ? q2 + ((q2 >> 4) << 1)
 // The two roles hand the slot over through LDS counters, and the fill waves synchronise among
 // themselves with an LDS-counter barrier (s_barrier would wait for the MFMA waves too).
 template <int TW, int NT, bool SHIFTED, int NTH, int M, bool RS = false>
-__global__ __launch_bounds__(NTH, RS ? 2 : STS_TILE_WGS) void tile_kernel(TileArgs a) {
+__global__ __launch_bounds__(NTH, RS ? 4 : STS_TILE_WGS) void tile_kernel(TileArgs a) {   // (2nd: waves per SIMD)
     constexpr int method = M;
     static_assert(!RS || (NT > 0 && SHIFTED && NTH == 512), "role split: fused ACF, 4 + 4 waves");
     constexpr int kThreads = RS ? 256 : NTH;   // fill threads: 256 (4 waves) or 128 (2 waves, TW = 2048)
@@ -416,7 +427,7 @@ __global__ __launch_bounds__(NTH, RS ? 2 : STS_TILE_WGS) void tile_kernel(TileAr
 #pragma unroll
     for (int t = 0; t < NA; t++) U[t] = d4{0.0, 0.0, 0.0, 0.0};
     bool series_err = false;
-#ifdef STS_STAMPS
+#if defined(STS_STAMPS) || defined(STS_RS_MSTAMP)
     unsigned long long st_acc[24] = {0};
     unsigned long long st_prev = __builtin_amdgcn_s_memtime();
 #endif
@@ -502,10 +513,46 @@ __global__ __launch_bounds__(NTH, RS ? 2 : STS_TILE_WGS) void tile_kernel(TileAr
                         ib[t] = cb + ob[t];
                         asm volatile("" : "+v"(ia[t]), "+v"(ib[t]));
                     }
+                    if constexpr (RS && STS_RS_BURST > 0) {
+                        // bursts: the operands of G chunks read and landed, then their MFMAs with
+                        // no read in flight, then a read of the accumulators (the wave waits for its
+                        // MFMAs) before the next reads -- same order of accumulation as below
+                        constexpr int G = STS_RS_BURST > 0 ? STS_RS_BURST : 1;
+                        static_assert((TE - F) % G == 0, "whole bursts");
+#pragma unroll
+                        for (int cg = F; cg < TE; cg += G) {
+                            double av[G][NTA], bv[G][NTA];
+#pragma unroll
+                            for (int g = 0; g < G; g++)
+#pragma unroll
+                                for (int t = 0; t < NT; t++) {
+                                    av[g][t] = vb[ia[t] + 72 * (cg + g)];
+                                    bv[g][t] = vb[ib[t] + 72 * (cg + g)];
+                                }
+                            __builtin_amdgcn_sched_barrier(0);
+                            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // every read landed
+                            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                            for (int g = 0; g < G; g++) {
+#pragma unroll
+                                for (int t = 0; t < NT; t++)
+                                    U[t % NA] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[g][t], bv[g][t], U[t % NA], 0, 0, 0);
+                                acc_s += av[g][0];
+                                acc_q = __builtin_fma(av[g][0], av[g][0], acc_q);
+                            }
+                            __builtin_amdgcn_sched_barrier(0);
+                            {   // a VALU read of both accumulators: the wave waits for its MFMAs here
+                                unsigned done = (unsigned)__builtin_bit_cast(unsigned long long, U[0][3]) ^
+                                                (unsigned)__builtin_bit_cast(unsigned long long, U[NA - 1][3]);
+                                asm volatile("" ::"v"(done));
+                            }
+                            __builtin_amdgcn_sched_barrier(0);
+                        }
+                    } else
                     if constexpr (RS) {
                         // the MFMA waves of the role split are one or two per SIMD: the operands
                         // of chunk cc + 1 are read while chunk cc's MFMAs run (same order of
-                        // accumulation as below)
+                        // accumulation as below).  (Chunk pairs read two ahead need 167 VGPRs.)
                         double av[NTA], bv[NTA];
 #pragma unroll
                         for (int t = 0; t < NT; t++) {
@@ -615,6 +662,12 @@ __global__ __launch_bounds__(NTH, RS ? 2 : STS_TILE_WGS) void tile_kernel(TileAr
             }
         }
         const bool have_next = (k + 1 < k_end) && interior(k + 1);
+        // role split: the fill waves have no MFMA phase to hide the next tile's loads behind, so
+        // they issue them as soon as the registers are free -- here, phases 2-5 ahead of their use
+        if constexpr (RS) {
+            if (have_next) STS_ISSUE(k + 1);
+            else STS_CLEAR();
+        }
         if constexpr (STS_TILE_L2PF > 0 && NT > 0) {
             // the lines of tile k + D's extended range (268 x 128 B), two touches per thread
             if (k + STS_TILE_L2PF < k_end) {
@@ -960,8 +1013,10 @@ __global__ __launch_bounds__(NTH, RS ? 2 : STS_TILE_WGS) void tile_kernel(TileAr
             // the look-back range as y = 0
             if (SHIFTED && NT > 0 && !RS && e0 < 0 && tid < kHB / 2) v2[px2(tid)] = make_double2(0.0, 0.0);
         }
-        if (have_next) STS_ISSUE(k + 1);   // in flight during the MFMA phase of tile k
-        else STS_CLEAR();
+        if constexpr (!RS) {
+            if (have_next) STS_ISSUE(k + 1);   // in flight during the MFMA phase of tile k
+            else STS_CLEAR();
+        }
         // lag matrix (fill only; S/Lag.scala:62-77): column c - init holds x[r + max_lag - c] at
         // row r.  Each column's rows of this tile go out as 16-B pairs aligned on the column's
         // own address (one wave instruction = 1 KB of one column; round 3 stored the two halves
@@ -1057,7 +1112,13 @@ __global__ __launch_bounds__(NTH, RS ? 2 : STS_TILE_WGS) void tile_kernel(TileAr
                 rs_arrive(&rs_cnt[2], lane);   // done with vals
                 wave_lds_sync();               // this wave's slot writes before its operand reads
                 STAMP(18);
-#if !defined(STS_RS_DIAG) || STS_RS_DIAG == 0
+#if defined(STS_RS_DIAG) && STS_RS_DIAG == 4
+                if ((k & 1) == 0)   // diagnostic: the lag products of every other tile only
+#endif
+#if defined(STS_RS_DIAG) && STS_RS_DIAG == 5   // diagnostic: the lag products twice
+                mfma_group(std::integral_constant<int, 0>{}, std::integral_constant<int, CPW>{}, yslot, k, t0, t1, m);
+#endif
+#if !defined(STS_RS_DIAG) || STS_RS_DIAG == 0 || STS_RS_DIAG >= 4
                 mfma_group(std::integral_constant<int, 0>{}, std::integral_constant<int, CPW>{}, yslot, k, t0, t1, m);
 #endif
                 STAMP(19);
@@ -1070,7 +1131,7 @@ __global__ __launch_bounds__(NTH, RS ? 2 : STS_TILE_WGS) void tile_kernel(TileAr
     }
     if constexpr (STS_TILE_L2PF > 0 && NT > 0) dma_wait();   // no sink write may outlive the workgroup
     if (series_err && a.err) a.err[s] = STS_ERR_ALL_NAN;
-#ifdef STS_STAMPS
+#if defined(STS_STAMPS) || defined(STS_RS_MSTAMP)
     if (lane == 0) {
 #pragma unroll
         for (int i = 0; i < 24; i++)
@@ -1250,7 +1311,7 @@ hipError_t launch_tile(int method, int tw, const TileArgs& a, hipStream_t st) {
     return hipErrorInvalidValue;
 }
 
-#ifdef STS_STAMPS
+#if defined(STS_STAMPS) || defined(STS_RS_MSTAMP)
 extern "C" int sts_debug_stamps(unsigned long long* out32) {
     if (hipMemcpyFromSymbol(out32, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * 32) != hipSuccess) return 4;
     unsigned long long z[32] = {0};

@@ -54,7 +54,7 @@ def main():
         torch.cuda.synchronize()
         ms = ev0.elapsed_time(ev1)
         lib.sts_debug_stamps(buf.ctypes.data)
-    tot = float(buf[:12].sum() + buf[13])
+    tot = max(float(buf[:12].sum() + buf[13]), 1.0)   # 1: an MFMA-wave-only build (-DSTS_RS_MSTAMP)
     res = {"S": S, "K": K, "method": method, "ms": ms, "waves": int(buf[12]),
            "share": {n: round(float(buf[i]) / tot, 4) for i, n in enumerate(NAMES)}}
     if buf[21]:   # role split: fill-wave shares include the copy wait; MFMA-wave shares of their own time
