@@ -138,13 +138,7 @@ int method_ok(int method, bool allow_none, const char* name) {
 }
 
 int tile_width(int64_t T) { return T <= 512 ? 512 : 4096; }
-#ifndef STS_ACF_TPC
-#define STS_ACF_TPC 16
-#endif
-#ifndef STS_ACF_TW
-#define STS_ACF_TW 4096   // tile width of the fused fill + ACF (K <= 60) tile kernel (A/B builds: 2048)
-#endif
-constexpr int64_t kTilesPerChunk = STS_ACF_TPC;  // tiles per workgroup (prefetch pipeline depth 1)
+constexpr int64_t kTilesPerChunk = 16;  // tiles per workgroup (prefetch pipeline depth 1)
 // without the ACF (fill only, fill + lag matrix: C5) one tile per workgroup: the denser sweep
 // beats the prefetch pipeline (C5: 1.527-1.534 vs 1.647-1.659 ms same box, and 1.83 vs 2.03-2.07 on
 // a box in its slow state, profiles/r04_v11_ab_c5_tpc.jsonl; fill only on the C3 shard 31.2-31.6 vs
@@ -202,9 +196,7 @@ int run_tile(const double* in, double* out, double* lagmat, int64_t S, int64_t T
     const bool seg = seg_ok && (force ? !std::strcmp(force, "seg") : T <= 16384);
     // STS_TILE_W=2048: 2-wave workgroups on 2048-step tiles for K <= 60 (A/B build only)
     const char* tw_env = (!seg && K > 0 && K <= 60 && !lagmat) ? sts::ab_knob("STS_TILE_W") : nullptr;
-    const int tw = seg ? sts::kSegW
-                       : (K > 0) ? (tw_env && std::atoi(tw_env) == 2048 ? 2048 : (K <= 60 && !lagmat ? STS_ACF_TW : 4096))
-                                 : tile_width(T);
+    const int tw = seg ? sts::kSegW : (K > 0) ? (tw_env && std::atoi(tw_env) == 2048 ? 2048 : 4096) : tile_width(T);
     sts::TileArgs a{};
     a.in = in;
     a.out = out;

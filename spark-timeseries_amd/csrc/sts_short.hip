@@ -40,10 +40,6 @@ namespace {
 #endif
 constexpr int kShortWaves = STS_SHORT_WAVES;
 
-#ifndef STS_SHORT_V
-#define STS_SHORT_V 1      // 1: the whole-series 20-KB block kernel; 2: the half-block kernel (round 5)
-#endif
-
 #ifndef STS_SHORT_DIAG
 #define STS_SHORT_DIAG 0   // timing-only cost models (tools/variant.sh): 1 no ACF, 2 no fill,
                            // 3 no per-lag finalize, 4 no robust shift, 5 no lag products;
@@ -291,267 +287,6 @@ __global__ __launch_bounds__(64 * kShortWaves, 2) void short_fill_acf_kernel(Til
     if (lane < K) a.acf_fused[s * K + lane] = r;
 }
 
-
-// ---------------------------------------------------------------------------------------
-// Round 5: the same operator with HALF the LDS block and no series in
-// registers.  The 20-KB block held the whole series and the lag pass held it in 80 VGPRs too
-// (217 VGPRs): 8 waves per CU.  Here the series passes through one 10-KB block in two halves
-// (lanes 0..31's steps, then lanes 32..63's), twice:
-//   1. each raw half is DMA'd in and its lanes take their validity masks, first / last valid
-//      values and the ACF samples (robust_shift's, read while that half is in the block);
-//   2. each raw half is DMA'd in again (from L2 / MALL), its runs are filled in the block (ends
-//      outside a lane's block come from the neighbours' first / last valid values), it leaves
-//      as coalesced 1-KB stores, and its lanes run their lag products reading y = F - c from the
-//      block (a rolling window as in sts_short; lane 32's look-back from lane 31's last KM
-//      filled steps, kept in a small LDS stash).  The row sums of each half go to LDS scratch.
-// The same shift, the same per-lane accumulation order and the same finalize as
-// short_fill_acf_kernel: the same ACF bits.
-template <int B, int KM, int M>
-__global__ __launch_bounds__(64, 3) void short2_fill_acf_kernel(TileArgs a) {
-    static_assert(M == STS_FILL_LINEAR || M == STS_FILL_PREVIOUS || M == STS_FILL_NEXT || M == STS_FILL_NEAREST,
-                  "fill method");
-    static_assert(KM <= B, "the window reaches one lane back only");
-    constexpr int HD = 32 * B;   // doubles per half block
-    __shared__ __attribute__((aligned(16))) double blk[HD];
-    __shared__ __attribute__((aligned(16))) double red[4 * (KM + 2)];   // row sums: [0..3] sum, [4d..] P_d, [4(KM+1)..] sq
-    __shared__ double stash[KM + 1];                                     // lane 31's last KM filled steps
-    const int lane = threadIdx.x & 63;
-    const int64_t s = blockIdx.x;
-    if (s >= a.S) return;
-    const int T = (int)a.T;
-    const int t0 = lane * B;
-    const int myh = lane >> 5;
-    const double* src = a.in + s * a.ld_in;
-    const int nh = (T > HD) ? 2 : 1;
-    const unsigned lb = lds_addr(blk);
-    const bool prev_fill = (M == STS_FILL_PREVIOUS);
-    auto dma_half = [&](int h) {
-#pragma unroll
-        for (int i = 0; i < B / 4; i++) {
-            const int u = h * HD + 2 * (i * 64 + lane);
-            glds16(src + (u < T ? u : 0), lb + i * 1024);
-        }
-        dma_wait();
-        wave_lds_sync();
-    };
-
-    // ---- 1. masks, first / last valid values, ACF samples ----
-    unsigned long long vm = 0ull;   // bit j: step t0 + j is inside the series and valid
-    double fvv = 0.0, lvv = 0.0;    // raw values at the block's first / last valid step (fill ends)
-    const int sa = (int)((int64_t)lane * T / 64), sb = (int)((int64_t)(lane + 1) * T / 64);
-    bool sfound = false;
-    double sv = 0.0;
-    for (int h = 0; h < nh; h++) {
-        dma_half(h);
-        if (myh == h) {
-            bool any = false;
-#pragma unroll
-            for (int j = 0; j < B / 2; j++) {
-                const double2 v = *reinterpret_cast<const double2*>(blk + t0 - h * HD + 2 * j);
-                const bool ok0 = t0 + 2 * j < T && !__builtin_isnan(v.x) && !(M == STS_FILL_NEAREST && t0 + 2 * j == 0);
-                const bool ok1 = t0 + 2 * j + 1 < T && !__builtin_isnan(v.y);
-                if (t0 + 2 * j < T && !__builtin_isnan(v.x)) vm |= 1ull << (2 * j);
-                if (ok1) vm |= 1ull << (2 * j + 1);
-                if (ok0) { if (!any) fvv = v.x; lvv = v.x; any = true; }
-                if (ok1) { if (!any) fvv = v.y; lvv = v.y; any = true; }
-            }
-        }
-        {   // the first valid raw step of [sa, sb) among the blocks of half h
-            const int ba = sa / B;
-            const int bb = ba + 1 < 64 ? ba + 1 : 63;
-            const unsigned long long m0f = __shfl(vm, ba), m1f = __shfl(vm, bb);
-            const unsigned long long m0 = ((ba >> 5) == h) ? m0f : 0ull;
-            const unsigned long long m1 = ((bb >> 5) == h && bb != ba) ? m1f : 0ull;
-            const int o = sa - ba * B;
-            const int e0 = (sb - ba * B < B) ? sb - ba * B : B;
-            const unsigned long long w0 = (o < e0) ? (m0 >> o) & ((e0 - o >= 64) ? ~0ull : ((1ull << (e0 - o)) - 1ull)) : 0ull;
-            const int e1 = sb - (ba + 1) * B;
-            const unsigned long long w1 = (e1 > 0) ? (m1 & ((e1 >= 64) ? ~0ull : ((1ull << e1) - 1ull))) : 0ull;
-            const bool here = !sfound && sa < sb && (w0 || w1);
-            const int idx = w0 ? sa + __builtin_ctzll(w0) : (ba + 1) * B + (w1 ? __builtin_ctzll(w1) : 0);
-            if (here) {
-                sv = blk[idx - h * HD];
-                sfound = true;
-            }
-        }
-        wave_lds_sync();
-    }
-    const double c0 = [&] {
-        const unsigned long long vmk = __ballot(sfound);
-        if (vmk == 0ull) return 0.0;
-        const unsigned long long ab = vmk & ~((2ull << lane) - 1ull);
-        const unsigned long long be = vmk & ((1ull << lane) - 1ull);
-        const int from = sfound ? lane : shift_fallback_lane(ab, be, prev_fill);
-        return median_of_lanes(__shfl(sv, from), true, lane);
-    }();
-
-    // ---- 2. fill, store and lag products, half by half ----
-    const unsigned long long vf = (M == STS_FILL_NEAREST && lane == 0) ? vm & ~1ull : vm;
-    const int fv = vf ? t0 + __builtin_ctzll(vf) : T;
-    const int lv = vf ? t0 + 63 - __builtin_clzll(vf) : -1;
-    const unsigned long long hv = __ballot(vf != 0ull);
-    const unsigned long long below = hv & ((1ull << lane) - 1ull);
-    const unsigned long long above = hv & ~((2ull << lane) - 1ull);
-    const int Lsrc = below ? 63 - __builtin_clzll(below) : lane;
-    const int Rsrc = above ? __builtin_ctzll(above) : lane;
-    const int lvs = __shfl(lv, Lsrc), fvs = __shfl(fv, Rsrc);
-    const double lvvs = __shfl(lvv, Lsrc), fvvs = __shfl(fvv, Rsrc);
-    const int Lc = below ? lvs : -1;
-    const int Rc = above ? fvs : T;
-    const int tend = (t0 + B < T) ? t0 + B : T;
-    const bool all_nan = (M == STS_FILL_NEAREST) && hv == 0ull && T >= 2;
-    const int K = a.K;
-    const bool acf = K > 0 && a.acf_fused != nullptr && STS_SHORT_DIAG != 1;
-    double yh = 0.0, zt = 0.0;   // y at step lane and at step T - 1 - lane (the finalize's head / tail)
-    const int row = lane >> 4;
-    const bool row_lead = (lane & 15) == 0;
-    for (int h = 0; h < nh; h++) {
-        double* buf = blk - h * HD;   // buf[t]: step t of half h
-        dma_half(h);
-        if (myh == h && STS_SHORT_DIAG != 2 && !all_nan) {
-            auto xat = [&](int t) -> double { return t == Lc ? lvvs : (t == Rc ? fvvs : buf[t]); };
-            auto fill_run = [&](int q0, int q1, int L, int R) {
-                if (M == STS_FILL_PREVIOUS || M == STS_FILL_NEXT) {
-                    if (M == STS_FILL_PREVIOUS ? L >= 0 : R < T) {
-                        const double v = xat(M == STS_FILL_PREVIOUS ? L : R);
-                        for (int q = q0; q < q1; q++) buf[q] = v;
-                    }
-                } else if (M == STS_FILL_NEAREST) {
-                    if (L >= 0 || R < T) {
-                        const double xL = (L >= 0) ? xat(L) : 0.0, xR = (R < T) ? xat(R) : 0.0;
-                        for (int q = q0; q < q1; q++) buf[q] = (R >= T || (L >= 0 && q - L < R - q)) ? xL : xR;
-                    }
-                } else if (L >= 0 && R < T) {   // linear: the reference's sequential accumulation
-                    const double xL = xat(L);
-                    const double inc = (xat(R) - xL) / (double)(R - L);
-                    double cur = xL;
-                    for (int q = L + 1; q < q0; q++) cur = cur + inc;
-                    for (int q = q0; q < q1; q++) {
-                        cur = cur + inc;
-                        buf[q] = cur;
-                    }
-                }
-            };
-            if (!(vf & 1ull) && t0 < T) {
-                const int R = vf ? fv : Rc;
-                const int q0 = (M == STS_FILL_NEAREST && t0 == 0) ? 1 : t0;
-                fill_run(q0, R < tend ? R : tend, Lc, R);
-            }
-            const unsigned long long inT = (tend - t0 >= 64) ? ~0ull : ((1ull << (tend > t0 ? tend - t0 : 0)) - 1ull);
-            unsigned long long rs = ~vf & (vf << 1) & inT;
-            while (rs) {
-                const int j = __builtin_ctzll(rs);
-                rs &= rs - 1ull;
-                const int t = t0 + j;
-                const unsigned long long hi = (j + 1 < 64) ? vf >> (j + 1) : 0ull;
-                const int R = hi ? t + 1 + __builtin_ctzll(hi) : Rc;
-                fill_run(t, R < tend ? R : tend, t - 1, R);
-            }
-        }
-        wave_lds_sync();   // half h of the block holds F
-        if (a.out) {
-            double* dst = a.out + s * a.ld_out;
-#pragma unroll
-            for (int i = 0; i < B / 4; i++) {
-                const int u = h * HD + 2 * (i * 64 + lane);
-                if (u < T) *reinterpret_cast<double2*>(dst + u) = *reinterpret_cast<const double2*>(blk + (u - h * HD));
-            }
-        }
-        if (acf) {
-            if (lane >= h * HD && lane < (h + 1) * HD) yh = buf[lane] - c0;
-            const int tz = T - 1 - lane;
-            if (tz >= h * HD && tz < (h + 1) * HD) zt = buf[tz] - c0;
-            if (h == 0 && lane < KM && 32 * B - 1 - lane < T) stash[lane + 1] = buf[32 * B - 1 - lane];   // lane 31's tail
-            // lag products of this half's lanes: P_d = sum_j fma(y_j, y_{j-d}) in step order
-            double win[KM + 1];
-#pragma unroll
-            for (int k = 1; k <= KM; k++) {
-                const int tk = t0 - k;
-                win[k] = (tk < 0) ? 0.0 : ((tk >= h * HD) ? buf[tk] - c0 : stash[k] - c0);
-            }
-            double P[KM + 1];
-#pragma unroll
-            for (int d = 0; d <= KM; d++) P[d] = 0.0;
-            double sm = 0.0, qm = 0.0;
-#pragma unroll
-            for (int j2 = 0; j2 < B / 2; j2++) {
-                const double2 v = *reinterpret_cast<const double2*>(buf + t0 + 2 * j2);
-#pragma unroll
-                for (int e = 0; e < 2; e++) {
-                    const int j = 2 * j2 + e;
-                    const double yj = (t0 + j < T) ? (e ? v.y : v.x) - c0 : 0.0;
-                    if (acf_mid(t0 + j, T)) {
-                        sm += yj;
-                        qm = __builtin_fma(yj, yj, qm);
-                    }
-#pragma unroll
-                    for (int d = 1; d <= KM; d++)
-                        if (STS_SHORT_DIAG != 5) P[d] = __builtin_fma(yj, win[d], P[d]);
-#pragma unroll
-                    for (int k = KM; k >= 2; k--) win[k] = win[k - 1];
-                    win[1] = yj;
-                }
-            }
-            // row sums of this half's two rows (rows 2h, 2h + 1)
-#pragma unroll
-            for (int d = 1; d <= KM; d++) {
-                const double v = row_sum_dpp(P[d]);
-                if (row_lead && myh == h) red[4 * d + row] = v;
-            }
-            const double v0 = row_sum_dpp(sm), v1 = row_sum_dpp(qm);
-            if (row_lead && myh == h) {
-                red[row] = v0;
-                red[4 * (KM + 1) + row] = v1;
-            }
-        }
-        wave_lds_sync();   // every read of half h is done before the next half is written
-    }
-    if (a.err && lane == 0) a.err[s] = all_nan ? STS_ERR_ALL_NAN : STS_OK;
-    if (!acf) return;
-    if (nh == 1) {   // a one-half series: rows 2, 3 hold nothing
-        if (lane < 2) {
-            for (int d = 0; d <= KM + 1; d++) red[4 * d + 2 + lane] = 0.0;
-        }
-        wave_lds_sync();
-    }
-
-    // ---- 3. finalize (sts_short's, the same operands in the same order) ----
-    const int li = (lane < KM) ? lane + 1 : KM;
-    const double4 pr = *reinterpret_cast<const double4*>(red + 4 * li);
-    const double Pi = (pr.x + pr.y) + (pr.z + pr.w);
-    const double4 sr = *reinterpret_cast<const double4*>(red);
-    const double4 qr = *reinterpret_cast<const double4*>(red + 4 * (KM + 1));
-    const double Sm = (sr.x + sr.y) + (sr.z + sr.w), Qm = (qr.x + qr.y) + (qr.z + qr.w);
-    double ys = yh, yq = yh * yh, zs = zt, zq = zt * zt;
-#pragma unroll
-    for (int k = 1; k < 64; k <<= 1) {
-        const double a0 = __shfl_down(ys, k), a1 = __shfl_down(yq, k), a2 = __shfl_down(zs, k),
-                     a3 = __shfl_down(zq, k);
-        if (lane + k < 64) {
-            ys += a0;
-            yq += a1;
-            zs += a2;
-            zq += a3;
-        }
-    }
-    const double Yall = lane_bcast(ys, 0), YQall = lane_bcast(yq, 0), Zall = lane_bcast(zs, 0),
-                 ZQall = lane_bcast(zq, 0);
-    double ysi = __shfl_down(ys, 1), yqi = __shfl_down(yq, 1), zsi = __shfl_down(zs, 1), zqi = __shfl_down(zq, 1);
-    if (lane == 63) ysi = yqi = zsi = zqi = 0.0;
-    const double sum1 = (Sm + Zall) + ysi, sq1 = (Qm + ZQall) + yqi;
-    const double sum2 = (Sm + Yall) + zsi, sq2 = (Qm + YQall) + zqi;
-    const double N = (double)(T - (lane + 1));
-    const double v1 = sq1 - sum1 * sum1 / N;
-    const double v2 = sq2 - sum2 * sum2 / N;
-    const double cv = Pi - sum1 * sum2 / N;
-    double r = cv / (__builtin_sqrt(v1) * __builtin_sqrt(v2));   // S/UnivariateTimeSeries.scala:89
-    if (__ballot(lane < K && acf_suspect(r, sum1, sq1, sum2, sq2, v1, v2, N, c0))) {
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-        if (lane < K) r = acf_exact_lag(a.out + s * a.ld_out, T, lane + 1);
-    }
-    if (lane < K) a.acf_fused[s * K + lane] = r;
-}
-
 }  // namespace
 
 // fill('linear') + fused ACF for 128 <= T <= 2 560, T even, K <= 24, 16-B aligned rows
@@ -573,13 +308,8 @@ hipError_t launch_short_m(const TileArgs& a, hipStream_t st) {
     const int KM = (a.K + 3) / 4 * 4 < 8 ? 8 : (a.K + 3) / 4 * 4;
     const int64_t nb = need < KM ? KM : need;
     const int B = nb <= 8 ? 8 : nb <= 16 ? 16 : nb <= 24 ? 24 : nb <= 32 ? 32 : 40;
-#if STS_SHORT_V == 2
-#define STS_SHORT_K(BB, KK) \
-    case KK: hipLaunchKernelGGL((short2_fill_acf_kernel<BB, (KK <= BB ? KK : BB), M>), dim3((unsigned)a.S), dim3(64), 0, st, a); break;
-#else
 #define STS_SHORT_K(BB, KK) \
     case KK: hipLaunchKernelGGL((short_fill_acf_kernel<BB, (KK <= BB ? KK : BB), M>), g, b, 0, st, a); break;
-#endif
 #define STS_SHORT(BB)                                                                              \
     case BB:                                                                                       \
         switch (KM) {                                                                              \

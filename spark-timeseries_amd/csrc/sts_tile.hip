@@ -35,7 +35,6 @@
 #include "sts_lanes.hpp"
 #include "sts_acf.hpp"
 #include "sts_scan.hpp"
-#include "sts_dma.hpp"
 
 #include <hip/hip_runtime.h>
 
@@ -53,15 +52,6 @@
 #endif
 #ifndef STS_TILE_WGS
 #define STS_TILE_WGS 4    // workgroups per CU the register budget is sized for (128 VGPRs; LDS 40.5 KB x 4 fits)
-#endif
-#ifndef STS_TILE_LDS_PAD
-#define STS_TILE_LDS_PAD 0   // bytes of unused LDS per workgroup (diagnostic builds: caps workgroups per CU)
-#endif
-#ifndef STS_TILE_RS
-#define STS_TILE_RS 0     // fused fill + ACF (K <= 60): the role-split kernel (fill waves + MFMA waves)
-#endif
-#ifndef STS_TILE_L2PF
-#define STS_TILE_L2PF 0   // ACF path: touch the lines of tile k + STS_TILE_L2PF at tile k's start (LDS-DMA into a sink)
 #endif
 
 
@@ -85,76 +75,16 @@ constexpr int kBig = 1 << 30;
 
 __device__ __forceinline__ bool isnan_d(double v) { return __builtin_isnan(v); }
 
-// Role-split hand-off (tile_kernel<..., RS = true>): LDS counters that only grow.  rs_arrive adds
-// one per wave after a release fence on LDS; rs_wait polls until the counter reaches target and
-// then fences (acquire, LDS).  Neither fence orders global memory, so no wait on the register
-// prefetch in flight.  A wait still unsatisfied after kRsSpin polls sets the abort word and every
-// later wait returns at once: a broken hand-off ends the kernel with an error, it never spins on.
-#ifndef STS_RS_SIMD
-#define STS_RS_SIMD 1     // role split: fill / MFMA roles by SIMD (HW_ID), one of each per SIMD
-#endif
-#ifndef STS_RS_BURST
-#define STS_RS_BURST 0    // MFMA waves: 0 = operands one chunk ahead; G = bursts of G chunks (A/B)
-#endif
-#ifndef STS_RS_MPRIO
-#define STS_RS_MPRIO 0    // wave priority of the MFMA waves (A/B)
-#endif
-#ifndef STS_RS_FSLEEP
-#define STS_RS_FSLEEP 0   // fill-wave barrier polls with s_sleep 1 between reads (A/B)
-#endif
-constexpr int kRsSpin = 1 << 20;
-__device__ __forceinline__ int lds_load_relaxed(int* p) {
-    return __builtin_amdgcn_readfirstlane(__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
-}
-__device__ __forceinline__ void rs_arrive(int* cnt, int lane) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-    if (lane == 0) __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-template <bool SLEEP>
-__device__ __forceinline__ bool rs_wait(int* cnt, int target, int* abort_w) {
-    if (lds_load_relaxed(abort_w) != 0) return false;
-    for (int it = 0; it < kRsSpin; it++) {
-        if (lds_load_relaxed(cnt) >= target) {
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-            return true;
-        }
-        if ((it & 255) == 255 && lds_load_relaxed(abort_w) != 0) return false;
-        if (SLEEP) __builtin_amdgcn_s_sleep(1);
-    }
-    __hip_atomic_store(abort_w, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    return false;
-}
-
-// L2 / MALL prefetch without registers: one global_load_lds_dword per lane into a 256-B LDS
-// sink nothing reads (the line lands in L2 and the memory-side cache; the register prefetch
-// that follows hits there).  asm, so the compiler neither tracks the LDS write nor waits on it.
-__device__ __forceinline__ void l2_touch(const double* p, unsigned lds_sink) {
-    unsigned keep;
-    lds_sink = __builtin_amdgcn_readfirstlane(lds_sink);
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
-                 : "=&s"(keep)
-                 : "v"(p), "s"(lds_sink)
-                 : "memory");
-}
-
 // Diagnostic build only (-DSTS_STAMPS, `make stamps`): per-phase s_memtime accumulation,
 // summed over waves into a device array read back by sts_debug_stamps().  The shipped
 // library has no stamps.
-// -DSTS_RS_MSTAMP: the role split's MFMA-wave stamps only (the fill waves run unstamped)
-#if defined(STS_STAMPS) || defined(STS_RS_MSTAMP)
-__device__ unsigned long long g_stamps[32];   // [0, 12) + 13 fill phases, 12 fill waves; [16, 21) MFMA-wave phases, 21 MFMA waves
 #ifdef STS_STAMPS
-#define STS_STAMP_FILL 1
-#else
-#define STS_STAMP_FILL 0
-#endif
+__device__ unsigned long long g_stamps[16];
 #define STAMP(i)                                                                            \
     do {                                                                                    \
-        if ((i) >= 16 || STS_STAMP_FILL) {                                                  \
-            const unsigned long long now_ = __builtin_amdgcn_s_memtime();                  \
-            st_acc[i] += now_ - st_prev;                                                    \
-            st_prev = now_;                                                                 \
-        }                                                                                   \
+        const unsigned long long now_ = __builtin_amdgcn_s_memtime();                      \
+        st_acc[i] += now_ - st_prev;                                                        \
+        st_prev = now_;                                                                     \
     } while (0)
 #else
 #define STAMP(i) \
@@ -249,18 +179,12 @@ __device__ __forceinline__ int px2_(int q2) { return PAD ? q2 + ((q2 >> 4) << 1)
 // M: the fill method (STS_FILL_*), a template parameter (round 4: as a kernel argument its tests
 // were hoisted out of the tile loop as masks and spilled; compile-time, every method-dependent
 // branch folds away)
-// RS (role split, K <= 60 only): 8-wave workgroups, two per CU.  Waves 0-3 (the FILL waves) run
-// phases 1-5 of every tile and write y = F - c into a second LDS buffer (the y slot); waves 4-7
-// (the MFMA waves) run phase 6 of tile k from the slot while the fill waves work on tile k + 1.
-// The two roles hand the slot over through LDS counters, and the fill waves synchronise among
-// themselves with an LDS-counter barrier (s_barrier would wait for the MFMA waves too).
-template <int TW, int NT, bool SHIFTED, int NTH, int M, bool RS = false>
-__global__ __launch_bounds__(NTH, RS ? 4 : STS_TILE_WGS) void tile_kernel(TileArgs a) {   // (2nd: waves per SIMD)
+template <int TW, int NT, bool SHIFTED, int NTH, int M>
+__global__ __launch_bounds__(NTH, STS_TILE_WGS) void tile_kernel(TileArgs a) {
     constexpr int method = M;
-    static_assert(!RS || (NT > 0 && SHIFTED && NTH == 512), "role split: fused ACF, 4 + 4 waves");
-    constexpr int kThreads = RS ? 256 : NTH;   // fill threads: 256 (4 waves) or 128 (2 waves, TW = 2048)
-    constexpr int kWaves = kThreads / 64;
-    constexpr int kAllWaves = NTH / 64;
+    if constexpr (NT > 0) __builtin_amdgcn_s_setprio(STS_FILL_PRIO);   // see the MFMA phase below
+    constexpr int kThreads = NTH;          // 256 (4 waves) or 128 (2 waves, TW = 2048)
+    constexpr int kWaves = NTH / 64;
     static_assert(TW / 64 % kWaves == 0, "whole 64-step chunks per wave");
     constexpr int EW = kHB + TW + kHA;
     constexpr int NA = SHIFTED ? 2 : (NT > 0 ? NT : 1);      // MFMA accumulators
@@ -298,48 +222,10 @@ __global__ __launch_bounds__(NTH, RS ? 4 : STS_TILE_WGS) void tile_kernel(TileAr
     // live across tiles for them): the last valid index before sh_c[0] is sh_c[1]; the first
     // valid index at or after sh_c[2] is sh_c[3]
     __shared__ int sh_c[4];
-    __shared__ __attribute__((aligned(16))) float l2pf_sink[(STS_TILE_L2PF > 0 && NT > 0) ? 64 : 1];
-    // role split: the y slot (same padded layout as vals) and the hand-off counters (rs_sync)
-    __shared__ __attribute__((aligned(16))) double yslot[RS ? EWP : 1];
-    __shared__ int rs_cnt[5];
-    __shared__ int rs_simd[RS ? 8 : 1];
-#if STS_TILE_LDS_PAD > 0
-    __shared__ char lds_pad[STS_TILE_LDS_PAD];
-    if (a.S < 0) {   // never taken: keeps the allocation
-        lds_pad[threadIdx.x] = 1;
-        __syncthreads();
-        a.err[threadIdx.x] = lds_pad[threadIdx.x ^ 1];
-    }
-#endif
 
-    // role split: the roles go by SIMD, not by wave index -- on each SIMD the workgroup's first
-    // wave fills and its second runs the MFMA work (the dispatcher need not put waves w and w + 4 on
-    // one SIMD); tid below is the thread's index in role order (fill waves 0-3, MFMA waves 4-7)
-    int vt = threadIdx.x;
-    if constexpr (RS && STS_RS_SIMD) {
-        unsigned hw;
-        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));   // SIMD id: bits 5:4
-        const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-        if ((threadIdx.x & 63) == 0) rs_simd[w] = (int)((hw >> 4) & 3u);
-        __syncthreads();
-        int rank = 0, nfill = 0, fidx = 0, midx = 0;
-        for (int v = 0; v < kAllWaves; v++) {
-            int r = 0;
-            for (int u = 0; u < v; u++) r += rs_simd[u] == rs_simd[v];
-            nfill += r == 0;
-            if (v < w) (r == 0 ? fidx : midx)++;
-            if (v == w) rank = r;
-        }
-        if (nfill == kWaves) vt = (rank == 0 ? fidx : kWaves + midx) * 64 + (int)(threadIdx.x & 63);
-    }
-    const int tid = vt;
+    const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform: scalar loop control
-    const bool fill_role = !RS || wave < kWaves;
-    if constexpr (NT > 0) {   // see the MFMA phase below
-        if (fill_role) __builtin_amdgcn_s_setprio(STS_FILL_PRIO);
-        else __builtin_amdgcn_s_setprio(STS_RS_MPRIO);
-    }
     // one workgroup = one CHUNK of tiles_per_chunk consecutive tiles of one series
     const int64_t nchunk = a.S * a.chunks_per_series;
     const int64_t ch = xcd_remap(blockIdx.x, nchunk);
@@ -366,23 +252,6 @@ __global__ __launch_bounds__(NTH, RS ? 4 : STS_TILE_WGS) void tile_kernel(TileAr
         sh_c[0] = -kBig;
         sh_c[2] = -1;
     }
-    // role split: rs_cnt = {fill-barrier arrivals, F ready in vals, vals copied, abort, slot read},
-    // counted per wave arrival (4 per event)
-    int fbar = 0;   // fill waves: arrivals the next fill barrier waits for (wave-uniform)
-    if constexpr (RS) {
-        if (tid < 5) rs_cnt[tid] = 0;
-        __syncthreads();
-    }
-    // barrier among the fill waves: s_barrier, or under the role split the LDS-counter barrier
-    auto fsync = [&]() {
-        if constexpr (RS) {
-            fbar += kWaves;
-            rs_arrive(&rs_cnt[0], lane);
-            rs_wait<STS_RS_FSLEEP != 0>(&rs_cnt[0], fbar, &rs_cnt[3]);
-        } else {
-            lds_barrier();
-        }
-    };
     double acc_s = 0.0, acc_q = 0.0;   // sum y, sum y^2 over this thread's middle positions
 
     // register prefetch of one INTERIOR extended tile [e0, e0 + EW); the first and last tile
@@ -427,11 +296,11 @@ __global__ __launch_bounds__(NTH, RS ? 4 : STS_TILE_WGS) void tile_kernel(TileAr
 #pragma unroll
     for (int t = 0; t < NA; t++) U[t] = d4{0.0, 0.0, 0.0, 0.0};
     bool series_err = false;
-#if defined(STS_STAMPS) || defined(STS_RS_MSTAMP)
-    unsigned long long st_acc[24] = {0};
+#ifdef STS_STAMPS
+    unsigned long long st_acc[12] = {0};
     unsigned long long st_prev = __builtin_amdgcn_s_memtime();
 #endif
-    bool have = fill_role && interior(k_begin);
+    bool have = interior(k_begin);
     if (have) STS_ISSUE(k_begin);
     else STS_CLEAR();
     // ACF shift (sts_acf.hpp: median of 64 raw samples of the series), computed once per
@@ -460,7 +329,7 @@ __global__ __launch_bounds__(NTH, RS ? 4 : STS_TILE_WGS) void tile_kernel(TileAr
         acc_s += z;
         acc_q = __builtin_fma(z, z, acc_q);
     };
-    auto mfma_group = [&](auto FROM, auto TO, const double* vb, int64_t kk, int tt0, int tt1, int wv) {
+    auto mfma_group = [&](auto FROM, auto TO, const double* vb, int64_t kk, int tt0, int tt1) {
         constexpr int F = decltype(FROM)::value, TE = decltype(TO)::value;
         if constexpr (NT > 0 && F < TE) {
             // a tile wholly inside the middle takes the unrolled loop with plain sums; the
@@ -468,9 +337,9 @@ __global__ __launch_bounds__(NTH, RS ? 4 : STS_TILE_WGS) void tile_kernel(TileAr
             const bool tile_mid = tt0 >= kAcfEdge && tt1 + kAcfEdge <= T;
             const int tlen = tt1 - tt0;
             const int nch = (tlen + 63) / 64;
-            const bool full = wv * CPW + CPW <= nch;
-            int c = wv * CPW + F;
-            int cend = wv * CPW + TE;
+            const bool full = wave * CPW + CPW <= nch;
+            int c = wave * CPW + F;
+            int cend = wave * CPW + TE;
             if (cend > nch) cend = nch;
             if constexpr (SHIFTED) {
                 // A = y(chunk + QS t + lane), B = y(chunk + QS t + 16 (lane >> 4) + h(lane & 15));
@@ -496,95 +365,22 @@ __global__ __launch_bounds__(NTH, RS ? 4 : STS_TILE_WGS) void tile_kernel(TileAr
                         U[t % NA] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[t], bv[t], U[t % NA], 0, 0, 0);
                     return av[0];   // y at chunk position lane
                 };
-                // (wv: the wave's index among the waves running lag products)
                 // wave 0 of the first tile also runs chunk -1 (the look-back, y = 0), whose
                 // shifted windows hold the series' first QS t steps
-                if (F == 0 && kk == 0 && wv == 0) chunk_mfma(vb);   // y = 0 there: no middle-sum term
+                if (F == 0 && kk == 0 && wave == 0) chunk_mfma(vb);   // y = 0 there: no middle-sum term
                 if (full && tile_mid) {
                     // full chunk range, unrolled: per-lane LDS indices made opaque once per
                     // group (else LICM hoists all of them out of the tile loop and spills),
                     // chunk offsets (72 doubles per padded chunk) fold into the ds_read
                     // immediates
                     int ia[NTA], ib[NTA];
-                    const int cb = px(qA0 + 64 * (wv * CPW));
+                    const int cb = px(qA0 + 64 * (wave * CPW));
 #pragma unroll
                     for (int t = 0; t < NT; t++) {
                         ia[t] = cb + oa[t];
                         ib[t] = cb + ob[t];
                         asm volatile("" : "+v"(ia[t]), "+v"(ib[t]));
                     }
-                    if constexpr (RS && STS_RS_BURST > 0) {
-                        // bursts: the operands of G chunks read and landed, then their MFMAs with
-                        // no read in flight, then a read of the accumulators (the wave waits for its
-                        // MFMAs) before the next reads -- same order of accumulation as below
-                        constexpr int G = STS_RS_BURST > 0 ? STS_RS_BURST : 1;
-                        static_assert((TE - F) % G == 0, "whole bursts");
-#pragma unroll
-                        for (int cg = F; cg < TE; cg += G) {
-                            double av[G][NTA], bv[G][NTA];
-#pragma unroll
-                            for (int g = 0; g < G; g++)
-#pragma unroll
-                                for (int t = 0; t < NT; t++) {
-                                    av[g][t] = vb[ia[t] + 72 * (cg + g)];
-                                    bv[g][t] = vb[ib[t] + 72 * (cg + g)];
-                                }
-                            __builtin_amdgcn_sched_barrier(0);
-                            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // every read landed
-                            __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-                            for (int g = 0; g < G; g++) {
-#pragma unroll
-                                for (int t = 0; t < NT; t++)
-                                    U[t % NA] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[g][t], bv[g][t], U[t % NA], 0, 0, 0);
-                                acc_s += av[g][0];
-                                acc_q = __builtin_fma(av[g][0], av[g][0], acc_q);
-                            }
-                            __builtin_amdgcn_sched_barrier(0);
-                            {   // a VALU read of both accumulators: the wave waits for its MFMAs here
-                                unsigned done = (unsigned)__builtin_bit_cast(unsigned long long, U[0][3]) ^
-                                                (unsigned)__builtin_bit_cast(unsigned long long, U[NA - 1][3]);
-                                asm volatile("" ::"v"(done));
-                            }
-                            __builtin_amdgcn_sched_barrier(0);
-                        }
-                    } else
-                    if constexpr (RS) {
-                        // the MFMA waves of the role split are one or two per SIMD: the operands
-                        // of chunk cc + 1 are read while chunk cc's MFMAs run (same order of
-                        // accumulation as below).  (Chunk pairs read two ahead need 167 VGPRs.)
-                        double av[NTA], bv[NTA];
-#pragma unroll
-                        for (int t = 0; t < NT; t++) {
-                            av[t] = vb[ia[t] + 72 * F];
-                            bv[t] = vb[ib[t] + 72 * F];
-                        }
-#pragma unroll
-                        for (int cc = F; cc < TE; cc++) {
-                            double an[NTA], bn[NTA];
-                            if (cc + 1 < TE) {
-#pragma unroll
-                                for (int t = 0; t < NT; t++) {
-                                    an[t] = vb[ia[t] + 72 * (cc + 1)];
-                                    bn[t] = vb[ib[t] + 72 * (cc + 1)];
-                                }
-                            }
-                            __builtin_amdgcn_sched_barrier(0);   // the reads stay ahead of the MFMAs
-#pragma unroll
-                            for (int t = 0; t < NT; t++)
-                                U[t % NA] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[t], bv[t], U[t % NA], 0, 0, 0);
-                            acc_s += av[0];
-                            acc_q = __builtin_fma(av[0], av[0], acc_q);
-                            __builtin_amdgcn_sched_barrier(0);
-                            if (cc + 1 < TE) {
-#pragma unroll
-                                for (int t = 0; t < NT; t++) {
-                                    av[t] = an[t];
-                                    bv[t] = bn[t];
-                                }
-                            }
-                        }
-                    } else
 #pragma unroll
                     for (int cc = F; cc < TE; cc++) {
                         double av[NTA], bv[NTA];
@@ -618,8 +414,7 @@ __global__ __launch_bounds__(NTH, RS ? 4 : STS_TILE_WGS) void tile_kernel(TileAr
             }
         }
     };
-    // the fill loop (the MFMA waves of the role split skip it: they run the loop after it)
-    for (int64_t k = fill_role ? k_begin : k_end; k < k_end; k++) {
+    for (int64_t k = k_begin; k < k_end; k++) {
         const int t0 = (int)(k * TW);
         const int t1 = (t0 + TW < T) ? t0 + TW : (int)T;
         const int e0 = t0 - kHB;
@@ -662,29 +457,8 @@ __global__ __launch_bounds__(NTH, RS ? 4 : STS_TILE_WGS) void tile_kernel(TileAr
             }
         }
         const bool have_next = (k + 1 < k_end) && interior(k + 1);
-        // role split: the fill waves have no MFMA phase to hide the next tile's loads behind, so
-        // they issue them as soon as the registers are free -- here, phases 2-5 ahead of their use
-        if constexpr (RS) {
-            if (have_next) STS_ISSUE(k + 1);
-            else STS_CLEAR();
-        }
-        if constexpr (STS_TILE_L2PF > 0 && NT > 0) {
-            // the lines of tile k + D's extended range (268 x 128 B), two touches per thread
-            if (k + STS_TILE_L2PF < k_end) {
-                const int64_t pe0 = (k + STS_TILE_L2PF) * TW - kHB;
-                const unsigned sink = lds_addr(l2pf_sink);
-#pragma unroll
-                for (int j = 0; j < 2; j++) {
-                    int64_t t = pe0 + 16 * (int64_t)(tid + j * kThreads);
-                    if (j == 0 || 16 * (tid + j * kThreads) < EW) {
-                        t = t < 0 ? 0 : (t >= T ? T - 1 : t);
-                        l2_touch(src + t, sink);
-                    }
-                }
-            }
-        }
         STAMP(0);
-        fsync();
+        lds_barrier();
         STAMP(1);
 
         // positions to produce: [qA, qB) (E-relative); the ACF needs REACH steps past the tile
@@ -708,7 +482,7 @@ __global__ __launch_bounds__(NTH, RS ? 4 : STS_TILE_WGS) void tile_kernel(TileAr
                 }
             }
             STAMP(2);
-            fsync();
+            lds_barrier();
         }
         STAMP(3);
 
@@ -818,7 +592,7 @@ __global__ __launch_bounds__(NTH, RS ? 4 : STS_TILE_WGS) void tile_kernel(TileAr
         }
         if constexpr (NT > 0) __builtin_amdgcn_s_setprio(STS_FILL_PRIO);
         STAMP(4);
-        fsync();
+        lds_barrier();
         STAMP(5);
 
         // ---- 4. impute the compacted NaN positions, all lanes busy; F goes back into
@@ -932,13 +706,11 @@ __global__ __launch_bounds__(NTH, RS ? 4 : STS_TILE_WGS) void tile_kernel(TileAr
             else impute(std::false_type{});
         }
         STAMP(6);
-        fsync();
+        lds_barrier();
         STAMP(7);
 
         // ---- 5. filled output + lag matrix (16-B stores), then y = F - F(0) in place
-        //      (0 past the series end) for the MFMA phase; start the next tile's loads.  Under
-        //      the role split F stays in vals: the MFMA waves copy y out of it (phase 6') ----
-        if constexpr (RS) rs_arrive(&rs_cnt[1], lane);   // F of tile k complete
+        //      (0 past the series end) for the MFMA phase; start the next tile's loads ----
         {
             const bool al = dst && ((reinterpret_cast<uintptr_t>(dst) & 15) == 0);
             double2* v2 = reinterpret_cast<double2*>(vals);
@@ -949,7 +721,7 @@ __global__ __launch_bounds__(NTH, RS ? 4 : STS_TILE_WGS) void tile_kernel(TileAr
             const bool fast = (dst == nullptr || al) && (t1 - t0 == TW) && (NT == 0 || e0 + qW + REACH <= T);
             if (fast) {
                 constexpr int FS = TW / 2 / kThreads;                          // stored double2
-                constexpr int FY = (NT > 0 && !RS) ? (NP2 - kHB / 2 + kThreads - 1) / kThreads : FS;
+                constexpr int FY = NT > 0 ? (NP2 - kHB / 2 + kThreads - 1) / kThreads : FS;
                 constexpr int FH = (FY + 1) / 2;     // two halves: fewer live registers
                 const int vq = (kHB >> 1) + tid;
                 const int pvq = opq(px2(vq));   // px2(vq + jj kThreads) = pvq + jj PX2S
@@ -980,7 +752,7 @@ __global__ __launch_bounds__(NTH, RS ? 4 : STS_TILE_WGS) void tile_kernel(TileAr
                             __builtin_nontemporal_store(fv[j].x, &dq->x);
                             __builtin_nontemporal_store(fv[j].y, &dq->y);
                         }
-                        if (NT > 0 && !RS && in) {
+                        if (NT > 0 && in) {
                             double2 y;
                             y.x = fv[j].x - c0;
                             y.y = fv[j].y - c0;
@@ -989,7 +761,7 @@ __global__ __launch_bounds__(NTH, RS ? 4 : STS_TILE_WGS) void tile_kernel(TileAr
                     }
                 }
             } else
-            for (int q2 = (qA >> 1) + tid; 2 * q2 < qW || (!RS && 2 * q2 < qBfull); q2 += kThreads) {
+            for (int q2 = (qA >> 1) + tid; 2 * q2 < qW || 2 * q2 < qBfull; q2 += kThreads) {
                 const int q = 2 * q2;
                 double2 f = v2[px2(q2)];
                 if (q < qW) {
@@ -1003,7 +775,7 @@ __global__ __launch_bounds__(NTH, RS ? 4 : STS_TILE_WGS) void tile_kernel(TileAr
                         }
                     }
                 }
-                if (NT > 0 && !RS && q < qBfull) {
+                if (NT > 0 && q < qBfull) {
                     f.x = (q < qB) ? f.x - c0 : 0.0;
                     f.y = (q + 1 < qB) ? f.y - c0 : 0.0;
                     v2[px2(q2)] = f;
@@ -1011,12 +783,10 @@ __global__ __launch_bounds__(NTH, RS ? 4 : STS_TILE_WGS) void tile_kernel(TileAr
             }
             // shifted scheme, first tile: the pre-chunk (positions [0, 4t) of the series) reads
             // the look-back range as y = 0
-            if (SHIFTED && NT > 0 && !RS && e0 < 0 && tid < kHB / 2) v2[px2(tid)] = make_double2(0.0, 0.0);
+            if (SHIFTED && NT > 0 && e0 < 0 && tid < kHB / 2) v2[px2(tid)] = make_double2(0.0, 0.0);
         }
-        if constexpr (!RS) {
-            if (have_next) STS_ISSUE(k + 1);   // in flight during the MFMA phase of tile k
-            else STS_CLEAR();
-        }
+        if (have_next) STS_ISSUE(k + 1);   // in flight during the MFMA phase of tile k
+        else STS_CLEAR();
         // lag matrix (fill only; S/Lag.scala:62-77): column c - init holds x[r + max_lag - c] at
         // row r.  Each column's rows of this tile go out as 16-B pairs aligned on the column's
         // own address (one wave instruction = 1 KB of one column; round 3 stored the two halves
@@ -1048,95 +818,31 @@ __global__ __launch_bounds__(NTH, RS ? 4 : STS_TILE_WGS) void tile_kernel(TileAr
         }
         STAMP(8);
 
-        if constexpr (NT > 0 && !RS) {
-            fsync();
+        if constexpr (NT > 0) {
+            lds_barrier();
             STAMP(9);
             // ---- 6. lag products on MFMA, at wave priority 0; the rest of the tile loop runs at
             //      STS_FILL_PRIO, so a SIMD's arbiter favours the waves of workgroups in their fill
             //      and store phases (memory issue) over the MFMA stream of the others ----
             __builtin_amdgcn_s_setprio(0);
-            mfma_group(std::integral_constant<int, 0>{}, std::integral_constant<int, CPW>{}, vals, k, t0, t1, wave);
+            mfma_group(std::integral_constant<int, 0>{}, std::integral_constant<int, CPW>{}, vals, k, t0, t1);
             __builtin_amdgcn_s_setprio(STS_FILL_PRIO);
         }
         have = have_next;
         STAMP(10);
-        // the MFMA waves have copied tile k's y out of vals
-        if constexpr (RS) rs_wait<STS_RS_FSLEEP != 0>(&rs_cnt[2], kWaves * (int)(k - k_begin + 1), &rs_cnt[3]);
-        STAMP(13);
-        fsync();   // vals / mask / lists are reused by the next tile
+        lds_barrier();   // vals / mask / lists are reused by the next tile
         STAMP(11);
     }
 #undef STS_ISSUE
 #undef STS_LD1
 #undef STS_ST1
 #undef STS_CLEAR
-    if constexpr (RS) {
-        // ---- 6'. role split, MFMA waves: per tile, copy y = F - c0 (0 from qB on; 0 in the
-        //      look-back of the first tile) out of vals into the slot -- each wave the range its own
-        //      chunks read, CPW chunks plus the 128-step reach into the next wave's range, so it
-        //      needs no other wave's copy -- release vals to the fill waves, then the lag products
-        //      of phase 6 (same chunks per wave index, same order: the same partial sums).  The
-        //      reach overlap is written by two waves with the same values; a wave copies tile k + 1
-        //      only once every MFMA wave is done reading tile k ----
-        if (!fill_role) {
-            const int m = wave - kWaves;
-            constexpr int CP2 = (64 * CPW + 128) / 2;   // double2 per wave's copy range
-            constexpr int CPR = (CP2 + 63) / 64;
-            static_assert(SHIFTED && 16 * (NT - 1) / NT + 48 + 16 * (15 / (16 / NT)) + (16 - 16 / NT) + 15 % (16 / NT) < 128,
-                          "the operands of a wave's chunks reach < 128 steps past its range");
-            static_assert(kHB + 64 * CPW * kWaves + 128 <= EW, "copy ranges inside the extended tile");
-            const double2* f2 = reinterpret_cast<const double2*>(vals);
-            double2* y2 = reinterpret_cast<double2*>(yslot);
-            for (int64_t k = k_begin; k < k_end; k++) {
-                const int t0 = (int)(k * TW);
-                const int t1 = (t0 + TW < T) ? t0 + TW : (int)T;
-                const int e0 = t0 - kHB;
-                int qB = kHB + (t1 - t0) + REACH;
-                if (e0 + qB > T) qB = (int)T - e0;
-                rs_wait<true>(&rs_cnt[1], kWaves * (int)(k - k_begin + 1), &rs_cnt[3]);   // F of tile k
-                STAMP(16);
-                if (k > k_begin) rs_wait<true>(&rs_cnt[4], kWaves * (int)(k - k_begin), &rs_cnt[3]);
-                STAMP(17);
-                const int b2 = kHB / 2 + 32 * CPW * m;
-#pragma unroll
-                for (int j = 0; j < CPR; j++) {
-                    const int q2 = b2 + lane + 64 * j;
-                    if ((j + 1) * 64 <= CP2 || lane + 64 * j < CP2) {
-                        double2 f = f2[px2(q2)];
-                        f.x = (2 * q2 < qB) ? f.x - c0 : 0.0;
-                        f.y = (2 * q2 + 1 < qB) ? f.y - c0 : 0.0;
-                        y2[px2(q2)] = f;
-                    }
-                }
-                if (m == 0 && e0 < 0 && lane < kHB / 2) y2[px2(lane)] = make_double2(0.0, 0.0);
-                rs_arrive(&rs_cnt[2], lane);   // done with vals
-                wave_lds_sync();               // this wave's slot writes before its operand reads
-                STAMP(18);
-#if defined(STS_RS_DIAG) && STS_RS_DIAG == 4
-                if ((k & 1) == 0)   // diagnostic: the lag products of every other tile only
-#endif
-#if defined(STS_RS_DIAG) && STS_RS_DIAG == 5   // diagnostic: the lag products twice
-                mfma_group(std::integral_constant<int, 0>{}, std::integral_constant<int, CPW>{}, yslot, k, t0, t1, m);
-#endif
-#if !defined(STS_RS_DIAG) || STS_RS_DIAG == 0 || STS_RS_DIAG >= 4
-                mfma_group(std::integral_constant<int, 0>{}, std::integral_constant<int, CPW>{}, yslot, k, t0, t1, m);
-#endif
-                STAMP(19);
-                rs_arrive(&rs_cnt[4], lane);   // done with the slot
-                STAMP(20);
-            }
-        }
-        __syncthreads();
-        if (tid == 0 && rs_cnt[3] != 0 && a.err) a.err[s] = STS_ERR_HIP;   // a hand-off timed out
-    }
-    if constexpr (STS_TILE_L2PF > 0 && NT > 0) dma_wait();   // no sink write may outlive the workgroup
     if (series_err && a.err) a.err[s] = STS_ERR_ALL_NAN;
-#if defined(STS_STAMPS) || defined(STS_RS_MSTAMP)
+#ifdef STS_STAMPS
     if (lane == 0) {
 #pragma unroll
-        for (int i = 0; i < 24; i++)
-            if (i != 12 && i != 21 && st_acc[i]) atomicAdd(&g_stamps[i], st_acc[i]);
-        atomicAdd(&g_stamps[fill_role ? 12 : 21], 1ull);
+        for (int i = 0; i < 12; i++) atomicAdd(&g_stamps[i], st_acc[i]);
+        atomicAdd(&g_stamps[12], 1ull);
     }
 #endif
 
@@ -1174,7 +880,7 @@ __global__ __launch_bounds__(NTH, RS ? 4 : STS_TILE_WGS) void tile_kernel(TileAr
             acc_s += __shfl_xor(acc_s, d);
             acc_q += __shfl_xor(acc_q, d);
         }
-        double* wsum = vals + kAllWaves * 256;
+        double* wsum = vals + kWaves * 256;
         wsum[wave * kPartStride + lane] = lagacc;
         if (lane == 0) {
             wsum[wave * kPartStride + kPartSum] = acc_s;
@@ -1185,12 +891,12 @@ __global__ __launch_bounds__(NTH, RS ? 4 : STS_TILE_WGS) void tile_kernel(TileAr
             double* part = a.partials + ch * kPartStride;
             double tot = 0.0;
 #pragma unroll
-            for (int w = 0; w < kAllWaves; w++) tot += wsum[w * kPartStride + lane];
+            for (int w = 0; w < kWaves; w++) tot += wsum[w * kPartStride + lane];
             part[lane] = tot;
             if (lane == 0) {
                 double ts = 0.0, tq = 0.0;
 #pragma unroll
-                for (int w = 0; w < kAllWaves; w++) {
+                for (int w = 0; w < kWaves; w++) {
                     ts += wsum[w * kPartStride + kPartSum];
                     tq += wsum[w * kPartStride + kPartSq];
                 }
@@ -1264,15 +970,15 @@ hipError_t launch_acf_shift(const double* in, int64_t S, int64_t T, int64_t ld, 
 }
 
 // one launch of tile_kernel<TW, NT, SHIFTED, NTH, method>
-template <int TW, int NT, bool SHIFTED, int NTH, bool RS = false>
+template <int TW, int NT, bool SHIFTED, int NTH>
 hipError_t launch_m(int method, dim3 grid, const TileArgs& a, hipStream_t st) {
     const dim3 block(NTH);
     switch (method) {
-    case STS_FILL_NONE: hipLaunchKernelGGL((tile_kernel<TW, NT, SHIFTED, NTH, STS_FILL_NONE, RS>), grid, block, 0, st, a); break;
-    case STS_FILL_LINEAR: hipLaunchKernelGGL((tile_kernel<TW, NT, SHIFTED, NTH, STS_FILL_LINEAR, RS>), grid, block, 0, st, a); break;
-    case STS_FILL_NEAREST: hipLaunchKernelGGL((tile_kernel<TW, NT, SHIFTED, NTH, STS_FILL_NEAREST, RS>), grid, block, 0, st, a); break;
-    case STS_FILL_NEXT: hipLaunchKernelGGL((tile_kernel<TW, NT, SHIFTED, NTH, STS_FILL_NEXT, RS>), grid, block, 0, st, a); break;
-    case STS_FILL_PREVIOUS: hipLaunchKernelGGL((tile_kernel<TW, NT, SHIFTED, NTH, STS_FILL_PREVIOUS, RS>), grid, block, 0, st, a); break;
+    case STS_FILL_NONE: hipLaunchKernelGGL((tile_kernel<TW, NT, SHIFTED, NTH, STS_FILL_NONE>), grid, block, 0, st, a); break;
+    case STS_FILL_LINEAR: hipLaunchKernelGGL((tile_kernel<TW, NT, SHIFTED, NTH, STS_FILL_LINEAR>), grid, block, 0, st, a); break;
+    case STS_FILL_NEAREST: hipLaunchKernelGGL((tile_kernel<TW, NT, SHIFTED, NTH, STS_FILL_NEAREST>), grid, block, 0, st, a); break;
+    case STS_FILL_NEXT: hipLaunchKernelGGL((tile_kernel<TW, NT, SHIFTED, NTH, STS_FILL_NEXT>), grid, block, 0, st, a); break;
+    case STS_FILL_PREVIOUS: hipLaunchKernelGGL((tile_kernel<TW, NT, SHIFTED, NTH, STS_FILL_PREVIOUS>), grid, block, 0, st, a); break;
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
@@ -1290,31 +996,18 @@ hipError_t launch_tile(int method, int tw, const TileArgs& a, hipStream_t st) {
         return launch_m<2048, 4, true, kThreads / 2>(method, grid, a, st);
     }
 #endif
-#if defined(STS_ACF_TW) && STS_ACF_TW == 2048
-    if (tw == 2048 && a.K > 0 && a.K <= 60) {   // A/B builds: 4-wave workgroups on 2048-step tiles
-        if (a.K <= 24) return launch_m<2048, 2, true, kThreads>(method, grid, a, st);
-        return launch_m<2048, 4, true, kThreads>(method, grid, a, st);
-    }
-#endif
     if (tw != 4096) return hipErrorInvalidValue;
     if (a.K == 0) return launch_m<4096, 0, false, kThreads>(method, grid, a, st);
-    // role split (fill waves + MFMA waves, two 8-wave workgroups per CU): STS_TILE_RS builds, or
-    // the A/B build's STS_TILE_RS knob
-    const char* rs_env = ab_knob("STS_TILE_RS");
-    if (rs_env ? std::atoi(rs_env) != 0 : STS_TILE_RS != 0) {
-        if (a.K <= 24) return launch_m<4096, 2, true, 2 * kThreads, true>(method, grid, a, st);
-        if (a.K <= 60) return launch_m<4096, 4, true, 2 * kThreads, true>(method, grid, a, st);
-    }
     if (a.K <= 24) return launch_m<4096, 2, true, kThreads>(method, grid, a, st);
     if (a.K <= 60) return launch_m<4096, 4, true, kThreads>(method, grid, a, st);
     if (a.K <= 63) return launch_m<4096, 5, false, kThreads>(method, grid, a, st);
     return hipErrorInvalidValue;
 }
 
-#if defined(STS_STAMPS) || defined(STS_RS_MSTAMP)
-extern "C" int sts_debug_stamps(unsigned long long* out32) {
-    if (hipMemcpyFromSymbol(out32, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * 32) != hipSuccess) return 4;
-    unsigned long long z[32] = {0};
+#ifdef STS_STAMPS
+extern "C" int sts_debug_stamps(unsigned long long* out16) {
+    if (hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * 16) != hipSuccess) return 4;
+    unsigned long long z[16] = {0};
     return hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), z, sizeof(z)) == hipSuccess ? 0 : 4;
 }
 #endif

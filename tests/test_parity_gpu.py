@@ -327,8 +327,6 @@ KNOB_VARIANTS = {
     "tile2048": {"STS_TILE_KERNEL": "tile", "STS_TILE_W": "2048"},    # 2-wave workgroups, 2048-step tiles
     "tilec4": {"STS_TILE_KERNEL": "tile", "STS_TILES_PER_CHUNK": "4"},  # 4 tiles per workgroup
     "seg3": {"STS_TILE_KERNEL": "seg", "STS_SEG_TILES": "3"},          # multi-segment partials + finalize
-    "tilers": {"STS_TILE_KERNEL": "tile", "STS_TILE_RS": "1"},        # role split: fill waves + MFMA waves
-    "tilersc4": {"STS_TILE_KERNEL": "tile", "STS_TILE_RS": "1", "STS_TILES_PER_CHUNK": "4"},
 }
 
 
@@ -353,27 +351,6 @@ def test_fill_autocorr_both_kernels(torch, ab_lib, kernel, method):
             got = host(uts.fillts(dev(torch, x), method))
             ref, _ = oracle.panel_fill(x, method)
             assert_bits(got, ref, "%s %s T=%d" % (kernel, method, T))
-
-
-@pytest.mark.parametrize("method", ["linear", "previous", "next", "nearest"])
-def test_role_split_tile_kernel_is_bit_identical(torch, ab_lib, method):
-    # the role-split tile kernel (STS_TILE_RS) runs the same chunks per MFMA-wave index in the
-    # same order as the shipped kernel's phase 6: fill AND autocorrelation bit for bit, on
-    # series with long NaN runs, a ragged last tile, and both MFMA decompositions (K <= 24, <= 60)
-    from sparkts import TimeSeriesRDD
-    rng = np.random.default_rng(zlib.crc32(("rs" + method).encode()))
-    for S, T, K in [(3, 70000, 60), (2, 4096 * 17 + 333, 24), (2, 40000, 1)]:
-        x = random_panel(rng, S, T, 0.07, runs=True)
-        x[0, 20000:29000] = NaN                               # a run longer than a tile
-        if method == "nearest":
-            x[:, 1] = 100.0
-        out = []
-        for knobs in ({"STS_TILE_KERNEL": "tile", "STS_TILE_RS": "0"}, {"STS_TILE_KERNEL": "tile", "STS_TILE_RS": "1"}):
-            ab_lib(**knobs)
-            f, a = TimeSeriesRDD(None, None, dev(torch, x)).fillAndAutocorr(method, K)
-            out.append((host(f.data), host(a)))
-        assert_bits(out[1][0], out[0][0], "rs fill %s T=%d" % (method, T))
-        assert_bits(out[1][1], out[0][1], "rs acf %s T=%d K=%d" % (method, T, K))
 
 
 @pytest.mark.parametrize("T", [121, 128, 512, 575, 576, 1000, 1024, 2520, 4097, 16384])

@@ -23,9 +23,6 @@ if os.environ.get("STS_HIP_LIB"):   # a tools/variant.sh build
 
 NAMES = ["regs->LDS", "bar A", "ballots", "bar B", "scan+NaN list", "bar C", "NaN fill", "bar D",
          "store+y+prefetch", "bar E", "MFMA", "bar F"]
-# role split (STS_TILE_RS): the fill waves' wait for the MFMA waves' copy, and the MFMA waves' phases
-RS_NAMES = {13: "fill: wait copied", 16: "mfma: wait F", 17: "mfma: wait slot", 18: "mfma: copy", 19: "mfma: MFMA",
-            20: "mfma: arrive"}
 
 
 def main():
@@ -43,7 +40,7 @@ def main():
     err = torch.zeros(S, dtype=torch.int32, device="cuda")
     sp = torch.cuda.current_stream().cuda_stream
     assert lib.sts_gen_panel(x.data_ptr(), 0, S, T, T, 3, 0.05, sp) == 0
-    buf = np.zeros(32, dtype=np.uint64)
+    buf = np.zeros(16, dtype=np.uint64)
     for it in range(2):
         lib.sts_debug_stamps(buf.ctypes.data)
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -54,15 +51,9 @@ def main():
         torch.cuda.synchronize()
         ms = ev0.elapsed_time(ev1)
         lib.sts_debug_stamps(buf.ctypes.data)
-    tot = max(float(buf[:12].sum() + buf[13]), 1.0)   # 1: an MFMA-wave-only build (-DSTS_RS_MSTAMP)
+    tot = float(buf[:12].sum())
     res = {"S": S, "K": K, "method": method, "ms": ms, "waves": int(buf[12]),
            "share": {n: round(float(buf[i]) / tot, 4) for i, n in enumerate(NAMES)}}
-    if buf[21]:   # role split: fill-wave shares include the copy wait; MFMA-wave shares of their own time
-        res["share"][RS_NAMES[13]] = round(float(buf[13]) / tot, 4)
-        mt = float(sum(buf[i] for i in (16, 17, 18, 19, 20)))
-        res["mfma_waves"] = int(buf[21])
-        res["mfma_share"] = {RS_NAMES[i]: round(float(buf[i]) / mt, 4) for i in (16, 17, 18, 19, 20)}
-        res["cycles_per_wave"] = {"fill": round(tot / max(int(buf[12]), 1)), "mfma": round(mt / int(buf[21]))}
     print(json.dumps(res))
 
 
