@@ -263,10 +263,19 @@ __global__ __launch_bounds__(NTH, STS_TILE_WGS) void tile_kernel(TileArgs a) {
         return e0 >= 0 && e0 + EW <= T && src_al;
     };
     // (a macro, not a lambda: a captured register array would be forced to scratch)
+// non-temporal loads on the fused-ACF instantiations (same-box A/B on the C3 shard, five rounds:
+// 40.83-41.26 against 41.10-41.55 ms, profiles/r05_s19_ab_c3_c5_ntload.jsonl); the fill-only ones
+// (C5) keep plain loads (1.850-1.856 against 1.820-1.826 ms)
 #define STS_LD1(j)                                                                          \
     if constexpr (j < RPT) {                                                                \
         const int q2_ = tid + j * kThreads;                                                 \
-        R##j = s2_[q2_ < NP2 ? q2_ : NP2 - 1];                                              \
+        const double2* p_ = &s2_[q2_ < NP2 ? q2_ : NP2 - 1];                                \
+        if constexpr (NT > 0) {                                                             \
+            const d2v v_ = __builtin_nontemporal_load(reinterpret_cast<const d2v*>(p_));    \
+            R##j = make_double2(v_.x, v_.y);                                                \
+        } else {                                                                            \
+            R##j = *p_;                                                                     \
+        }                                                                                   \
     }
 #define STS_ISSUE(kk)                                                                       \
     do {                                                                                    \

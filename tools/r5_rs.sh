@@ -7,7 +7,7 @@ O=${OUT_DIR:-gpurun_out/r5}
 mkdir -p $O
 set -e
 B=spark-timeseries_amd/build
-timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread -p no:cacheprovider -m gpu \
+[ "${RS_PARITY:-1}" = 0 ] || timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread -p no:cacheprovider -m gpu \
     tests/test_parity_gpu.py -k "tilers or role_split" > $O/rs_parity.log 2>&1
 for rep in 1 2; do
   for V in ${RS_ARMS:-base rs0 rs1 head}; do
