@@ -448,7 +448,7 @@ __global__ __launch_bounds__(64 * NWV, STS_AR_WAVES_PER_EU) void ar_fit_blk_kern
 #pragma unroll
         for (int i = 0; i < B / 2; i++) {
             const int u = 2 * (i * 64 + lane);   // series position of this lane's 16-B piece
-            glds16(xg + (u < T ? u : 0), lb + i * 1024);
+            glds16<true>(xg + (u < T ? u : 0), lb + i * 1024);   // nt loads + nt stores: C4 4.121-4.128 vs 4.149 ms
         }
         dma_wait();
         wave_lds_sync();
@@ -709,7 +709,7 @@ __global__ __launch_bounds__(64 * NWV, STS_AR_WAVES_PER_EU) void ar_fit_blk_kern
 #pragma unroll
         for (int i = 0; i < B / 2; i++) {
             const int u = 2 * (i * 64 + lane);
-            if (u < T) *reinterpret_cast<double2*>(dst + u) = *reinterpret_cast<const double2*>(buf + u);
+            if (u < T) store_pair16<true>(dst + u, buf + u);
         }
     }
 #ifdef STS_STAMPS

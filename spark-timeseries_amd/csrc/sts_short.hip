@@ -180,7 +180,7 @@ __global__ __launch_bounds__(64 * kShortWaves, 2) void short_fill_acf_kernel(Til
 #pragma unroll
         for (int i = 0; i < B / 2; i++) {
             const int u = 2 * (i * 64 + lane);
-            if (u < T) *reinterpret_cast<double2*>(dst + u) = *reinterpret_cast<const double2*>(buf + u);
+            if (u < T) store_pair16<true>(dst + u, buf + u);   // nt stores: C1 0.0926 vs 0.1030 ms (nt loads too: 0.098)
         }
     }
     if (a.err && lane == 0) a.err[s] = all_nan ? STS_ERR_ALL_NAN : STS_OK;
