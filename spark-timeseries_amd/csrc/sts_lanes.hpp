@@ -39,6 +39,19 @@ __device__ __forceinline__ double row_sum_dpp(double v) {
 }
 // lane l - 1's value (wave_shr:1; lane 0 gets 0)
 __device__ __forceinline__ double lane_prev(double v) { return dpp_d<0x138>(v); }
+// lane l + 1's value (wave_shl:1; lane 63 gets 0)
+__device__ __forceinline__ double lane_next(double v) { return dpp_d<0x130>(v); }
+// inclusive suffix sum over lanes l .. 63: row_shl 1 / 2 / 4 / 8 inside the rows of 16 (lanes
+// past the row end contribute 0), then the totals of the rows above from lanes 16 / 32 / 48
+__device__ __forceinline__ double suffix_sum_dpp(double v, int lane) {
+    v = v + dpp_d<0x101>(v);
+    v = v + dpp_d<0x102>(v);
+    v = v + dpp_d<0x104>(v);
+    v = v + dpp_d<0x108>(v);
+    const double r3 = lane_bcast(v, 48), r2 = lane_bcast(v, 32) + r3, r1 = lane_bcast(v, 16) + r2;
+    const int row = lane >> 4;
+    return row == 3 ? v : v + (row == 2 ? r3 : row == 1 ? r2 : r1);
+}
 
 // Bijective XCD-aware remap of a workgroup id (cdna_hip_programming.md §5 "XCD swizzle must be
 // bijective"): workgroups go to the 8 XCDs round-robin (b % 8); this hands XCD x one contiguous

@@ -254,23 +254,14 @@ __global__ __launch_bounds__(64 * kShortWaves, 2) void short_fill_acf_kernel(Til
     //      = y[i..64) of the head + the whole tail + the middle, slice 2 = the whole head +
     //      z[i..64) of the tail + the middle; every partial is a sum of its own terms (suffix
     //      scans over the lanes, no "total minus head") ----
-    double ys = yh, yq = yh * yh, zs = zt, zq = zt * zt;   // suffix sums from lane .. 63
-#pragma unroll
-    for (int k = 1; k < 64; k <<= 1) {
-        const double a0 = __shfl_down(ys, k), a1 = __shfl_down(yq, k), a2 = __shfl_down(zs, k),
-                     a3 = __shfl_down(zq, k);
-        if (lane + k < 64) {
-            ys += a0;
-            yq += a1;
-            zs += a2;
-            zq += a3;
-        }
-    }
+    // suffix sums from lane .. 63 by DPP (round 5: the ds_bpermute scan it replaces was ~1/3 of the
+    // finalize's latency)
+    const double ys = suffix_sum_dpp(yh, lane), yq = suffix_sum_dpp(yh * yh, lane);
+    const double zs = suffix_sum_dpp(zt, lane), zq = suffix_sum_dpp(zt * zt, lane);
     const double Yall = lane_bcast(ys, 0), YQall = lane_bcast(yq, 0), Zall = lane_bcast(zs, 0),
                  ZQall = lane_bcast(zq, 0);
     // lag i = lane + 1 wants the suffixes from position i: lane i's (none for i = 64)
-    double ysi = __shfl_down(ys, 1), yqi = __shfl_down(yq, 1), zsi = __shfl_down(zs, 1), zqi = __shfl_down(zq, 1);
-    if (lane == 63) ysi = yqi = zsi = zqi = 0.0;
+    const double ysi = lane_next(ys), yqi = lane_next(yq), zsi = lane_next(zs), zqi = lane_next(zq);
     const double sum1 = (Sm + Zall) + ysi, sq1 = (Qm + ZQall) + yqi;
     const double sum2 = (Sm + Yall) + zsi, sq2 = (Qm + YQall) + zqi;
     const double N = (double)(T - (lane + 1));
