@@ -164,5 +164,20 @@ case "$SESSION" in
     bash tools/ab_bench.sh c1 c1dpp base >> $O/ab_c1dpp.jsonl
     bash tools/sessions_r5.sh s24
     ;;
-  *) echo "usage: $0 {c1ab|rs|rs_sq|s18|s19|s20|s21|s22|s23|s24|s25}" >&2; exit 2 ;;
+  s27)
+    # the tile kernel with y formed in registers by the MFMA phase (var_yreg, STS_TILE_YREG=1): parity of
+    # the tile / fill + ACF / robust-ACF rows, then C3 kernel A/B, three alternating rounds
+    set -e
+    O=gpurun_out/r5; mkdir -p $O
+    timeout -k 10 600 python -u -m pytest -x -q --timeout 200 --timeout-method thread -p no:cacheprovider -m gpu tests/test_parity_gpu.py tests/test_acf_robust.py \
+        -k "tile or fill_acf or autocorr or c3" --sts-lib spark-timeseries_amd/build/var_yreg/libsts_hip.so > $O/yreg_parity.log 2>&1
+    for rep in 1 2 3; do
+      for V in base yreg; do
+        L=spark-timeseries_amd/build/libsts_hip.so; [ $V != base ] && L=spark-timeseries_amd/build/var_$V/libsts_hip.so
+        STS_HIP_LIB=$L timeout -k 10 300 python -u tools/kbench.py --series 12500 --reps 3 --cases tile:linear:60 \
+          | grep -v amdgpu.ids | sed "s/^{/{\"lib\": \"$V\", \"rep\": $rep, /" >> $O/ab_c3_yreg.jsonl
+      done
+    done
+    ;;
+  *) echo "usage: $0 {c1ab|rs|rs_sq|s18|s19|s20|s21|s22|s23|s24|s25|s27}" >&2; exit 2 ;;
 esac
