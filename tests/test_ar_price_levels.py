@@ -16,6 +16,7 @@ recorded as information only (STS_AR_LEVELS_JSON).
 """
 import json
 import os
+import zlib
 from fractions import Fraction
 
 import numpy as np
@@ -298,3 +299,49 @@ def test_gpu_ar_rule_constant_and_near_constant_series(torch):
             assert_same_bits(np.r_[c.item(), coef.cpu().numpy()[0]], np.r_[rc, rcoef], "row %r" % x[:2])
         except oracle.OracleError as e:   # the reference throws: same status on the device
             assert int(err.item()) == e.code, (int(err.item()), e.code)
+
+
+def family_series(kind, level, sigma, T, seed):
+    """Series shapes of the calibration study (tools/ar_flag_study.py) beyond the random walk."""
+    rng = np.random.default_rng(seed)
+    if kind == "ar1":   # stationary AR(1), phi = 0.9, around the level
+        e = rng.standard_normal(T) * sigma
+        y = np.empty(T)
+        y[0] = e[0]
+        for t in range(1, T):
+            y[t] = 0.9 * y[t - 1] + e[t]
+        return level + y
+    if kind == "noise":
+        return level + rng.standard_normal(T) * sigma
+    if kind == "trend":
+        return level + sigma * (np.arange(T) / T * 10 + rng.uniform(-0.5, 0.5, T))
+    if kind == "walk2":   # integrated random walk: nearly collinear lags
+        return level + np.cumsum(np.cumsum(rng.standard_normal(T))) * sigma
+    if kind == "sine":    # smooth: collinear lags
+        t = np.arange(T)
+        return level + sigma * (np.sin(2 * np.pi * t / 500.0) + 1e-3 * rng.standard_normal(T))
+    raise ValueError(kind)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["ar1", "noise", "trend", "walk2", "sine"])
+@pytest.mark.parametrize("p", [1, 2, 5, 8, 16])
+def test_gpu_ar_fit_series_families(torch, kind, p):
+    # every family of the calibration study at levels 0 .. 1e6 and two spreads, in one panel per
+    # (family, p): device vs oracle <= 1e-10 elementwise on every row, whichever path the rule
+    # sends it down
+    rows, tags = [], []
+    for T in (700, 2520, 6000):   # 6000: the long-series fit kernel; p = 16: staged kernel + wave QR
+        for level in (0.0, 1e2, 1e4, 1e6):
+            for sigma in (1.0, 1e-2):
+                seed = zlib.crc32(repr((kind, p, T, level, sigma)).encode())   # deterministic (hash() of str is salted)
+                rows.append((T, family_series(kind, level, sigma, T, seed)))
+                tags.append((T, level, sigma))
+    for T in (700, 2520, 6000):
+        xs = np.stack([x for t, x in rows if t == T])
+        tg = [g for g in tags if g[0] == T]
+        got = fit_gpu(torch, xs, p, False)
+        for s in range(xs.shape[0]):
+            rc, rcoef = oracle.ar_fit(xs[s], p)
+            e = elementwise(got[s], np.r_[rc, rcoef])
+            assert e <= ELEM_TOL, (kind, p, tg[s], e)
