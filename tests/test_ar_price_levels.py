@@ -327,12 +327,12 @@ def family_series(kind, level, sigma, T, seed):
 @pytest.mark.parametrize("kind", ["ar1", "noise", "trend", "walk2", "sine"])
 @pytest.mark.parametrize("p", [1, 2, 5, 8, 16])
 def test_gpu_ar_fit_series_families(torch, kind, p):
-    # every family of the calibration study at levels 0 .. 1e6 and two spreads, in one panel per
+    # every family of the calibration study at levels 0 .. 1e6 (and -3e5) and two spreads, in one panel per
     # (family, p): device vs oracle <= 1e-10 elementwise on every row, whichever path the rule
     # sends it down
     rows, tags = [], []
     for T in (700, 2520, 6000):   # 6000: the long-series fit kernel; p = 16: staged kernel + wave QR
-        for level in (0.0, 1e2, 1e4, 1e6):
+        for level in (0.0, 1e2, 1e4, 1e6, -3e5):
             for sigma in (1.0, 1e-2):
                 seed = zlib.crc32(repr((kind, p, T, level, sigma)).encode())   # deterministic (hash() of str is salted)
                 rows.append((T, family_series(kind, level, sigma, T, seed)))
