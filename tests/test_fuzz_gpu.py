@@ -1,0 +1,109 @@
+"""Randomised parity sweeps through the product library (seeded, deterministic).
+
+Every case draws a panel shape (T log-uniform over 2 .. 40 000, so the short, segment and tile
+kernels all run), a fill method, numLags, a NaN rate with or without long runs, a level and a
+series family, and checks the fused fill + autocorr against the oracle: the fill bit for bit,
+the ACF within the tolerance contract of tests/test_acf_robust.py (1e-10 relative plus the
+reference's own rounding-noise floor, computed on the filled series).  A second sweep does the
+same for the AR(p) fit (both intercept modes, 1e-10 elementwise against commons-math3's
+Householder QR as restated in the oracle).  These complement the hand-picked edge cases of
+test_parity_gpu.py with breadth."""
+import os
+import zlib
+
+import numpy as np
+import pytest
+
+import oracle
+from test_acf_robust import noise_floor, within
+
+METHODS = ["linear", "previous", "next", "nearest"]
+# STS_FUZZ_SCALE=n multiplies the number of cases (a deeper one-off sweep; default 1)
+SCALE = int(os.environ.get("STS_FUZZ_SCALE", "1"))
+
+
+@pytest.fixture(scope="module")
+def torch():
+    import torch as _t
+    if not _t.cuda.is_available():
+        pytest.skip("no GPU")
+    from sparkts import _native
+    _native.ensure_device(0)
+    return _t
+
+
+def fuzz_panel(rng, S, T, family, level, nan_p, runs):
+    if family == "walk":
+        x = level + np.cumsum(rng.standard_normal((S, T)), axis=1) * 0.1
+    elif family == "noise":
+        x = level + rng.standard_normal((S, T))
+    elif family == "ar1":
+        e = rng.standard_normal((S, T))
+        x = np.empty((S, T))
+        x[:, 0] = e[:, 0]
+        for t in range(1, T):
+            x[:, t] = 0.95 * x[:, t - 1] + e[:, t]
+        x += level
+    else:   # steps: piecewise constant with a few jumps
+        x = level + np.cumsum((rng.random((S, T)) < 0.01) * rng.standard_normal((S, T)), axis=1)
+    x[rng.random((S, T)) < nan_p] = np.nan
+    if runs and T > 10:
+        for s in range(S):
+            a = int(rng.integers(0, T))
+            x[s, a: min(T, a + int(rng.integers(1, max(2, T // 4))))] = np.nan
+    return x
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", range(40 * SCALE))
+def test_fuzz_fill_autocorr(torch, case):
+    from sparkts import TimeSeriesRDD
+    rng = np.random.default_rng(zlib.crc32(b"fuzz-acf-%d" % case))
+    T = int(np.exp(rng.uniform(np.log(2), np.log(40000))))
+    S = int(rng.integers(1, 9))
+    method = METHODS[case % 4]
+    K = int(rng.integers(1, max(2, min(61, T))))
+    family = ["walk", "noise", "ar1", "steps"][int(rng.integers(0, 4))]
+    level = float(rng.choice([0.0, 100.0, 1e4, 1e6]))
+    x = fuzz_panel(rng, S, T, family, level, float(rng.choice([0.0, 0.02, 0.1, 0.4])), bool(rng.integers(0, 2)))
+    if method == "nearest" and T > 1:
+        x[:, 1] = level + 1.0   # a valid step after index 0: no "Input is all NaNs!"
+    filled, acf = TimeSeriesRDD(None, None, torch.as_tensor(x, device="cuda:0")).fillAndAutocorr(method, K)
+    rf, racf, err = oracle.panel_fill_autocorr(x, method, K)
+    assert (err == 0).all()
+    f = filled.data.cpu().numpy()
+    same = (f.view(np.uint64) == rf.view(np.uint64)) | (np.isnan(f) & np.isnan(rf))
+    assert same.all(), (case, T, method, int((~same).sum()))
+    got = acf.cpu().numpy()
+    for s in range(S):
+        w = within(got[s], racf[s], noise_floor(rf[s], K))
+        assert w <= 1.0, (case, s, T, K, method, family, level, w)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", range(24 * SCALE))
+def test_fuzz_ar_fit(torch, case):
+    from sparkts.models import Autoregression
+    rng = np.random.default_rng(zlib.crc32(b"fuzz-ar-%d" % case))
+    p = int(rng.integers(1, 9))
+    T = int(rng.integers(2 * p + 3, 6001))
+    S = int(rng.integers(1, 40))
+    no_int = bool(case % 3 == 2)
+    family = ["walk", "noise", "ar1"][int(rng.integers(0, 3))]   # (piecewise-constant rows can be singular)
+    level = float(rng.choice([0.0, 10.0, 1e3, 1e5, -2e4]))
+    x = fuzz_panel(rng, S, T, family, level, 0.0, False)
+    m = Autoregression.fitModel(torch.as_tensor(x, device="cuda:0"), p, no_int)
+    c = np.atleast_1d(m.c.cpu().numpy()) if hasattr(m.c, "cpu") else np.full(S, m.c)
+    coef = m.coefficients.cpu().numpy().reshape(S, p)
+    for s in range(S):
+        rc, rcoef = oracle.ar_fit(x[s], p, no_int)
+        ref = np.r_[rc, rcoef]
+        got = np.r_[c[s], coef[s]]
+        if no_int:
+            ref, got = ref[1:], got[1:]
+        if not np.all(np.isfinite(ref)):
+            assert np.array_equal(np.isnan(got), np.isnan(ref)), (case, s)
+            continue
+        big = np.abs(ref) > 1e-6 * np.linalg.norm(ref)
+        e = float(np.max(np.abs(got[big] - ref[big]) / np.abs(ref[big])))
+        assert e <= 1e-10, (case, s, p, T, no_int, family, level, e)
