@@ -107,3 +107,56 @@ def test_fuzz_ar_fit(torch, case):
         big = np.abs(ref) > 1e-6 * np.linalg.norm(ref)
         e = float(np.max(np.abs(got[big] - ref[big]) / np.abs(ref[big])))
         assert e <= 1e-10, (case, s, p, T, no_int, family, level, e)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", range(24 * SCALE))
+def test_fuzz_fill_diff_ewma(torch, case):
+    # C2's fused pipeline: fillPrevious -> differencesAtLag(lag) -> EWMA add, bit for bit
+    from sparkts import _native
+    rng = np.random.default_rng(zlib.crc32(b"fuzz-c2-%d" % case))
+    T = int(np.exp(rng.uniform(np.log(2), np.log(3000))))
+    S = int(rng.integers(1, 70))
+    lag = int(rng.integers(1, max(2, min(6, T))))
+    family = ["walk", "noise", "steps"][int(rng.integers(0, 3))]
+    x = fuzz_panel(rng, S, T, family, float(rng.choice([0.0, 100.0, 1e6])), float(rng.choice([0.0, 0.05, 0.3])),
+                   bool(rng.integers(0, 2)))
+    s = rng.uniform(0.01, 0.99, S)
+    xd = torch.as_tensor(x, device="cuda:0")
+    out = torch.empty_like(xd)
+    sd = torch.as_tensor(s, device="cuda:0")
+    assert _native.lib().sts_fill_diff_ewma(xd.data_ptr(), out.data_ptr(), S, T, T, T, 3, lag, sd.data_ptr(),
+                                            None, None) == 0
+    ref = np.array([oracle.ewma_add(oracle.differences_at_lag(oracle.fill_previous(r), lag), float(si))
+                    for r, si in zip(x, s)])
+    got = out.cpu().numpy()
+    same = (got.view(np.uint64) == ref.view(np.uint64)) | (np.isnan(got) & np.isnan(ref))
+    assert same.all(), (case, S, T, lag, int((~same).sum()))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", range(16 * SCALE))
+def test_fuzz_fill_lag_matrix(torch, case):
+    # C5's fused pipeline: fill(method) -> lag(p, includeOriginal), bit for bit
+    from sparkts import _native
+    from sparkts import UnivariateTimeSeries as uts
+    rng = np.random.default_rng(zlib.crc32(b"fuzz-c5-%d" % case))
+    T = int(np.exp(rng.uniform(np.log(16), np.log(30000))))
+    S = int(rng.integers(1, 6))
+    p = int(rng.integers(1, min(12, T - 1)))
+    inc = int(rng.integers(0, 2))
+    method = METHODS[case % 4]
+    x = fuzz_panel(rng, S, T, "walk", 100.0, float(rng.choice([0.0, 0.05, 0.3])), bool(rng.integers(0, 2)))
+    x[:, 1] = 100.0   # nearest: a valid step after index 0
+    xd = torch.as_tensor(x, device="cuda:0")
+    filled = torch.empty_like(xd)
+    ncol = p + inc
+    lm = torch.empty((S, ncol, T - p), dtype=torch.float64, device="cuda:0")
+    assert _native.lib().sts_fill_lag_matrix(xd.data_ptr(), filled.data_ptr(), lm.data_ptr(), S, T, T, T,
+                                             uts.fill_method_code(method), p, inc, None, None) == 0
+    rf, _ = oracle.panel_fill(x, method)
+    f = filled.cpu().numpy()
+    assert ((f.view(np.uint64) == rf.view(np.uint64)) | (np.isnan(f) & np.isnan(rf))).all(), (case, "fill")
+    ref = np.array([oracle.lag(r, p, bool(inc)) for r in rf])   # (S, rows, cols)
+    got = lm.cpu().numpy().transpose(0, 2, 1)
+    assert ((got.view(np.uint64) == ref.view(np.uint64)) | (np.isnan(got) & np.isnan(ref))).all(), (case, "lag")
