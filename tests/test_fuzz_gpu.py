@@ -160,3 +160,23 @@ def test_fuzz_fill_lag_matrix(torch, case):
     ref = np.array([oracle.lag(r, p, bool(inc)) for r in rf])   # (S, rows, cols)
     got = lm.cpu().numpy().transpose(0, 2, 1)
     assert ((got.view(np.uint64) == ref.view(np.uint64)) | (np.isnan(got) & np.isnan(ref))).all(), (case, "lag")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", range(12 * SCALE))
+def test_fuzz_ewma_fit(torch, case):
+    # EWMA.fitModel (commons-math3 nonlinear CG + bracketing + Brent per series): the smoothing
+    # parameter bit for bit and the same per-series errors as the restatement
+    from sparkts.models import EWMA
+    rng = np.random.default_rng(zlib.crc32(b"fuzz-ewma-%d" % case))
+    T = int(np.exp(rng.uniform(np.log(2), np.log(1500))))
+    S = int(rng.integers(1, 70))
+    family = ["walk", "noise", "ar1", "steps"][int(rng.integers(0, 4))]
+    x = fuzz_panel(rng, S, T, family, float(rng.choice([0.0, 100.0, 1e4])), 0.0, False)
+    err = torch.zeros(S, dtype=torch.int32, device="cuda:0")
+    m = EWMA.fitModel(torch.as_tensor(x, device="cuda:0"), errors=err)
+    ref_s, ref_err = oracle.panel_ewma_fit(x, threads=8)
+    assert np.array_equal(err.cpu().numpy(), ref_err), case
+    got = np.asarray(m.smoothing.cpu().numpy(), dtype=np.float64)
+    same = (got.view(np.uint64) == ref_s.view(np.uint64)) | (np.isnan(got) & np.isnan(ref_s))
+    assert same.all(), (case, S, T, family, int((~same).sum()))
