@@ -180,3 +180,28 @@ def test_fuzz_ewma_fit(torch, case):
     got = np.asarray(m.smoothing.cpu().numpy(), dtype=np.float64)
     same = (got.view(np.uint64) == ref_s.view(np.uint64)) | (np.isnan(got) & np.isnan(ref_s))
     assert same.all(), (case, S, T, family, int((~same).sum()))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", range(6 * SCALE))
+def test_fuzz_garch_fit(torch, case):
+    # GARCH.fitModel (commons-math3 CG without a GoalType, per series): (omega, alpha, beta) bit for
+    # bit and the same per-series errors as the restatement, over random GARCH(1,1) samples
+    from sparkts.models import GARCH
+    from test_garch import MersenneTwister, garch_sample
+    rng = np.random.default_rng(zlib.crc32(b"fuzz-garch-%d" % case))
+    T = int(rng.integers(40, 700))
+    S = int(rng.integers(1, 12))
+    rows = []
+    for s in range(S):
+        om, al = float(rng.uniform(0.05, 0.5)), float(rng.uniform(0.02, 0.4))
+        be = float(rng.uniform(0.0, 0.95 - al))
+        rows.append(garch_sample(om, al, be, T, MersenneTwister(int(rng.integers(1, 2**31)))))
+    x = np.array(rows)
+    err = torch.zeros(S, dtype=torch.int32, device="cuda:0")
+    m = GARCH.fitModel(torch.as_tensor(x, device="cuda:0"), errors=err)
+    got = np.stack([m.omega.cpu().numpy(), m.alpha.cpu().numpy(), m.beta.cpu().numpy()], axis=1)
+    rpar, rerr = oracle.panel_garch_fit(x)
+    assert np.array_equal(err.cpu().numpy(), rerr), case
+    same = (got.view(np.uint64) == rpar.view(np.uint64)) | (np.isnan(got) & np.isnan(rpar))
+    assert same.all(), (case, S, T, int((~same).sum()))
