@@ -205,3 +205,33 @@ def test_fuzz_garch_fit(torch, case):
     assert np.array_equal(err.cpu().numpy(), rerr), case
     same = (got.view(np.uint64) == rpar.view(np.uint64)) | (np.isnan(got) & np.isnan(rpar))
     assert same.all(), (case, S, T, int((~same).sum()))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", range(12 * SCALE))
+def test_fuzz_stats_instants(torch, case):
+    # seriesStats (Spark StatCounter per series), removeInstantsWithNaNs and toInstants on random
+    # shapes, magnitudes, NaN / inf patterns: bit for bit
+    from sparkts.timeseriesrdd import TimeSeriesRDD
+    rng = np.random.default_rng(zlib.crc32(b"fuzz-f2-%d" % case))
+    S = int(np.exp(rng.uniform(0, np.log(400))))
+    T = int(np.exp(rng.uniform(0, np.log(6000))))
+    x = rng.standard_normal((S, T)) * 10.0 ** rng.integers(-200, 200, size=(S, 1))
+    if rng.random() < 0.5:
+        x[rng.random((S, T)) < float(rng.choice([1e-4, 1e-3, 0.02]))] = np.nan
+    if rng.random() < 0.3:
+        x[rng.random((S, T)) < 1e-3] = np.inf * rng.choice([-1.0, 1.0])
+    st = TimeSeriesRDD(None, None, torch.as_tensor(x, device="cuda:0")).seriesStats()
+    ref = np.array([oracle.stat_counter(r)[1:] for r in x])
+    got = st.stats.cpu().numpy()[:, :4]
+    same = (got.view(np.uint64) == ref.view(np.uint64)) | (np.isnan(got) & np.isnan(ref))
+    assert same.all(), (case, S, T, "stats", int((~same).sum()))
+    r = TimeSeriesRDD(None, None, torch.as_tensor(x, device="cuda:0")).removeInstantsWithNaNs()
+    rref, active = oracle.remove_instants_with_nans(x)
+    assert np.array_equal(r.index, active), (case, "instants")
+    g = r.data.cpu().numpy().reshape(rref.shape)
+    assert ((g.view(np.uint64) == rref.view(np.uint64)) | (np.isnan(g) & np.isnan(rref))).all(), (case, "gather")
+    _, inst = TimeSeriesRDD(None, None, torch.as_tensor(x, device="cuda:0")).toInstants()
+    ti = inst.cpu().numpy()
+    tref = oracle.to_instants(x)
+    assert ((ti.view(np.uint64) == tref.view(np.uint64)) | (np.isnan(ti) & np.isnan(tref))).all(), (case, "toInstants")
