@@ -235,3 +235,26 @@ def test_fuzz_stats_instants(torch, case):
     ti = inst.cpu().numpy()
     tref = oracle.to_instants(x)
     assert ((ti.view(np.uint64) == tref.view(np.uint64)) | (np.isnan(ti) & np.isnan(tref))).all(), (case, "toInstants")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", range(12 * SCALE))
+def test_fuzz_ar_fit_remove(torch, case):
+    # C4's fused fit + removeTimeDependentEffects: the model at 1e-10 elementwise against the
+    # reference's QR, the residuals bit for bit given the device's own model
+    from sparkts.models import Autoregression
+    rng = np.random.default_rng(zlib.crc32(b"fuzz-c4-%d" % case))
+    p = int(rng.integers(1, 9))
+    T = int(rng.integers(2 * p + 3, 4001))
+    S = int(rng.integers(1, 90))
+    family = ["walk", "noise", "ar1"][int(rng.integers(0, 3))]
+    x = fuzz_panel(rng, S, T, family, float(rng.choice([0.0, 1.0, 1e3, 1e6])), 0.0, False)
+    m, resid = Autoregression.fitModelAndRemove(torch.as_tensor(x, device="cuda:0"), p)
+    c, coef, res = m.c.cpu().numpy(), m.coefficients.cpu().numpy().reshape(S, p), resid.cpu().numpy()
+    for s in range(S):
+        rc, rcoef = oracle.ar_fit(x[s], p)
+        ref, got = np.r_[rc, rcoef], np.r_[c[s], coef[s]]
+        big = np.abs(ref) > 1e-6 * np.linalg.norm(ref)
+        assert float(np.max(np.abs(got[big] - ref[big]) / np.abs(ref[big]))) <= 1e-10, (case, s, p, T, family)
+        rr = oracle.ar_remove(x[s], c[s], coef[s])
+        assert (res[s].view(np.uint64) == rr.view(np.uint64)).all(), (case, s, "residuals")
