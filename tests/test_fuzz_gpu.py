@@ -258,3 +258,47 @@ def test_fuzz_ar_fit_remove(torch, case):
         assert float(np.max(np.abs(got[big] - ref[big]) / np.abs(ref[big]))) <= 1e-10, (case, s, p, T, family)
         rr = oracle.ar_remove(x[s], c[s], coef[s])
         assert (res[s].view(np.uint64) == rr.view(np.uint64)).all(), (case, s, "residuals")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", range(8 * SCALE))
+def test_fuzz_host_entry_points(torch, case):
+    # the _host entry points: host panels through the pinned staging pipeline (chunked by series,
+    # padded row strides), the same bits as the oracle -- fills, the fused fill + ACF (contract),
+    # C2's fused pipeline
+    import ctypes
+    from sparkts import _native
+    lib = _native.lib()
+    P = lambda a: a.ctypes.data_as(ctypes.c_void_p)   # noqa: E731
+    rng = np.random.default_rng(zlib.crc32(b"fuzz-host-%d" % case))
+    T = int(np.exp(rng.uniform(np.log(4), np.log(20000))))
+    S = int(np.exp(rng.uniform(0, np.log(max(2, 4e7 // (8 * T))))))   # up to ~40 MB panels: several chunks
+    pad = int(rng.integers(0, 3))
+    ld = T + pad
+    method = int(rng.integers(0, 4))   # STS_FILL_LINEAR .. STS_FILL_PREVIOUS
+    xb = fuzz_panel(rng, S, ld, "walk", 100.0, float(rng.choice([0.0, 0.05, 0.3])), bool(rng.integers(0, 2)))
+    xb[:, 1] = 100.0
+    x = np.ascontiguousarray(xb)
+    out = np.full((S, ld), -1.0)
+    err = np.zeros(S, dtype=np.int32)
+    assert lib.sts_fill_host(P(x), P(out), S, T, ld, method, P(err)) == 0, lib.sts_last_error()
+    name = {0: "linear", 1: "nearest", 2: "next", 3: "previous"}[method]
+    rf, rerr = oracle.panel_fill(x[:, :T].copy(), name)
+    assert np.array_equal(err, rerr)
+    got = out[:, :T]
+    assert ((got.view(np.uint64) == rf.view(np.uint64)) | (np.isnan(got) & np.isnan(rf))).all(), (case, "fill_host")
+    if T >= 2:
+        K = int(rng.integers(1, min(61, T)))
+        acf = np.empty((S, K))
+        filled = np.empty((S, ld))
+        assert lib.sts_fill_autocorr_host(P(x), P(filled), S, T, ld, method, K, P(acf), P(err)) == 0, lib.sts_last_error()
+        _, racf, _ = oracle.panel_fill_autocorr(x[:, :T].copy(), name, K)
+        for s in range(0, S, max(1, S // 16)):
+            assert within(acf[s], racf[s], noise_floor(rf[s], K)) <= 1.0, (case, s, "fill_autocorr_host")
+    sm = rng.uniform(0.05, 0.95, S)
+    o2 = np.empty((S, ld))
+    assert lib.sts_fill_diff_ewma_host(P(x), P(o2), S, T, ld, 3, 1, P(sm), P(err)) == 0, lib.sts_last_error()
+    for s in range(0, S, max(1, S // 16)):
+        r = oracle.ewma_add(oracle.differences_at_lag(oracle.fill_previous(x[s, :T]), 1), float(sm[s]))
+        g = o2[s, :T]
+        assert ((g.view(np.uint64) == r.view(np.uint64)) | (np.isnan(g) & np.isnan(r))).all(), (case, s, "c2_host")
