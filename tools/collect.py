@@ -35,11 +35,17 @@ def pmc_values(d, counter, kernel=KERNEL):
 # FP64 pipe counters (tools/gpu_all.sh fp64_<wl>): one --pmc pass per workload
 FP64_COUNTERS = ["SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_ADD_F64",
                  "SQ_INSTS_VALU_MFMA_MOPS_F64", "SQ_VALU_MFMA_BUSY_CYCLES", "GRBM_GUI_ACTIVE"]
-FP64_KERNELS = {"c3": "tile_kernel", "c4": "ar_fit_blk_kernel"}
+FP64_KERNELS = {"c3": "tile_kernel", "c4": "ar_fit_blk_kernel", "ewma_fit": "ewma_fit_kernel",
+                "garch_fit": "garch_fit_kernel"}
 # dominant kernel per workload (the c3 passes are of the default `python bench.py` command;
 # c3 directories keep their round-1 names pmc_fetch_c3 / pmc_write_c3 / prof_c3)
 TRAFFIC_KERNELS = {"c3": "tile_kernel", "c1": "short_fill_acf_kernel", "c2": "recur_row_kernel", "c4": "ar_fit_blk_kernel",
-                   "c5": "tile_kernel"}
+                   "c5": "tile_kernel",
+                   # the f rows; nan_instants: both of its kernels ("_instants" matches
+                   # nan_instants16_kernel and gather_instants_kernel), per launch like bench.py's figure
+                   "ewma_fit": "ewma_fit_kernel", "stats": "stats_fast_kernel", "nan_instants": "_instants",
+                   "to_instants": "transpose16_kernel", "wire_decode": "wire_decode_rows_kernel",
+                   "garch_fit": "garch_fit_kernel", "stage_c2": "recur_row_kernel"}
 
 
 def collect_fp64(tag, wl):
