@@ -34,6 +34,9 @@
 #ifndef STS_STATS_CH
 #define STS_STATS_CH 16               // seriesStats chunk (steps staged per series)
 #endif
+#ifndef STS_STATS_LA
+#define STS_STATS_LA 1                // seriesStats chunks on 128-B line boundaries (stats_fast_kernel)
+#endif
 
 namespace sts {
 namespace {
@@ -135,62 +138,111 @@ __device__ __forceinline__ double newton_rcp(double b) {
     return __builtin_fma(y, e, y);
 }
 
-template <int SPW, int CH>
+// LA (line-aligned chunks): the chunks of row r start at the 128-B line boundaries of ITS
+// addresses, t = tc + col - off(r) with off(r) = (address of step 0 / 8) mod 16, so every
+// staged row segment is whole L2 lines.  With chunks aligned on the series' steps
+// instead, a row whose stride is not a multiple of 128 B (390 steps: 3 120 B) straddles two
+// lines per chunk and the other half is evicted before the next chunk asks for it: 1.74x the
+// panel's bytes fetched on 1M x 390 (profiles/r05_final_stats_traffic.json).  The per-step
+// arithmetic and its order are unchanged (same bits); only which chunk a step is staged in moves.
+template <int SPW, int CH, bool LA>
 __global__ __launch_bounds__(64) void stats_fast_kernel(const double* __restrict__ in, double* __restrict__ out,
                                                         int64_t S, int64_t T, int64_t ld) {
     constexpr int kRow = CH + 1;
     constexpr int NLD = SPW * CH / 64;
-    static_assert(CH <= 64, "one lane per step of the reciprocal table");
+    constexpr int kOff = LA ? CH - 1 : 0;   // largest lead-in of a row (doubles before its step 0)
+    static_assert(CH + kOff <= 64, "one lane per step of the reciprocal table");
+    static_assert(!LA || (CH % 16 == 0), "LA: a chunk row is whole 128-B lines");
     __shared__ double tile[SPW * kRow];
-    __shared__ double ytab[CH], nbtab[CH];
+    __shared__ double ytab[CH + kOff], nbtab[CH + kOff];
     const int lane = threadIdx.x;
     const int64_t s0 = (int64_t)blockIdx.x * SPW;
     const bool live = lane < SPW && s0 + lane < S;
     const int ns = (S - s0 < SPW) ? (int)(S - s0) : SPW;
     const double* base = in + s0 * ld;
-    double mu = 0.0, m2 = 0.0, mx = -__builtin_inf(), mn = __builtin_inf();
-    double pre[NLD];
-    auto fetch = [&](int64_t tc) {   // clamped loads, no branches around the prefetch registers
+    // off(row) = (address of row's step 0 / 8) mod CH (only the low bits of row * ld matter)
+    const unsigned o0 = (unsigned)(reinterpret_cast<uintptr_t>(base) >> 3), lm = (unsigned)ld;
+    auto roff = [&](int row) -> int { return LA ? (int)((o0 + (unsigned)row * lm) & 15u) : 0; };
+    int tend = (int)T;   // chunks run while some row of the wave still has steps: tc < T + max off
+    if (LA) {
+        int mo = live ? roff(lane) : 0;
 #pragma unroll
-        for (int i = 0; i < NLD; i++) {
-            const int row = (i * 64 + lane) / CH, col = (i * 64 + lane) % CH;
-            const int rr = row < ns ? row : ns - 1;
-            const int64_t cc = (tc + col < T) ? tc + col : T - 1;
-            pre[i] = base[rr * ld + cc];
+        for (int d = 32; d >= 1; d >>= 1) {
+            const int o = __shfl_xor(mo, d);
+            mo = o > mo ? o : mo;
+        }
+        tend += mo;
+    }
+    if (T <= 0) tend = 0;   // empty series: no loads at all (the panel pointer may be null)
+    double mu = 0.0, m2 = 0.0, mx = -__builtin_inf(), mn = __builtin_inf();
+    // LA: 16-B loads of whole lines (8 lanes per row line): the doubles before step 0 / after
+    // step T - 1 share a line with a step of the row (mapped memory: lines never cross pages)
+    // and are never used; else element loads clamped into the row
+    constexpr int NLQ = LA ? NLD / 2 : NLD;
+    double2 pq[LA ? NLQ : 1];
+    double pre[LA ? 1 : NLD];
+    auto fetch = [&](int64_t tc) {   // no branches around the prefetch registers
+#pragma unroll
+        for (int i = 0; i < NLQ; i++) {
+            if constexpr (LA) {
+                const int row = (i * 64 + lane) / (CH / 2), cp = (i * 64 + lane) % (CH / 2);
+                const int rr = row < ns ? row : ns - 1;
+                const int o = roff(rr);
+                // a pair past the row's last line (its steps ended, or the chunk's next line)
+                // re-reads that line's last pair: never a line past the row (the panel's end
+                // may be unmapped)
+                const int64_t pl = ((T - 1 + o) | 15) - 1, pos = tc + 2 * cp;
+                pq[i] = *reinterpret_cast<const double2*>(base + rr * ld - o + (pos < pl ? pos : pl));
+            } else {
+                const int row = (i * 64 + lane) / CH, col = (i * 64 + lane) % CH;
+                const int rr = row < ns ? row : ns - 1;
+                const int64_t cc = (tc + col < T) ? tc + col : T - 1;
+                pre[i] = base[rr * ld + cc];
+            }
         }
     };
-    fetch(0);
-    for (int64_t tc = 0; tc < T; tc += CH) {
-        const int len = (T - tc < CH) ? (int)(T - tc) : CH;
+    const int myoff = live ? roff(lane) : 0;
+    auto step = [&](double v, double y, double nb) {
+        const double delta = v - mu;            // StatCounter.merge(value)
+        const double ad = __builtin_fabs(delta);
+        const double q0 = delta * y;
+        const double r = __builtin_fma(nb, q0, delta);
+        double q = __builtin_fma(r, y, q0);
+        q = (ad == 0.0) ? delta : q;            // 0 / n = 0 with the sign of delta
+        if (!(ad == 0.0 || (ad >= 0x1p-900 && ad <= 0x1p700))) q = delta / (-nb);
+        mu += q;
+        m2 += delta * (v - mu);
+        mx = jmax_sel(mx, v);
+        mn = jmin_sel(mn, v);
+    };
+    if (tend > 0) fetch(0);
+    for (int64_t tc = 0; tc < tend; tc += CH) {
 #pragma unroll
-        for (int i = 0; i < NLD; i++) {
-            const int row = (i * 64 + lane) / CH, col = (i * 64 + lane) % CH;
-            tile[row * kRow + col] = pre[i];
+        for (int i = 0; i < NLQ; i++) {
+            if constexpr (LA) {
+                const int row = (i * 64 + lane) / (CH / 2), cp = (i * 64 + lane) % (CH / 2);
+                tile[row * kRow + 2 * cp] = pq[i].x;
+                tile[row * kRow + 2 * cp + 1] = pq[i].y;
+            } else {
+                const int row = (i * 64 + lane) / CH, col = (i * 64 + lane) % CH;
+                tile[row * kRow + col] = pre[i];
+            }
         }
-        if (lane < CH) {
-            const double n = (double)(tc + lane + 1);   // exact (T < 2^53)
+        if (lane < CH + kOff) {   // entry j: step count n = tc + j - kOff + 1 (unused where n < 1)
+            const double n = (double)(tc + lane - kOff + 1);   // exact (T < 2^52)
             ytab[lane] = newton_rcp(n);
             nbtab[lane] = -n;
         }
-        if (tc + CH < T) fetch(tc + CH);
+        if (tc + CH < tend) fetch(tc + CH);
         __syncthreads();
         if (live) {
             const double* row = tile + lane * kRow;
-            for (int c = 0; c < len; c++) {
-                const double v = row[c];
-                const double y = ytab[c], nb = nbtab[c];
-                const double delta = v - mu;            // StatCounter.merge(value)
-                const double ad = __builtin_fabs(delta);
-                const double q0 = delta * y;
-                const double r = __builtin_fma(nb, q0, delta);
-                double q = __builtin_fma(r, y, q0);
-                q = (ad == 0.0) ? delta : q;            // 0 / n = 0 with the sign of delta
-                if (!(ad == 0.0 || (ad >= 0x1p-900 && ad <= 0x1p700))) q = delta / (-nb);
-                mu += q;
-                m2 += delta * (v - mu);
-                mx = jmax_sel(mx, v);
-                mn = jmin_sel(mn, v);
-            }
+            const double* yt = ytab + kOff - myoff;   // column c: step tc + c - off, entry c - off + kOff
+            const double* nt = nbtab + kOff - myoff;
+            // steps of this row in the chunk: columns [cs, ce) (all CH of them inside the series)
+            const int cs = (myoff - tc > 0) ? (int)(myoff - tc) : 0;
+            const int ce = (T - tc + myoff < CH) ? (int)(T - tc + myoff) : CH;
+            for (int c = cs; c < ce; c++) step(row[c], yt[c], nt[c]);
         }
         __syncthreads();
     }
@@ -394,7 +446,7 @@ hipError_t launch_series_stats(const double* in, double* out, int64_t S, int64_t
     if (S <= 0) return hipSuccess;
     constexpr int SPW = 64, CH = STS_STATS_CH;   // A/B on 1M x 390: 1.00 ms vs 1.44 (32 x 64), 1.96 (16 x 64)
     if (STS_STATS_FAST && T < (1LL << 52))
-        hipLaunchKernelGGL((stats_fast_kernel<SPW, CH>), dim3((unsigned)((S + SPW - 1) / SPW)), dim3(64), 0, st, in, out,
+        hipLaunchKernelGGL((stats_fast_kernel<SPW, CH, STS_STATS_LA != 0 && CH % 16 == 0>), dim3((unsigned)((S + SPW - 1) / SPW)), dim3(64), 0, st, in, out,
                            S, T, ld);
     else
         hipLaunchKernelGGL((stats_kernel<SPW, CH>), dim3((unsigned)((S + SPW - 1) / SPW)), dim3(64), 0, st, in, out, S,

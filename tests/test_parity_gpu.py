@@ -920,6 +920,39 @@ def test_series_stats_extremes(torch):
         assert_bits(host(st.stats[:, c]), ref[:, c], name)
 
 
+@pytest.mark.parametrize("T", [1, 2, 15, 16, 17, 63, 64, 65, 390])
+def test_stats_and_ewma_row_alignments(torch, T):
+    # the line-aligned chunks of stats_fast_kernel / ewma_fit_kernel (a row's chunks start on
+    # the 128-B lines of its own addresses): strided views whose rows start at every offset
+    # within a line, NaN in the padding (a staged pad step would show), and the last row ending
+    # on the allocation's last element -- bit for bit against the restatements
+    from sparkts.timeseriesrdd import TimeSeriesRDD
+    from sparkts.models import EWMA, EWMAModel
+    from sparkts.models.EWMA import gradient, sse
+    rng = np.random.default_rng(1000 + T)
+    S = 70   # three EWMA waves of 32 series (the last partial), two seriesStats waves of 64
+    for pad in [0, 1, 3, 7, 13, 16, 29]:
+        ld = T + pad
+        x = np.cumsum(rng.standard_normal((S, T)), axis=1) + 50 + rng.uniform(-5, 5, (S, 1))
+        flat = torch.full((S * ld,), NaN, dtype=torch.float64, device="cuda:0")
+        v = flat.view(S, ld)[:, pad:]
+        v.copy_(torch.as_tensor(x))
+        st = TimeSeriesRDD(None, None, v).seriesStats()
+        ref = np.array([oracle.stat_counter(r)[1:] for r in x])
+        for c, name in enumerate(["mean", "m2", "max", "min"]):
+            assert_bits(host(st.stats[:, c]), ref[:, c], "stats %s T=%d pad=%d" % (name, T, pad))
+        err = torch.zeros(S, dtype=torch.int32, device="cuda:0")
+        m = EWMA.fitModel(v, errors=err)
+        ref_s, ref_err = oracle.panel_ewma_fit(x, threads=8)
+        assert np.array_equal(host(err), ref_err)
+        assert_bits(host(m.smoothing), ref_s, "EWMA.fitModel T=%d pad=%d" % (T, pad))
+        sm = rng.uniform(0.05, 1.5, S)
+        f = host(sse(EWMAModel(dev(torch, sm)), v))
+        g = host(gradient(EWMAModel(dev(torch, sm)), v))
+        assert_bits(f, np.array([oracle.ewma_sse(r, q) for r, q in zip(x, sm)]), "sse T=%d pad=%d" % (T, pad))
+        assert_bits(g, np.array([oracle.ewma_gradient(r, q) for r, q in zip(x, sm)]), "gradient T=%d pad=%d" % (T, pad))
+
+
 def test_remove_instants_with_nans_kat(torch):
     # T/TimeSeriesRDDSuite.scala:210-231
     from sparkts.timeseriesrdd import TimeSeriesRDD
