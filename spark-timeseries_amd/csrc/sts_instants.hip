@@ -13,6 +13,7 @@
 // the compaction and the gather are plain streaming kernels; the transpose goes through a
 // padded LDS tile.
 #include "sts_internal.hpp"
+#include "sts_lanes.hpp"
 
 #include <hip/hip_runtime.h>
 
@@ -24,6 +25,9 @@
 #endif
 #ifndef STS_GATHER_BATCH
 #define STS_GATHER_BATCH 1            // instant gather: batched loads before the stores
+#endif
+#ifndef STS_TR_XCD
+#define STS_TR_XCD 1                  // transpose tiles XCD-contiguous (see transpose16_kernel)
 #endif
 #ifndef STS_NAN16
 #define STS_NAN16 1                   // 16-B NaN-instant scan when shapes allow
@@ -410,10 +414,26 @@ __global__ __launch_bounds__(256) void transpose_kernel(const double* __restrict
 // an odd pitch, so the column reads of the store phase spread over the banks.
 typedef double v2t __attribute__((ext_vector_type(2)));
 constexpr int kTrPitch = 64 + 1;
+// Tiles are XCD-contiguous (STS_TR_XCD): the instant tiles of one series block share the lines
+// that straddle their boundaries (a 64-instant row segment of a 390-step row covers 5 lines for
+// 4), so they run on one XCD and its L2 serves the shared line once; dispatched round-robin over
+// the 8 XCDs (linear id x-fastest), the neighbours sat on different L2s and the panel was read
+// 1.25 x (profiles/r05_final_to_instants_traffic.json).
+__device__ __forceinline__ void tr_tile(int64_t& t0, int64_t& s0) {
+    int64_t bx = blockIdx.x, by = blockIdx.y;
+    if (STS_TR_XCD) {
+        const int64_t nx = gridDim.x, b = xcd_remap(bx + by * nx, nx * (int64_t)gridDim.y);
+        bx = b % nx;
+        by = b / nx;
+    }
+    t0 = bx * 64;
+    s0 = by * 64;
+}
 __global__ __launch_bounds__(256) void transpose16_kernel(const double* __restrict__ in, double* __restrict__ out,
                                                           int64_t S, int64_t T, int64_t ld_in, int64_t ld_out) {
     __shared__ double tile[64 * kTrPitch];   // tile[t * pitch + s]
-    const int64_t t0 = (int64_t)blockIdx.x * 64, s0 = (int64_t)blockIdx.y * 64;
+    int64_t t0, s0;
+    tr_tile(t0, s0);
     const int p = threadIdx.x & 31, r0 = threadIdx.x >> 5;   // pair p, row r0 + 8 i
     v2t v[8];
 #pragma unroll
