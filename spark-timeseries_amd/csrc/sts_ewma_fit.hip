@@ -48,6 +48,7 @@ struct SseGrad {
         bad = x0 != x0;
     }
     __device__ __forceinline__ void run(const double* row, int c0, int len, double s, double oms) {
+#pragma unroll 8
         for (int c = c0; c < len; c++) {
             const double x = row[c];
             bad |= x != x;

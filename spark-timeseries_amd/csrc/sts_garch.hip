@@ -48,6 +48,7 @@ struct GarchEval {
         bad = x0 != x0;
     }
     __device__ __forceinline__ void run(const double* row, int c0, int len) {
+#pragma unroll 4
         for (int c = c0; c < len; c++) {
             const double eta = row[c];
             bad |= eta != eta;
