@@ -79,11 +79,16 @@ def parse():
     ap.add_argument("--series", type=int, default=0, help="override series per GPU (testing)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--percall", action="store_true",
+                    help="per-call latency of S = 1 (per-series) calls against the one-core CPU loop: the "
+                         "crossover INTEGRATION.md's JVM facade uses (prints its own JSON line, not the metric)")
     return ap.parse_args()
 
 
 def main():
     args = parse()
+    if args.percall:
+        return percall()
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -606,6 +611,119 @@ def cpu_baseline(args, S, T, K, seed, nan_p, out, acf, p_ar, smooth=None, gpar_r
                       "the reference loops, one series per thread (Spark local[%d] analogue); the JVM reference "
                       "cannot run here" % (done, T, elapsed, threads),
             "sample_check": ar_check if ar_check is not None else {"filled_bit_exact": exact, "acf_max_rel_err": worst_rel}}
+
+
+def percall():
+    """Per-call latency of the drop-in for ONE series (S = 1: UnivariateTimeSeries called from
+    a per-record closure, ARIMA's differencing inside its optimizer, lbtest's autocorr) and for
+    small partitions, against the same operation on one core (the oracle's C loop timed inside C
+    -- a lower bound on the JIT-compiled Scala loop, so the crossover it gives is conservative).
+    GPU legs: the `_host` entry point on pageable numpy memory (the JNI shim's form: arrays copied
+    into pinned buffers, staged, results copied back), on pinned memory, and the device entry
+    point on HBM-resident data (launch + stream synchronize).  Best of `reps` calls each."""
+    import ctypes
+    import numpy as np
+    import torch
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    from sparkts import _native
+    from sparkts.errors import raise_for_status
+    _native.ensure_device(0)
+    lib = _native.lib()
+    reps = 40
+
+    def best(fn, n=reps):
+        fn()
+        b = 1e300
+        for _ in range(n):
+            t0 = time.perf_counter()
+            fn()
+            b = min(b, time.perf_counter() - t0)
+        return b * 1e6   # us
+
+    def pinned(nbytes):
+        p = ctypes.c_void_p()
+        raise_for_status(lib.sts_host_alloc(max(nbytes, 16), ctypes.byref(p)), "sts_host_alloc")
+        return p
+
+    rows = []
+    for T in (10, 100, 1000, 10_000, 100_000):
+        x = oracle.gen_panel(1, 1, T, 0.05)
+        x[0, 0] = 1.0
+        x[0, -1] = 2.0
+        o = np.empty_like(x)
+        K = min(20, T - 1)
+        acf = np.empty(K)
+        nb = 8 * T
+        pin_in, pin_out = pinned(nb), pinned(nb)
+        hin = np.frombuffer((ctypes.c_char * nb).from_address(pin_in.value), dtype=np.float64)
+        hout = np.frombuffer((ctypes.c_char * nb).from_address(pin_out.value), dtype=np.float64)
+        hin[:] = x[0]
+        xd = torch.as_tensor(x, device="cuda:0")
+        od = torch.empty_like(xd)
+        ad = torch.empty(K, dtype=torch.float64, device="cuda:0")
+        sp = torch.cuda.current_stream().cuda_stream
+        row = {"T": T}
+        for method, code in (("linear", 0), ("previous", 3), ("spline", 4)):
+            row["fill_%s_host_pageable_us" % method] = best(
+                lambda: raise_for_status(lib.sts_fill_host(x.ctypes.data, o.ctypes.data, 1, T, T, code, None), "f"))
+            row["fill_%s_host_pinned_us" % method] = best(
+                lambda: raise_for_status(lib.sts_fill_host(hin.ctypes.data, hout.ctypes.data, 1, T, T, code, None),
+                                         "f"))
+
+            def dev_call():
+                raise_for_status(lib.sts_fill(xd.data_ptr(), od.data_ptr(), 1, T, T, T, code, None, sp), "f")
+                torch.cuda.synchronize()
+            row["fill_%s_device_us" % method] = best(dev_call)
+            row["fill_%s_cpu_1core_us" % method] = oracle.time_fill_ns(x[0], method, reps) / 1e3
+            assert np.array_equal(o.view(np.uint64), oracle.panel_fill(x, method)[0].view(np.uint64))
+        row["autocorr%d_host_pageable_us" % K] = best(
+            lambda: raise_for_status(lib.sts_autocorr_host(x.ctypes.data, 1, T, T, K, acf.ctypes.data), "a"))
+
+        def dev_acf():
+            raise_for_status(lib.sts_fill_autocorr(xd.data_ptr(), None, 1, T, T, T, -1, K, ad.data_ptr(), None, sp),
+                             "a")
+            torch.cuda.synchronize()
+        row["autocorr%d_device_us" % K] = best(dev_acf)
+        row["autocorr%d_cpu_1core_us" % K] = oracle.time_autocorr_ns(x[0], K, reps) / 1e3
+        lib.sts_host_free(pin_in)
+        lib.sts_host_free(pin_out)
+        rows.append({k: (round(v, 2) if isinstance(v, float) else v) for k, v in row.items()})
+
+    # partition-sized calls (the mapPartitions form): S series x 390 steps per call
+    parts = []
+    for S in (1, 16, 256, 4096, 65536):
+        T = 390
+        x = oracle.gen_panel(2, S, T, 0.05)
+        o = np.empty_like(x)
+        g = best(lambda: raise_for_status(lib.sts_fill_host(x.ctypes.data, o.ctypes.data, S, T, T, 3, None), "f"),
+                 n=10)
+        c = oracle.time_fill_ns(x[0], "previous", reps) / 1e3 * S
+        parts.append({"S": S, "T": T, "fill_previous_host_pageable_us": round(g, 2),
+                      "cpu_1core_us (S x one series)": round(c, 2)})
+    lib.sts_staging_release()
+
+    def crossover(op, gpu_key):
+        for r in rows:
+            cpu = r.get("%s_cpu_1core_us" % op)
+            if cpu is not None and r.get(gpu_key) is not None and r[gpu_key] < cpu:
+                return r["T"]
+        return None
+    K20 = "autocorr20"
+    line = {"metric": "per-call latency, one series (S = 1) and small partitions, vs one CPU core",
+            "unit": "us (best of %d calls)" % reps, "rows": rows, "partitions": parts,
+            "crossover_T": {
+                "fill_linear_host": crossover("fill_linear", "fill_linear_host_pageable_us"),
+                "fill_previous_host": crossover("fill_previous", "fill_previous_host_pageable_us"),
+                "fill_spline_host": crossover("fill_spline", "fill_spline_host_pageable_us"),
+                "autocorr20_host": crossover(K20, "autocorr20_host_pageable_us"),
+                "fill_linear_device": crossover("fill_linear", "fill_linear_device_us"),
+                "autocorr20_device": crossover(K20, "autocorr20_device_us")},
+            "note": "crossover_T = the smallest tested T at which ONE call through the GPU path beats the one-core "
+                    "C loop (the oracle, timed inside C; the JVM's Breeze loop is not faster), None = never at "
+                    "T <= 100000; the CPU leg runs on the GPU box's host",
+            "lib_sha16": lib_sha16(lib._name)}
+    print(json.dumps(line), flush=True)
 
 
 if __name__ == "__main__":

@@ -63,7 +63,10 @@ typedef enum sts_status {
     STS_ERR_SINGULAR = 8,           /* commons-math3 SingularMatrixException                 */
     STS_ERR_NO_DEVICE = 9,          /* no gfx950 device visible                              */
     STS_ERR_TOO_MANY_EVALUATIONS = 10, /* commons-math3 TooManyEvaluationsException (EWMA fit) */
-    STS_ERR_TOO_MANY_ITERATIONS = 11   /* commons-math3 TooManyIterationsException (EWMA fit)  */
+    STS_ERR_TOO_MANY_ITERATIONS = 11,  /* commons-math3 TooManyIterationsException (EWMA fit)  */
+    STS_ERR_TOO_FEW_POINTS = 12        /* commons-math3 NumberIsTooSmallException(NUMBER_OF_POINTS,
+                                          n, 3, true): fill "spline" on a series with fewer than
+                                          3 non-NaN values (SplineInterpolator.interpolate)     */
 } sts_status;
 
 /* Fill methods of UnivariateTimeSeries.fillts (S/UnivariateTimeSeries.scala:141-150). */
@@ -73,8 +76,8 @@ typedef enum sts_fill_method {
     STS_FILL_NEAREST = 1,   /* fillNearest  :156-184 */
     STS_FILL_NEXT = 2,      /* fillNext     :214-224 */
     STS_FILL_PREVIOUS = 3,  /* fillPrevious :194-204 */
-    STS_FILL_SPLINE = 4     /* fillSpline   :277-297 -- not on the device path: returns
-                               STS_ERR_UNSUPPORTED_METHOD (out of scope) */
+    STS_FILL_SPLINE = 4     /* fillSpline   :268-297 (commons-math3 3.4.1 natural cubic
+                               SplineInterpolator; sts_spline.hip, not fused) */
 } sts_fill_method;
 
 /* ---- library / runtime ---- */
@@ -96,9 +99,9 @@ int         sts_profile_begin(void);
 int         sts_profile_end(double* kernel_ms, int64_t* launches);
 
 /* ---- a1-a5: TimeSeriesRDD.fill(method) -> UnivariateTimeSeries.fillts
- *      (S/TimeSeriesRDD.scala:180-182, S/UnivariateTimeSeries.scala:141-266).
- * out must not alias in (the reference always fills a fresh copy, :157/:195/:215/:248).
- * Bit-exact. */
+ *      (S/TimeSeriesRDD.scala:180-182, S/UnivariateTimeSeries.scala:141-297).
+ * out must not alias in (the reference always fills a fresh copy, :157/:195/:215/:248/:276).
+ * Per-series errors: STS_ERR_ALL_NAN (nearest), STS_ERR_TOO_FEW_POINTS (spline).  Bit-exact. */
 int sts_fill(const double* in, double* out, int64_t S, int64_t T, int64_t ld_in, int64_t ld_out,
              int method, int32_t* err_per_series, void* stream);
 

@@ -21,8 +21,8 @@ LIB_PATH = os.path.join(HERE, "_build", "libsts_oracle.so")
 
 OK, ERR_BAD_ARG, ERR_ALL_NAN, ERR_UNSUPPORTED_METHOD = 0, 1, 2, 3
 ERR_REQUIREMENT, ERR_NOT_ENOUGH_DATA, ERR_SINGULAR = 5, 7, 8
-ERR_TOO_MANY_EVALUATIONS, ERR_TOO_MANY_ITERATIONS = 10, 11
-FILL_METHODS = {"linear": 0, "nearest": 1, "next": 2, "previous": 3}
+ERR_TOO_MANY_EVALUATIONS, ERR_TOO_MANY_ITERATIONS, ERR_TOO_FEW_POINTS = 10, 11, 12
+FILL_METHODS = {"linear": 0, "nearest": 1, "next": 2, "previous": 3, "spline": 4}
 
 _lib = None
 _dp = ctypes.POINTER(ctypes.c_double)
@@ -45,6 +45,9 @@ def lib():
             "orc_fill_next": (None, [_dp, _dp, _i64]),
             "orc_fill_nearest": (ctypes.c_int, [_dp, _dp, _i64]),
             "orc_fill_linear": (None, [_dp, _dp, _i64]),
+            "orc_fill_spline": (ctypes.c_int, [_dp, _dp, _i64]),
+            "orc_time_fill": (ctypes.c_double, [_dp, _dp, _i64, ctypes.c_int, ctypes.c_int]),
+            "orc_time_autocorr": (ctypes.c_double, [_dp, _i64, ctypes.c_int, _dp, ctypes.c_int]),
             "orc_fillts": (ctypes.c_int, [_dp, _dp, _i64, ctypes.c_int]),
             "orc_autocorr": (None, [_dp, _i64, ctypes.c_int, _dp]),
             "orc_lag_mat_trim_both": (ctypes.c_int, [_dp, _i64, ctypes.c_int, ctypes.c_int, _dp]),
@@ -129,11 +132,31 @@ def fill_linear(x):
     x = _vec(x); r = np.empty_like(x); lib().orc_fill_linear(_p(x), _p(r), x.size); return r
 
 
+def fill_spline(x):
+    """S/UnivariateTimeSeries.scala:268-297 over commons-math3 3.4.1 SplineInterpolator."""
+    x = _vec(x); r = np.empty_like(x)
+    st = lib().orc_fill_spline(_p(x), _p(r), x.size)
+    if st == ERR_TOO_FEW_POINTS:
+        raise OracleError(st, "number of points (%d)" % int(np.count_nonzero(~np.isnan(x))))
+    return r
+
+
 def fillts(x, method: str):
     if method not in FILL_METHODS:
         raise OracleError(ERR_UNSUPPORTED_METHOD, "unsupported fill method %r" % method)
     return {"linear": fill_linear, "nearest": fill_nearest, "next": fill_next,
-            "previous": fill_previous}[method](x)
+            "previous": fill_previous, "spline": fill_spline}[method](x)
+
+
+def time_fill_ns(x, method: str, reps: int = 50) -> float:
+    """Best-of-reps ns of one fillts call on one core (timed inside C)."""
+    x = _vec(x); r = np.empty_like(x)
+    return lib().orc_time_fill(_p(x), _p(r), x.size, FILL_METHODS[method], reps)
+
+
+def time_autocorr_ns(x, num_lags: int, reps: int = 50) -> float:
+    x = _vec(x); out = np.empty(max(num_lags, 1))
+    return lib().orc_time_autocorr(_p(x), x.size, num_lags, _p(out), reps)
 
 
 def autocorr(x, num_lags: int):

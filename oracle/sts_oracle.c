@@ -14,6 +14,7 @@
 #include <math.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #ifdef _OPENMP
 #include <omp.h>
@@ -87,15 +88,106 @@ void orc_fill_linear(const double* x, double* r, int64_t n) {
     }
 }
 
-/* S/UnivariateTimeSeries.scala:141-150 (fillts dispatch).  "spline" (commons-
- * math3 SplineInterpolator) is outside the north_star path and is reported as
- * unsupported here, exactly as the device library does. */
+/* commons-math3 3.4.1 PolynomialFunction(double[] c) + value(x): the constructor drops
+ * trailing zero coefficients (`while (n > 1 && c[n - 1] == 0) --n`), value() is Horner's
+ * rule `result = c[n-1]; for j = n-2..0: result = x * result + c[j]` (no FMA on the JVM).
+ * The trimming matters only for signed zeros and infinities, but it is the reference's. */
+static double cm3_poly_value(const double c[4], double x) {
+    int n = 4;
+    while (n > 1 && c[n - 1] == 0.0) --n;
+    double result = c[n - 1];
+    for (int j = n - 2; j >= 0; j--) result = x * result + c[j];
+    return result;
+}
+
+/* java.util.Arrays.binarySearch(double[], double) for the spline's knots (strictly
+ * increasing integers, never -0.0 or NaN, so the bit comparisons of the JDK's tie branch
+ * never decide anything): the index of key, else -(insertion point) - 1. */
+static int64_t java_binary_search(const double* a, int64_t len, double key) {
+    int64_t low = 0, high = len - 1;
+    while (low <= high) {
+        int64_t mid = (int64_t)(((uint64_t)low + (uint64_t)high) >> 1);
+        double midVal = a[mid];
+        if (midVal < key) low = mid + 1;
+        else if (midVal > key) high = mid - 1;
+        else return mid;
+    }
+    return -(low + 1);
+}
+
+/* S/UnivariateTimeSeries.scala:268-297 (fillSpline): the knots are the non-NaN steps
+ * (x = index as double, y = value), `new SplineInterpolator().interpolate(knotsX, knotsY)`,
+ * then result(i) = filler.value(i) for EVERY i in [knotsX(0), knotsX.last) -- valid steps
+ * included (the spline's value at a knot is y up to signed zeros / non-finite data) -- and
+ * the raw value elsewhere.  commons-math3 3.4.1 (not vendored in /root/reference; restated
+ * from its published source):
+ *   SplineInterpolator.interpolate: x.length < 3 -> NumberIsTooSmallException(NUMBER_OF_POINTS,
+ *     x.length, 3, true) (ORC_ERR_TOO_FEW_POINTS); n = x.length - 1; h[i] = x[i+1] - x[i];
+ *     mu[0] = z[0] = 0; for i = 1..n-1: g = 2(x[i+1] - x[i-1]) - h[i-1] mu[i-1];
+ *     mu[i] = h[i] / g; z[i] = (3 (y[i+1] h[i-1] - y[i] (x[i+1] - x[i-1]) + y[i-1] h[i]) /
+ *     (h[i-1] h[i]) - h[i-1] z[i-1]) / g; z[n] = c[n] = 0; for j = n-1..0: c[j] = z[j] -
+ *     mu[j] c[j+1]; b[j] = (y[j+1] - y[j]) / h[j] - h[j] (c[j+1] + 2 c[j]) / 3;
+ *     d[j] = (c[j+1] - c[j]) / (3 h[j]); polynomial j = {y[j], b[j], c[j], d[j]}.
+ *   PolynomialSplineFunction.value(v): i = binarySearch(knots, v); i < 0 -> -i - 2;
+ *     i >= n -> i - 1; polynomials[i].value(v - knots[i]).
+ * Every expression keeps Java's left-to-right evaluation order. */
+int orc_fill_spline(const double* x, double* r, int64_t len) {
+    if (r != x) memcpy(r, x, (size_t)len * sizeof(double));
+    int64_t m = 0;
+    for (int64_t i = 0; i < len; i++) m += !isnan(x[i]);
+    if (m < 3) return ORC_ERR_TOO_FEW_POINTS;
+    double* kx = (double*)malloc((size_t)m * 8 * sizeof(double));
+    if (!kx) return ORC_ERR_BAD_ARG;
+    double *ky = kx + m, *h = ky + m, *mu = h + m, *z = mu + m, *b = z + m, *c = b + m, *d = c + m;
+    int64_t k = 0;
+    for (int64_t i = 0; i < len; i++)
+        if (!isnan(x[i])) {
+            kx[k] = (double)i;
+            ky[k] = x[i];
+            k++;
+        }
+    const int64_t n = m - 1;
+    for (int64_t i = 0; i < n; i++) h[i] = kx[i + 1] - kx[i];
+    mu[0] = 0.0;
+    z[0] = 0.0;
+    double g = 0;
+    for (int64_t i = 1; i < n; i++) {
+        g = 2.0 * (kx[i + 1] - kx[i - 1]) - h[i - 1] * mu[i - 1];
+        mu[i] = h[i] / g;
+        z[i] = (3.0 * (ky[i + 1] * h[i - 1] - ky[i] * (kx[i + 1] - kx[i - 1]) + ky[i - 1] * h[i]) /
+                    (h[i - 1] * h[i]) -
+                h[i - 1] * z[i - 1]) /
+               g;
+    }
+    z[n] = 0.0;
+    c[n] = 0.0;
+    for (int64_t j = n - 1; j >= 0; j--) {
+        c[j] = z[j] - mu[j] * c[j + 1];
+        b[j] = (ky[j + 1] - ky[j]) / h[j] - h[j] * (c[j + 1] + 2.0 * c[j]) / 3.0;
+        d[j] = (c[j + 1] - c[j]) / (3.0 * h[j]);
+    }
+    /* :289-294: i from knotsX(0).toInt until knotsX.last.toInt */
+    const int64_t end = (int64_t)kx[n];
+    for (int64_t i = (int64_t)kx[0]; i < end; i++) {
+        const double v = (double)i;
+        int64_t s = java_binary_search(kx, m, v);
+        if (s < 0) s = -s - 2;
+        if (s >= n) s--;
+        const double cf[4] = {ky[s], b[s], c[s], d[s]};
+        r[i] = cm3_poly_value(cf, v - kx[s]);
+    }
+    free(kx);
+    return ORC_OK;
+}
+
+/* S/UnivariateTimeSeries.scala:141-150 (fillts dispatch) */
 int orc_fillts(const double* x, double* r, int64_t n, int method) {
     switch (method) {
     case ORC_FILL_LINEAR: orc_fill_linear(x, r, n); return ORC_OK;
     case ORC_FILL_NEAREST: return orc_fill_nearest(x, r, n);
     case ORC_FILL_NEXT: orc_fill_next(x, r, n); return ORC_OK;
     case ORC_FILL_PREVIOUS: orc_fill_previous(x, r, n); return ORC_OK;
+    case ORC_FILL_SPLINE: return orc_fill_spline(x, r, n);
     default: return ORC_ERR_UNSUPPORTED_METHOD;
     }
 }
@@ -633,24 +725,57 @@ void orc_to_instants(const double* in, int64_t S, int64_t T, int64_t ld, double*
 
 static int clamp_threads(int threads) { return threads > 0 ? threads : 1; }
 
+static double now_ns(void) {
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return (double)ts.tv_sec * 1e9 + (double)ts.tv_nsec;
+}
+
+/* bench.py --percall: one series' fillts / autocorr on one core, as the JVM's per-record
+ * closure runs it (best of reps; the C loop is a lower bound on the JIT-compiled Scala's) */
+double orc_time_fill(const double* x, double* r, int64_t n, int method, int reps) {
+    double best = 1e300;
+    for (int i = 0; i < reps; i++) {
+        const double t0 = now_ns();
+        (void)orc_fillts(x, r, n, method);
+        const double dt = now_ns() - t0;
+        if (dt < best) best = dt;
+    }
+    return best;
+}
+
+double orc_time_autocorr(const double* x, int64_t n, int K, double* out, int reps) {
+    double best = 1e300;
+    for (int i = 0; i < reps; i++) {
+        const double t0 = now_ns();
+        orc_autocorr(x, n, K, out);
+        const double dt = now_ns() - t0;
+        if (dt < best) best = dt;
+    }
+    return best;
+}
+
 int orc_panel_fill(const double* in, double* out, int64_t S, int64_t T, int64_t ld, int method,
                    int32_t* err, int threads) {
-    if (method < 0 || method > 3) return ORC_ERR_UNSUPPORTED_METHOD;
-    int any = 0;
-#pragma omp parallel for schedule(static) num_threads(clamp_threads(threads)) reduction(| : any)
+    if (method < 0 || method > 4) return ORC_ERR_UNSUPPORTED_METHOD;
+    int first = ORC_OK;
+#pragma omp parallel for schedule(static) num_threads(clamp_threads(threads))
     for (int64_t s = 0; s < S; s++) {
         int st = orc_fillts(in + s * ld, out + s * ld, T, method);
         if (err) err[s] = st;
-        any |= (st != ORC_OK);
+        if (st != ORC_OK) {
+#pragma omp atomic write
+            first = st;
+        }
     }
-    return any ? ORC_ERR_ALL_NAN : ORC_OK;
+    return first;
 }
 
 int orc_panel_fill_autocorr(const double* in, double* filled, int64_t S, int64_t T, int64_t ld,
                             int method, int K, double* acf, int32_t* err, int threads) {
-    if (method < -1 || method > 3) return ORC_ERR_UNSUPPORTED_METHOD;
+    if (method < -1 || method > 4) return ORC_ERR_UNSUPPORTED_METHOD;
     int any = 0;
-#pragma omp parallel for schedule(static) num_threads(clamp_threads(threads)) reduction(| : any)
+#pragma omp parallel for schedule(static) num_threads(clamp_threads(threads)) reduction(max : any)
     for (int64_t s = 0; s < S; s++) {
         int st = ORC_OK;
         if (method >= 0) st = orc_fillts(in + s * ld, filled + s * ld, T, method);
@@ -658,12 +783,12 @@ int orc_panel_fill_autocorr(const double* in, double* filled, int64_t S, int64_t
         if (err) err[s] = st;
         if (st != ORC_OK) {
             for (int k = 0; k < K; k++) acf[s * K + k] = NAN;
-            any = 1;
+            any = st;
         } else {
             orc_autocorr(filled + s * ld, T, K, acf + s * K);
         }
     }
-    return any ? ORC_ERR_ALL_NAN : ORC_OK;
+    return any;
 }
 
 /* C2 pipeline: fillPrevious -> differencesAtLag(1) -> EWMAModel(s).add */

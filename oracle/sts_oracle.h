@@ -33,18 +33,21 @@ extern "C" {
 #define ORC_ERR_SINGULAR 8
 #define ORC_ERR_TOO_MANY_EVALUATIONS 10
 #define ORC_ERR_TOO_MANY_ITERATIONS 11
+#define ORC_ERR_TOO_FEW_POINTS 12     /* commons-math3 NumberIsTooSmallException (spline: < 3 knots) */
 
 /* fill methods (same numbering as include/sts.h) */
 #define ORC_FILL_LINEAR 0
 #define ORC_FILL_NEAREST 1
 #define ORC_FILL_NEXT 2
 #define ORC_FILL_PREVIOUS 3
+#define ORC_FILL_SPLINE 4
 
 /* ---- single-series restatements ---- */
 void orc_fill_previous(const double* x, double* r, int64_t n);
 void orc_fill_next(const double* x, double* r, int64_t n);
 int  orc_fill_nearest(const double* x, double* r, int64_t n);   /* ORC_ERR_ALL_NAN on throw */
 void orc_fill_linear(const double* x, double* r, int64_t n);
+int  orc_fill_spline(const double* x, double* r, int64_t n);    /* ORC_ERR_TOO_FEW_POINTS on throw */
 int  orc_fillts(const double* x, double* r, int64_t n, int method);
 void orc_autocorr(const double* x, int64_t n, int K, double* out);
 int  orc_lag_mat_trim_both(const double* x, int64_t n, int max_lag, int include_original,
@@ -99,6 +102,11 @@ int orc_panel_ar_fit_remove(const double* in, double* out, int64_t S, int64_t T,
 
 int orc_panel_ewma_fit(const double* in, int64_t S, int64_t T, int64_t ld, double* smoothing,
                        int32_t* err, int threads);
+
+/* ---- per-call cost of one series (bench.py --percall: the CPU side of the S = 1 crossover),
+ * timed inside C so no FFI overhead is counted: ns per call, best of `reps` calls. ---- */
+double orc_time_fill(const double* x, double* r, int64_t n, int method, int reps);
+double orc_time_autocorr(const double* x, int64_t n, int K, double* out, int reps);
 
 /* ---- synthetic generator; bit-identical to the device generator ---- */
 void   orc_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]);

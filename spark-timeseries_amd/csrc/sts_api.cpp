@@ -129,10 +129,7 @@ struct ErrSink {
 };
 
 int method_ok(int method, bool allow_none, const char* name) {
-    if (method == STS_FILL_SPLINE)
-        return fail(STS_ERR_UNSUPPORTED_METHOD,
-                    "%s: fill method \"spline\" (commons-math3 SplineInterpolator) is not on the device path", name);
-    if (method < (allow_none ? STS_FILL_NONE : STS_FILL_LINEAR) || method > STS_FILL_PREVIOUS)
+    if (method < (allow_none ? STS_FILL_NONE : STS_FILL_LINEAR) || method > STS_FILL_SPLINE)
         return fail(STS_ERR_UNSUPPORTED_METHOD, "%s: unsupported fill method %d", name, method);
     return STS_OK;
 }
@@ -173,11 +170,36 @@ hipError_t timed(hipStream_t st, F&& launch) {
     return e;
 }
 
+// fillts "spline" (sts_spline.hip): its own kernel, not a tile-kernel method.  err (device,
+// S entries) is written for every series.
+int run_spline(const double* in, double* out, int64_t S, int64_t T, int64_t ld_in, int64_t ld_out, int32_t* err,
+               hipStream_t st) {
+    if (S == 0) return STS_OK;
+    if (T == 0) {
+        if (err) HIP_TRY(hipMemsetAsync(err, 0, (size_t)S * sizeof(int32_t), st), "hipMemsetAsync(err)");
+        return STS_OK;
+    }
+    const int64_t batch = sts::spline_batch(S, T);
+    Scratch sc(st);
+    hipError_t e = sc.alloc((size_t)batch * (size_t)T * 2 * sizeof(double));
+    if (e != hipSuccess) return hip_fail(e, "hipMallocAsync(spline scratch)");
+    e = timed(st, [&] {
+        return sts::launch_spline(in, out, S, T, ld_in, ld_out, err, static_cast<double*>(sc.p), batch, st);
+    });
+    if (e != hipSuccess) return hip_fail(e, "fill (spline)");
+    return STS_OK;
+}
+
 // fill (+ optional ACF partials / lag matrix) through the tile kernel
 // err: zeroed here unless the chosen kernel writes every entry (the seg kernel with one
 // segment per series); callers prepare their ErrSink with zero = false.
 int run_tile(const double* in, double* out, double* lagmat, int64_t S, int64_t T, int64_t ld_in, int64_t ld_out,
              int method, int K, double* acf, int max_lag, int inc, int32_t* err, hipStream_t st, const char* name) {
+    if (method == STS_FILL_SPLINE) {
+        // the spline is not fused: callers compose it (sts_fill_autocorr / _lag_matrix / _diff_ewma)
+        if (K > 0 || lagmat) return fail(STS_ERR_BAD_ARG, "%s: spline fill is not fused", name);
+        return run_spline(in, out, S, T, ld_in, ld_out, err, st);
+    }
     if (S == 0) return STS_OK;
     if (T == 0) {
         if (err) HIP_TRY(hipMemsetAsync(err, 0, (size_t)S * sizeof(int32_t), st), "hipMemsetAsync(err)");
@@ -280,6 +302,10 @@ int series_status(const int32_t* h, int64_t S, const char* what) {
     for (int64_t s = 0; s < S; s++) {
         if (h[s] == STS_ERR_ALL_NAN) return fail(STS_ERR_ALL_NAN, "Input is all NaNs! (series %lld)", (long long)s);
         if (h[s] == STS_ERR_SINGULAR) return fail(STS_ERR_SINGULAR, "singular AR design matrix (series %lld)", (long long)s);
+        if (h[s] == STS_ERR_TOO_FEW_POINTS)
+            return fail(STS_ERR_TOO_FEW_POINTS,
+                        "NumberIsTooSmallException: number of points: fewer than 3 non-NaN values for a spline (series %lld)",
+                        (long long)s);
         if (h[s] == STS_ERR_TOO_MANY_EVALUATIONS)
             return fail(STS_ERR_TOO_MANY_EVALUATIONS,
                         "TooManyEvaluationsException: illegal state: maximal count (10000) exceeded: evaluations (series %lld)",
@@ -399,6 +425,18 @@ int sts_fill_autocorr(const double* in, double* filled, int64_t S, int64_t T, in
     hipStream_t st = as_stream(stream);
     ErrSink es(err_per_series, S, st);
     if ((r = es.prepare(false))) return r;   // zeroed by run_tile, or below when it does not run
+    if (method == STS_FILL_SPLINE) {
+        // fillSpline (not fused: sts_spline.hip), then autocorr of the filled panel; the ACF
+        // pass reports into a scratch array so the spline's per-series status stands
+        if ((r = run_spline(in, filled, S, T, ld_in, ld_out, es.dev, st))) return r;
+        if (K > 0 && S > 0) {
+            Scratch e2(st);
+            HIP_TRY(e2.alloc((size_t)S * sizeof(int32_t)), "hipMallocAsync(err)");
+            if ((r = sts_fill_autocorr(filled, nullptr, S, T, ld_out, ld_out, STS_FILL_NONE, K, acf,
+                                       static_cast<int32_t*>(e2.p), st))) return r;
+        }
+        return es.finish("fill_autocorr");
+    }
     if (S > 0 && (T == 0 || (K == 0 && method == STS_FILL_NONE)))
         HIP_TRY(hipMemsetAsync(es.dev, 0, (size_t)S * sizeof(int32_t), st), "hipMemsetAsync(err)");
     if (T == 0 && S > 0 && K > 0) {
@@ -490,6 +528,20 @@ int sts_fill_lag_matrix(const double* in, double* filled, double* lagmat, int64_
     hipStream_t st = as_stream(stream);
     ErrSink es(err_per_series, S, st);
     if ((r = es.prepare(false))) return r;   // run_tile zeroes err unless its kernel writes all of it
+    if (method == STS_FILL_SPLINE) {
+        // fillSpline (sts_spline.hip) into `filled` (or a scratch panel), then the lag matrix
+        Scratch tmp(st);
+        double* F = filled;
+        int64_t ldF = ld_out;
+        if (!F && S * T > 0) {
+            HIP_TRY(tmp.alloc((size_t)(S * T) * sizeof(double)), "hipMallocAsync(filled)");
+            F = static_cast<double*>(tmp.p);
+            ldF = T;
+        }
+        if ((r = run_spline(in, F, S, T, ld_in, ldF, es.dev, st))) return r;
+        if (n > 0) HIP_TRY(sts::launch_lagmat(F, lagmat, S, T, ldF, max_lag, include_original ? 1 : 0, st), "lag");
+        return es.finish("fill_lag_matrix");
+    }
     if ((r = run_tile(in, filled, n > 0 ? lagmat : nullptr, S, T, ld_in, ld_out, method, 0, nullptr, max_lag,
                       include_original ? 1 : 0, es.dev, st, "fill_lag_matrix"))) return r;
     return es.finish("fill_lag_matrix");
@@ -1040,14 +1092,29 @@ int sts_fill_diff_ewma(const double* in, double* out, int64_t S, int64_t T, int6
         HIP_TRY(timed(st, [&] { return sts::launch_recur(sts::kFillDiffEwma, a, st); }), "fill_diff_ewma");
         return es.finish("fill_diff_ewma");
     }
-    // general composition: fill -> (in place) differences -> (in place) EWMA add, all on `out`
+    // general composition: fill (a fresh vector) -> differencesAtLag(filled, lag), which reads
+    // the FILLED values (out of place: the reference's (ts, lag) form copies, :384-386) ->
+    // EWMA add in place on `out` (dest eq ts is safe for add, S/models/EWMA.scala:135-142)
+    const double* F = in;
+    int64_t ldF = ld_in;
+    Scratch tmp(st);
     if (method != STS_FILL_NONE) {
-        if ((r = run_tile(in, out, nullptr, S, T, ld_in, ld_out, method, 0, nullptr, 0, 0, es.dev, st, "fill"))) return r;
-    } else {
-        HIP_TRY(hipMemcpy2DAsync(out, ld_out * sizeof(double), in, ld_in * sizeof(double), T * sizeof(double), S,
+        double* f = out;
+        if (lag > 0) {
+            HIP_TRY(tmp.alloc((size_t)(S * T) * sizeof(double)), "hipMallocAsync(filled)");
+            f = static_cast<double*>(tmp.p);
+        }
+        const int64_t ldf = lag > 0 ? T : ld_out;
+        if ((r = run_tile(in, f, nullptr, S, T, ld_in, ldf, method, 0, nullptr, 0, 0, es.dev, st, "fill"))) return r;
+        F = f;
+        ldF = ldf;
+    }
+    if (lag > 0) {
+        HIP_TRY(sts::launch_diff(F, out, S, T, ldF, ld_out, lag, lag, st), "differencesAtLag");
+    } else if (F != out) {
+        HIP_TRY(hipMemcpy2DAsync(out, ld_out * sizeof(double), F, ldF * sizeof(double), T * sizeof(double), S,
                                  hipMemcpyDeviceToDevice, st), "copy");
     }
-    if (lag > 0) HIP_TRY(sts::launch_diff_inplace(out, S, T, ld_out, lag, lag, st), "differencesAtLag");
     sts::RecurArgs a{};
     a.in = out; a.out = out; a.S = S; a.T = T; a.ld_in = ld_out; a.ld_out = ld_out; a.sm = smoothing;
     HIP_TRY(sts::launch_recur(sts::kEwmaAdd, a, st), "ewma_add");

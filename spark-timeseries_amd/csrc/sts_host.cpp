@@ -440,7 +440,7 @@ int sts_fill_host(const double* in, double* out, int64_t S, int64_t T, int64_t l
     if (S > 0 && T > 0 && (!in || !out)) return sts::set_error(STS_ERR_BAD_ARG, "fill: null panel pointer");
     if (in == out && S * T > 0) return sts::set_error(STS_ERR_BAD_ARG, "fill: out must not alias in (fillts returns a new vector)");
     // validate through the device entry point's own checks first (no staging on bad input)
-    if (method == STS_FILL_SPLINE || method < STS_FILL_LINEAR || method > STS_FILL_PREVIOUS)
+    if (method < STS_FILL_LINEAR || method > STS_FILL_SPLINE)
         return sts_fill(nullptr, nullptr, 0, 0, 0, 0, method, nullptr, nullptr);
     if (ld < T) return sts_fill(in, out, S, T, ld, ld, method, nullptr, nullptr);
     ErrOut eo(err, S);
@@ -476,7 +476,7 @@ int sts_fill_autocorr_host(const double* in, double* filled, int64_t S, int64_t 
         if (filled) return sts::set_error(STS_ERR_BAD_ARG, "fill_autocorr: filled must be NULL for STS_FILL_NONE");
         return sts_autocorr_host(in, S, T, ld, K, acf);
     }
-    if (method == STS_FILL_SPLINE || method < STS_FILL_LINEAR || method > STS_FILL_PREVIOUS || K < 0 || ld < T ||
+    if (method < STS_FILL_LINEAR || method > STS_FILL_SPLINE || K < 0 || ld < T ||
         (S * T > 0 && (!in || !filled || in == filled)) || (S > 0 && K > 0 && !acf))
         return sts_fill_autocorr(in, filled, S, T, ld, ld, method, K, acf, nullptr, nullptr);
     const size_t row = (size_t)(T > 0 ? T : 0) * sizeof(double), krow = (size_t)K * sizeof(double);
@@ -553,7 +553,7 @@ int sts_ewma_remove_host(const double* in, double* out, int64_t S, int64_t T, in
 
 int sts_fill_diff_ewma_host(const double* in, double* out, int64_t S, int64_t T, int64_t ld, int method, int lag,
                             const double* smoothing, int32_t* err) {
-    if (method == STS_FILL_SPLINE || method < STS_FILL_NONE || method > STS_FILL_PREVIOUS || lag < 0 || ld < T ||
+    if (method < STS_FILL_NONE || method > STS_FILL_SPLINE || lag < 0 || ld < T ||
         (S > 0 && !smoothing) || (S * T > 0 && (!in || !out || in == out)))
         return sts_fill_diff_ewma(in, out, S, T, ld, ld, method, lag, smoothing, nullptr, nullptr);
     if (S * T == 0) return STS_OK;

@@ -97,6 +97,12 @@ hipError_t launch_segment(int method, const TileArgs& a, hipStream_t st);
 bool short_ok(int method, int64_t T, int K);
 hipError_t launch_short(int method, const TileArgs& a, hipStream_t st);
 
+// fillts "spline" (sts_spline.hip): series per launch for the (mu, z) scratch rows (16 B per
+// step), and the batched launches over S series (scratch: spline_batch(S, T) x T double2)
+int64_t spline_batch(int64_t S, int64_t T);
+hipError_t launch_spline(const double* in, double* out, int64_t S, int64_t T, int64_t ld_in, int64_t ld_out,
+                         int32_t* err, double* scratch, int64_t batch, hipStream_t st);
+
 hipError_t launch_diff(const double* in, double* out, int64_t S, int64_t T, int64_t ld_in,
                        int64_t ld_out, int lag, int start, hipStream_t st);
 hipError_t launch_diff_inplace(double* x, int64_t S, int64_t T, int64_t ld, int lag, int start,

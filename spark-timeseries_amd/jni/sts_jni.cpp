@@ -44,7 +44,9 @@ Cls g_iae, g_uoe, g_npe, g_rte, g_oome;      // java.lang.*(String)
 Cls g_singular;                               // commons-math3 SingularMatrixException()
 Cls g_tme, g_tmi;                             // TooManyEvaluations / TooManyIterationsException(Number)
 Cls g_miae;                                   // MathIllegalArgumentException(Localizable, Object...)
+Cls g_too_small;                              // NumberIsTooSmallException(Localizable, Number, Number, boolean)
 jobject g_not_enough = nullptr;               // LocalizedFormats.NOT_ENOUGH_DATA_FOR_NUMBER_OF_PREDICTORS
+jobject g_number_of_points = nullptr;         // LocalizedFormats.NUMBER_OF_POINTS
 jclass g_integer = nullptr;
 jclass g_object = nullptr;
 jclass g_double_array = nullptr;              // "[D": element class of the *Records results
@@ -81,7 +83,8 @@ jobject boxed(JNIEnv* env, jint v) {
 }
 
 // Throw the reference's exception for a non-OK status.  nobs / nvars: the commons-math3
-// NOT_ENOUGH_DATA_FOR_NUMBER_OF_PREDICTORS arguments (rows, regressors) of an AR fit.
+// NOT_ENOUGH_DATA_FOR_NUMBER_OF_PREDICTORS arguments (rows, regressors) of an AR fit; for
+// STS_ERR_TOO_FEW_POINTS nobs is the failing series' point count (spline_points).
 void throw_for(JNIEnv* env, int status, jint nobs = 0, jint nvars = 0) {
     if (status == STS_OK || env->ExceptionCheck()) return;
     const char* msg = sts_last_error();
@@ -100,6 +103,14 @@ void throw_for(JNIEnv* env, int status, jint nobs = 0, jint nvars = 0) {
         const Cls& c = status == STS_ERR_TOO_MANY_EVALUATIONS ? g_tme : g_tmi;
         jobject max = boxed(env, 10000);   // MaxEval / MaxIter of the reference's optimizers
         if (c.cls && c.ctor && max) t = static_cast<jthrowable>(env->NewObject(c.cls, c.ctor, max));
+        break;
+    }
+    case STS_ERR_TOO_FEW_POINTS: {
+        // SplineInterpolator.interpolate: new NumberIsTooSmallException(NUMBER_OF_POINTS, x.length, 3, true)
+        jobject wrong = boxed(env, nobs), min = boxed(env, 3);
+        if (g_too_small.cls && g_too_small.ctor && g_number_of_points && wrong && min)
+            t = static_cast<jthrowable>(
+                env->NewObject(g_too_small.cls, g_too_small.ctor, g_number_of_points, wrong, min, (jboolean)JNI_TRUE));
         break;
     }
     case STS_ERR_NOT_ENOUGH_DATA:
@@ -155,8 +166,10 @@ thread_local PinBuf t_in, t_out;
 // The heap fallback of a call buffer, allocated without exceptions (a std::bad_alloc out of a
 // JNIEXPORT function would abort the JVM): a failure becomes a pending
 // java.lang.OutOfMemoryError and a null buffer; every native returns as soon as it sees the
-// pending exception.
+// pending exception.  With an exception already pending (an earlier buffer of the same
+// declaration failed) nothing is allocated or thrown: JNI allows no ThrowNew then.
 double* heap_buf(JNIEnv* env, std::unique_ptr<double[]>& own, size_t n) {
+    if (env->ExceptionCheck()) return nullptr;
     own.reset(n <= SIZE_MAX / sizeof(double) ? new (std::nothrow) double[n] : nullptr);
     if (!own) throw_string(env, g_oome.cls ? g_oome : g_rte, "sts_jni: cannot allocate the partition buffer");
     return own.get();
@@ -169,6 +182,7 @@ struct CallBuf {
     std::unique_ptr<double[]> own;
     double* p = nullptr;
     CallBuf(JNIEnv* env, PinBuf* b, int64_t count) : pb(b) {
+        if (env->ExceptionCheck()) return;   // an earlier buffer failed: touch nothing
         const size_t n = (size_t)(count > 0 ? count : 1);
         p = pb->get(n * sizeof(double));
         if (!p) p = heap_buf(env, own, n);
@@ -199,6 +213,7 @@ struct Region {
     // pinned: use the thread's pinned buffer `pb` (the panel); copy_in: read the array
     Region(JNIEnv* e, jdoubleArray a, int64_t count, bool copy_in, PinBuf* pb = nullptr)
         : env(e), arr(a), n((jsize)count), pb_(pb) {
+        if (env->ExceptionCheck()) return;   // an earlier buffer failed: no JNI array access now
         if (pb) p = pb->get((size_t)(count > 0 ? count : 1) * sizeof(double));
         if (!p) p = heap_buf(env, own, (size_t)(count > 0 ? count : 1));
         if (p && copy_in && count > 0) env->GetDoubleArrayRegion(arr, 0, n, p);
@@ -212,6 +227,17 @@ struct Region {
 };
 
 int64_t prod(int64_t a, int64_t b) { return (a > 0 && b > 0) ? a * b : 0; }
+
+// fill "spline" failed (STS_ERR_TOO_FEW_POINTS): the non-NaN count of the first series with
+// fewer than 3 of them, the `x.length` of the reference's NumberIsTooSmallException
+jint spline_points(const double* in, int64_t S, int64_t T) {
+    for (int64_t s = 0; s < S; s++) {
+        jint n = 0;
+        for (int64_t t = 0; t < T && n < 3; t++) n += in[s * T + t] == in[s * T + t];
+        if (n < 3) return n;
+    }
+    return 0;
+}
 
 // ---- per-record arrays: a partition's records in, one fresh array per record out ----
 
@@ -300,6 +326,8 @@ JNIEXPORT jint JNICALL JNI_OnLoad(JavaVM* vm, void*) {
     g_tmi = resolve(env, "org/apache/commons/math3/exception/TooManyIterationsException", "(Ljava/lang/Number;)V");
     g_miae = resolve(env, "org/apache/commons/math3/exception/MathIllegalArgumentException",
                      "(Lorg/apache/commons/math3/exception/util/Localizable;[Ljava/lang/Object;)V");
+    g_too_small = resolve(env, "org/apache/commons/math3/exception/NumberIsTooSmallException",
+                          "(Lorg/apache/commons/math3/exception/util/Localizable;Ljava/lang/Number;Ljava/lang/Number;Z)V");
     g_integer = global_class(env, "java/lang/Integer");
     g_object = global_class(env, "java/lang/Object");
     g_double_array = global_class(env, "[D");
@@ -313,6 +341,13 @@ JNIEXPORT jint JNICALL JNI_OnLoad(JavaVM* vm, void*) {
         if (f) {
             jobject v = env->GetStaticObjectField(lf, f);
             if (v) g_not_enough = env->NewGlobalRef(v);
+        } else {
+            env->ExceptionClear();
+        }
+        jfieldID np = env->GetStaticFieldID(lf, "NUMBER_OF_POINTS", "Lorg/apache/commons/math3/exception/util/LocalizedFormats;");
+        if (np) {
+            jobject v = env->GetStaticObjectField(lf, np);
+            if (v) g_number_of_points = env->NewGlobalRef(v);
         } else {
             env->ExceptionClear();
         }
@@ -337,7 +372,7 @@ JNIEXPORT void JNICALL Java_com_cloudera_sparkts_StsNative_fill(JNIEnv* env, jcl
     if (env->ExceptionCheck()) return;
     const int st = sts_fill_host(ri.p, ro.p, S, T, T, code, nullptr);
     if (st == STS_OK) ro.copy_out();
-    throw_for(env, st);
+    throw_for(env, st, st == STS_ERR_TOO_FEW_POINTS ? spline_points(ri.p, S, T) : 0);
 }
 
 // UnivariateTimeSeries.autocorr (S/UnivariateTimeSeries.scala:68-93); acf is S x numLags
@@ -377,7 +412,7 @@ JNIEXPORT void JNICALL Java_com_cloudera_sparkts_StsNative_fillAutocorr(JNIEnv* 
         rf.copy_out();
         ra.copy_out();
     }
-    throw_for(env, st);
+    throw_for(env, st, st == STS_ERR_TOO_FEW_POINTS ? spline_points(ri.p, S, T) : 0);
 }
 
 // UnivariateTimeSeries.differencesAtLag(ts, dest, lag, startIndex); dest may be ts (in place)
@@ -467,7 +502,7 @@ JNIEXPORT void JNICALL Java_com_cloudera_sparkts_StsNative_fillDiffEwma(JNIEnv* 
     if (env->ExceptionCheck()) return;
     const int st = sts_fill_diff_ewma_host(ri.p, ro.p, S, T, T, code, lag, rs.p, nullptr);
     if (st == STS_OK) ro.copy_out();
-    throw_for(env, st);
+    throw_for(env, st, st == STS_ERR_TOO_FEW_POINTS ? spline_points(ri.p, S, T) : 0);
 }
 
 // EWMA.fitModel over a partition panel (S/models/EWMA.scala:44-68)
@@ -605,7 +640,7 @@ JNIEXPORT jobjectArray JNICALL Java_com_cloudera_sparkts_StsNative_fillRecords(J
     double *in = bin.p, *out = bout.p;
     if (!gather_records(env, recs, S, T, in)) return nullptr;
     const int st = sts_fill_host(in, out, S, T, T, code, nullptr);
-    if (st != STS_OK) return throw_for(env, st), nullptr;
+    if (st != STS_OK) return throw_for(env, st, st == STS_ERR_TOO_FEW_POINTS ? spline_points(in, S, T) : 0), nullptr;
     return scatter_records(env, out, S, T);
 }
 
@@ -626,7 +661,7 @@ JNIEXPORT jobjectArray JNICALL Java_com_cloudera_sparkts_StsNative_fillDiffEwmaR
     Region rs(env, smoothing, S, true);
     if (env->ExceptionCheck()) return nullptr;
     const int st = sts_fill_diff_ewma_host(in, out, S, T, T, code, lag, rs.p, nullptr);
-    if (st != STS_OK) return throw_for(env, st), nullptr;
+    if (st != STS_OK) return throw_for(env, st, st == STS_ERR_TOO_FEW_POINTS ? spline_points(in, S, T) : 0), nullptr;
     return scatter_records(env, out, S, T);
 }
 

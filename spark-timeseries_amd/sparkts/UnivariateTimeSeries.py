@@ -14,7 +14,7 @@ from . import _native
 from ._panel import Panel, check, ptr
 from .errors import UnsupportedOperationException
 
-__all__ = ["fillts", "fillLinear", "fillNearest", "fillNext", "fillPrevious", "autocorr", "lag",
+__all__ = ["fillts", "fillLinear", "fillNearest", "fillNext", "fillPrevious", "fillSpline", "autocorr", "lag",
            "differencesAtLag", "ar", "fill_method_code"]
 
 
@@ -38,7 +38,8 @@ def _fill(ts, code: int):
 
 
 def fillts(ts, fillMethod: str):
-    """S/UnivariateTimeSeries.scala:141-150; "spline" is not on the device path."""
+    """S/UnivariateTimeSeries.scala:141-150: "linear" | "nearest" | "next" | "previous" |
+    "spline"; anything else raises UnsupportedOperationException."""
     return _fill(ts, fill_method_code(fillMethod))
 
 
@@ -60,6 +61,13 @@ def fillNext(values):
 def fillPrevious(values):
     """S/UnivariateTimeSeries.scala:194-204."""
     return _fill(values, 3)
+
+
+def fillSpline(values):
+    """S/UnivariateTimeSeries.scala:268-297: natural cubic spline through the non-NaN steps
+    (commons-math3 3.4.1 SplineInterpolator), evaluated at every step from the first valid one
+    up to the last; bit-exact.  Fewer than 3 non-NaN values raises NumberIsTooSmallException."""
+    return _fill(values, 4)
 
 
 def autocorr(ts, numLags: int):

@@ -18,6 +18,7 @@ STS_ERR_SINGULAR = 8
 STS_ERR_NO_DEVICE = 9
 STS_ERR_TOO_MANY_EVALUATIONS = 10
 STS_ERR_TOO_MANY_ITERATIONS = 11
+STS_ERR_TOO_FEW_POINTS = 12
 
 
 class IllegalArgumentException(ValueError):
@@ -46,6 +47,11 @@ class TooManyEvaluationsException(RuntimeError):
 
 class TooManyIterationsException(RuntimeError):
     """commons-math3 TooManyIterationsException (EWMA.fitModel: MaxIter 10000 exceeded)."""
+
+
+class NumberIsTooSmallException(ValueError):
+    """commons-math3 NumberIsTooSmallException (fillSpline: SplineInterpolator needs at least
+    3 non-NaN values, NUMBER_OF_POINTS)."""
 
 
 class DeviceError(RuntimeError):
@@ -80,4 +86,6 @@ def raise_for_status(status: int, what: str = "") -> None:
         raise TooManyEvaluationsException(msg)
     if status == STS_ERR_TOO_MANY_ITERATIONS:
         raise TooManyIterationsException(msg)
+    if status == STS_ERR_TOO_FEW_POINTS:
+        raise NumberIsTooSmallException(msg)
     raise DeviceError("%s (status %d)" % (msg, status))

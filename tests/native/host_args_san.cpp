@@ -48,8 +48,10 @@ static void run_checks(int tid) {
     expect(sts_fill_host(nullptr, out.data(), S, T, T, STS_FILL_LINEAR, nullptr), STS_ERR_BAD_ARG, "fill null in");
     expect(sts_fill_host(in.data(), in.data(), S, T, T, STS_FILL_LINEAR, nullptr), STS_ERR_BAD_ARG, "fill alias");
     expect(sts_fill_host(in.data(), out.data(), S, T, T, 99, nullptr), STS_ERR_UNSUPPORTED_METHOD, "fill method");
-    expect(sts_fill_host(in.data(), out.data(), S, T, T, STS_FILL_SPLINE, nullptr), STS_ERR_UNSUPPORTED_METHOD,
-           "fill spline");
+    expect(sts_fill_host(in.data(), out.data(), S, T, T - 1, STS_FILL_SPLINE, nullptr), STS_ERR_BAD_ARG,
+           "fill spline ld < T");
+    expect(sts_fill_host(in.data(), out.data(), S, T, T, STS_FILL_SPLINE + 1, nullptr), STS_ERR_UNSUPPORTED_METHOD,
+           "fill method past spline");
     expect(sts_fill_host(in.data(), out.data(), S, T, T - 1, STS_FILL_LINEAR, nullptr), STS_ERR_BAD_ARG, "fill ld < T");
     expect(sts_fill_host(in.data(), out.data(), -1, T, T, STS_FILL_LINEAR, nullptr), STS_ERR_BAD_ARG, "fill S < 0");
     expect(sts_autocorr_host(in.data(), S, T, T, -1, acf.data()), STS_ERR_BAD_ARG, "autocorr K < 0");

@@ -185,11 +185,10 @@ int sts_host_free(void* p) {
     return STS_OK;
 }
 int sts_fill_host(const double* in, double* out, int64_t S, int64_t T, int64_t ld, int method, int32_t* err) {
-    if (method == STS_FILL_SPLINE) return fail(STS_ERR_UNSUPPORTED_METHOD, "spline");
     for (int64_t s = 0; s < S; s++) {
-        const int r = orc_fillts(in + s * ld, out + s * ld, T, method);
-        if (err) err[s] = r ? STS_ERR_ALL_NAN : 0;
-        else if (r) return fail(STS_ERR_ALL_NAN, "Input is all NaNs!");
+        const int r = orc_fillts(in + s * ld, out + s * ld, T, method);   // ORC_* == STS_* codes
+        if (err) err[s] = r;
+        else if (r) return fail(r, r == STS_ERR_ALL_NAN ? "Input is all NaNs!" : "number of points");
     }
     return STS_OK;
 }
@@ -283,7 +282,7 @@ int main() {
     jclass cls = env->FindClass("com/cloudera/sparkts/StsNative");
 
     // ---- fillRecords: fresh, distinct arrays per record, oracle values, inputs untouched ----
-    for (const char* m : {"linear", "previous", "next", "nearest"}) {
+    for (const char* m : {"linear", "previous", "next", "nearest", "spline"}) {
         jobjectArray out = Java_com_cloudera_sparkts_StsNative_fillRecords(env, cls, recs, T, new_string(m));
         check(out && !g_pending, m);
         if (!out) continue;
@@ -307,10 +306,30 @@ int main() {
               pending_class() == "java/lang/UnsupportedOperationException",
           "unknown method -> UnsupportedOperationException");
     env->ExceptionClear();
-    check(!Java_com_cloudera_sparkts_StsNative_fillRecords(env, cls, recs, T, new_string("spline")) &&
-              pending_class() == "java/lang/UnsupportedOperationException",
-          "spline -> UnsupportedOperationException");
-    env->ExceptionClear();
+    {
+        // "spline" stays a working method (S/UnivariateTimeSeries.scala:147): fresh records, the
+        // restated commons-math3 spline's bits; a record with fewer than 3 points throws
+        // commons-math3 NumberIsTooSmallException, as SplineInterpolator.interpolate does
+        jobjectArray got = Java_com_cloudera_sparkts_StsNative_fillRecords(env, cls, recs, T, new_string("spline"));
+        check(got && !env->ExceptionCheck(), "spline -> filled records");
+        for (int64_t s = 0; got && s < S; s++) {
+            std::vector<double> want((size_t)T);
+            check(orc_fill_spline(data[s].data(), want.data(), T) == 0, "spline oracle");
+            jdoubleArray r = static_cast<jdoubleArray>(env->GetObjectArrayElement(got, (jsize)s));
+            check(same_bits(deref(r)->d.data(), want.data(), (size_t)T), "spline values");
+        }
+        env->ExceptionClear();
+        jobjectArray few = env->NewObjectArray(2, env->FindClass("[D"), nullptr);
+        std::vector<double> two((size_t)T, NAN);
+        two[1] = 1.0;
+        two[3] = 2.0;
+        env->SetObjectArrayElement(few, 0, new_doubles(data[0]));
+        env->SetObjectArrayElement(few, 1, new_doubles(two));
+        check(!Java_com_cloudera_sparkts_StsNative_fillRecords(env, cls, few, T, new_string("spline")) &&
+                  pending_class() == "org/apache/commons/math3/exception/NumberIsTooSmallException",
+              "spline on 2 points -> NumberIsTooSmallException");
+        env->ExceptionClear();
+    }
     jobjectArray ragged = env->NewObjectArray(2, env->FindClass("[D"), nullptr);
     env->SetObjectArrayElement(ragged, 0, new_doubles(data[0]));
     env->SetObjectArrayElement(ragged, 1, new_doubles(std::vector<double>(T - 1, 1.0)));

@@ -11,6 +11,8 @@
 #define JNIEXPORT __attribute__((visibility("default")))
 #define JNICALL
 #define JNI_OK 0
+#define JNI_FALSE 0
+#define JNI_TRUE 1
 #define JNI_ERR (-1)
 #define JNI_VERSION_1_6 0x00010006
 

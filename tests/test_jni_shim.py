@@ -14,7 +14,8 @@ from the oracle's primitives, and run (under ASan/UBSan): the record-level nativ
 arrays, return a FRESH double[] per record (no two records share a backing array and none
 aliases an input: each record owns its vector as in S/TimeSeriesRDD.scala:538, VERDICT r2
 "What's missing" #4), keep record order and values, and throw the reference's exception
-classes (unknown method, spline, ragged records, nearest on [5, NaN]), and turn a partition
+classes (unknown method, ragged records, nearest on [5, NaN], spline on fewer than 3 points), keep
+"spline" a working method, and turn a partition
 too large for any buffer into java.lang.OutOfMemoryError instead of aborting the JVM."""
 import os
 import re

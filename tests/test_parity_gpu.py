@@ -236,12 +236,15 @@ def test_fill_nearest_raises(torch):
 
 
 def test_fill_unsupported(torch):
+    # only an unknown method throws (:148); "spline" is a working method (tests/test_spline.py)
     from sparkts import UnivariateTimeSeries as uts
     from sparkts.errors import UnsupportedOperationException
     with pytest.raises(UnsupportedOperationException):
-        uts.fillts(dev(torch, [1.0, NaN, 2.0]), "spline")
-    with pytest.raises(UnsupportedOperationException):
         uts.fillts(dev(torch, [1.0, NaN, 2.0]), "cubic")
+    with pytest.raises(UnsupportedOperationException):
+        uts.fillts(dev(torch, [1.0, NaN, 2.0]), "Spline")
+    got = uts.fillts(dev(torch, [1.0, NaN, 2.0, 5.0]), "spline")
+    assert_bits(host(got), oracle.fill_spline([1.0, NaN, 2.0, 5.0]), "spline")
 
 
 def test_fill_padded_leading_dimension(torch):

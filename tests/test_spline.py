@@ -1,0 +1,262 @@
+"""fillts(ts, "spline") = UnivariateTimeSeries.fillSpline (S/UnivariateTimeSeries.scala:268-297).
+
+The reference dispatches "spline" (:147) to a natural cubic spline built by commons-math3 3.4.1's
+SplineInterpolator (not vendored in /root/reference: the oracle restates its published source,
+oracle/sts_oracle.c `orc_fill_spline`).  VERDICT r5 found the round-5 drop-in turning this
+working method into UnsupportedOperationException; it is now a device kernel
+(csrc/sts_spline.hip), bit-exact against the restatement.
+
+Pins of the restatement (CPU, no GPU needed):
+  * the reference's own test "signal reconstruction with spline"
+    (T/UnivariateTimeSeriesSuite.scala:85-110: on sin(i/100) downsampled by 100 and upsampled
+    again, the spline's MSE is below fillLinear's), on the reference's own input;
+  * agreement with an independent natural cubic spline (scipy CubicSpline, bc_type="natural")
+    to 1e-12 relative: the algorithm, not its roundings (those follow the Java source order);
+  * the reference's edge semantics: values before the first and from the last knot stay raw,
+    knots themselves are re-evaluated, fewer than 3 points raise NumberIsTooSmallException.
+GPU tests: device vs restatement bit for bit (device and `_host` paths, padded rows, every
+fused entry point that takes a fill method), and the per-series status.
+"""
+import numpy as np
+import pytest
+
+import oracle
+
+NaN = np.nan
+
+
+# ---------------- CPU: the restatement ----------------
+
+def _upsample(v, n):
+    out = np.full(v.size * n, NaN)
+    out[::n] = v
+    return out
+
+
+def test_reference_signal_reconstruction_with_spline():
+    # T/UnivariateTimeSeriesSuite.scala:85-110, the reference's own input and assertion
+    y = np.sin(np.arange(1, 1001, dtype=np.float64) / 100.0)
+    more = _upsample(y[::100], 100)            # downsample(vy, 100) then upsample(_, 100)
+    spline = oracle.fill_spline(more)
+    line = oracle.fill_linear(more)
+
+    def mse(est, obs):
+        m = ~np.isnan(est)
+        return float(np.sum((est[m] - obs[m]) ** 2) / m.sum())
+    assert mse(spline, y) < mse(line, y)
+    # no extrapolation: the tail after the last knot (index 900) stays NaN
+    assert np.isnan(spline[901:]).all() and not np.isnan(spline[:900]).any()
+
+
+def test_restatement_is_a_natural_cubic_spline():
+    from scipy.interpolate import CubicSpline
+    rng = np.random.default_rng(11)
+    for _ in range(150):
+        T = int(rng.integers(3, 600))
+        x = np.cumsum(rng.normal(size=T)) + rng.uniform(-1e3, 1e3)
+        x[rng.random(T) < rng.uniform(0.0, 0.8)] = NaN
+        k = np.flatnonzero(~np.isnan(x))
+        if k.size < 3:
+            continue
+        r = oracle.fill_spline(x)
+        i = np.arange(k[0], k[-1])
+        want = CubicSpline(k.astype(np.float64), x[k], bc_type="natural")(i)
+        assert np.max(np.abs(r[i] - want) / np.maximum(1.0, np.abs(want))) < 1e-12
+        # raw outside [first knot, last knot): leading NaNs, the last knot, trailing NaNs
+        assert np.array_equal(r[:k[0]], x[:k[0]], equal_nan=True)
+        assert np.array_equal(r[k[-1]:], x[k[-1]:], equal_nan=True)
+
+
+def test_restatement_edge_semantics():
+    # fewer than 3 points: SplineInterpolator.interpolate throws NumberIsTooSmallException
+    for v in ([], [1.0], [NaN, 2.0, NaN, 3.0], [NaN] * 5):
+        with pytest.raises(oracle.OracleError) as e:
+            oracle.fill_spline(np.array(v, dtype=np.float64))
+        assert e.value.code == oracle.ERR_TOO_FEW_POINTS
+    # three collinear points: the natural spline is the line (c = d = 0 after the trim)
+    r = oracle.fill_spline(np.array([NaN, 1.0, NaN, 3.0, NaN, 5.0, NaN]))
+    assert np.array_equal(r[:6], [NaN, 1.0, 2.0, 3.0, 4.0, 5.0], equal_nan=True) and np.isnan(r[6])
+    # a knot's -0.0 is re-evaluated by Horner: 0 * b + (-0.0) = +0.0 when b > 0
+    r = oracle.fill_spline(np.array([-0.0, 1.0, 4.0, 9.0]))
+    assert np.signbit(r[0]) == np.signbit(0.0 * 2.0 + -0.0)
+    assert oracle.fillts(np.array([0.0, NaN, 2.0, 3.0]), "spline")[1] == oracle.fill_spline(
+        np.array([0.0, NaN, 2.0, 3.0]))[1]
+
+
+# ---------------- GPU: the device kernel ----------------
+
+@pytest.fixture(scope="module")
+def torch():
+    import torch as _t
+    if not _t.cuda.is_available():
+        pytest.skip("no GPU")
+    from sparkts import _native
+    _native.ensure_device(0)
+    return _t
+
+
+def assert_bits(got, ref, what=""):
+    got = np.ascontiguousarray(got, dtype=np.float64)
+    ref = np.ascontiguousarray(ref, dtype=np.float64)
+    assert got.shape == ref.shape, (what, got.shape, ref.shape)
+    same = (got.view(np.uint64) == ref.view(np.uint64)) | (np.isnan(got) & np.isnan(ref))
+    if not same.all():
+        idx = np.argwhere(~same)[:5]
+        raise AssertionError("%s: %d mismatches, first %s got %s ref %s" % (
+            what, (~same).sum(), idx.tolist(), [got[tuple(i)] for i in idx], [ref[tuple(i)] for i in idx]))
+
+
+def _panel(rng, S, T, nan_p, level=100.0):
+    x = level + np.cumsum(rng.normal(size=(S, T)), axis=1)
+    x[rng.random((S, T)) < nan_p] = NaN
+    return x
+
+
+def _edge_rows(T):
+    rows = []
+    r = np.linspace(1.0, 2.0, T)
+    if T >= 6:
+        a = r.copy(); a[:T // 3] = NaN; rows.append(a)                 # leading NaNs
+        a = r.copy(); a[-T // 3:] = NaN; rows.append(a)                # trailing NaNs
+        a = r.copy(); a[1:-1] = NaN; rows.append(a)                    # 2 points: too few
+        a = np.full(T, NaN); a[[0, T // 2, T - 1]] = [1.0, -3.0, 2.0]; rows.append(a)   # exactly 3
+        a = r.copy(); a[2:T - 2] = NaN; rows.append(a)                 # one long gap
+        a = r.copy(); a[::2] = NaN; rows.append(a)                     # alternating
+        a = r * 1e6 + 0.25; a[T // 2] = NaN; rows.append(a)            # far level
+        a = r.copy(); a[0] = -0.0; a[1] = 0.0; rows.append(a)          # signed zeros on knots
+        a = r.copy(); a[T // 2] = np.inf; a[T // 2 + 1] = NaN; rows.append(a)   # a non-finite knot
+        a = np.full(T, 7.5); a[T // 3] = NaN; rows.append(a)           # constant (b = c = d = 0)
+    rows.append(np.full(T, NaN))                                       # all NaN: too few
+    return np.array(rows)
+
+
+def _ref(x):
+    S, T = x.shape
+    out, err = oracle.panel_fill(x, "spline")
+    return out, err
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("T", [1, 2, 3, 4, 5, 15, 16, 17, 33, 100, 390, 2520, 5003])
+@pytest.mark.parametrize("nan_p", [0.0, 0.05, 0.3, 0.9])
+def test_gpu_spline_bit_exact(torch, T, nan_p):
+    from sparkts import _native
+    rng = np.random.default_rng(T * 31 + int(nan_p * 100))
+    x = np.vstack([_panel(rng, 37, T, nan_p), _edge_rows(T)])
+    S = x.shape[0]
+    ref, rerr = _ref(x)
+    xd = torch.as_tensor(x, device="cuda:0")
+    out = torch.full_like(xd, 12345.0)
+    err = torch.full((S,), -1, dtype=torch.int32, device="cuda:0")
+    st = _native.lib().sts_fill(xd.data_ptr(), out.data_ptr(), S, T, T, T, 4, err.data_ptr(), None)
+    assert st == 0, _native.lib().sts_last_error()
+    torch.cuda.synchronize()
+    e = err.cpu().numpy()
+    assert np.array_equal(e, rerr), (e, rerr)
+    ok = e == 0
+    assert_bits(out.cpu().numpy()[ok], ref[ok], "spline T=%d nan=%g" % (T, nan_p))
+    # a failed series (the reference throws) keeps its raw values
+    assert_bits(out.cpu().numpy()[~ok], x[~ok], "spline failed rows")
+
+
+@pytest.mark.gpu
+def test_gpu_spline_padded_rows_and_host_path(torch):
+    from sparkts import _native
+    lib = _native.lib()
+    rng = np.random.default_rng(3)
+    S, T, ld = 50, 1001, 1005
+    x = _panel(rng, S, T, 0.2)
+    ref, rerr = _ref(x)
+    assert (rerr == 0).all()
+    xp = np.full((S, ld), -9.0)
+    xp[:, :T] = x
+    xd = torch.as_tensor(xp, device="cuda:0")
+    out = torch.full((S, ld + 3), 5.0, dtype=torch.float64, device="cuda:0")
+    assert lib.sts_fill(xd.data_ptr(), out.data_ptr(), S, T, ld, ld + 3, 4, None, None) == 0, lib.sts_last_error()
+    o = out.cpu().numpy()
+    assert_bits(o[:, :T], ref, "spline padded")
+    assert (o[:, T:] == 5.0).all(), "wrote past T"
+    # _host staging path (pinned pipeline, per-chunk scratch)
+    oh = np.empty_like(x)
+    eh = np.full(S, -1, np.int32)
+    P = lambda a: a.ctypes.data  # noqa: E731
+    assert lib.sts_fill_host(P(x), P(oh), S, T, T, 4, P(eh)) == 0, lib.sts_last_error()
+    assert_bits(oh, ref, "spline _host")
+    assert (eh == 0).all()
+
+
+@pytest.mark.gpu
+def test_gpu_spline_errors_are_the_references(torch):
+    from sparkts import UnivariateTimeSeries as uts
+    from sparkts.errors import NumberIsTooSmallException, UnsupportedOperationException
+    t = torch.as_tensor(np.array([1.0, NaN, 2.0]), device="cuda:0")
+    with pytest.raises(NumberIsTooSmallException):
+        uts.fillts(t, "spline")
+    with pytest.raises(NumberIsTooSmallException):
+        uts.fillSpline(np.array([[1.0, 2.0, 3.0, NaN], [NaN, 1.0, NaN, NaN]]))
+    with pytest.raises(UnsupportedOperationException):
+        uts.fillts(t, "cubic")
+    # a working series through the mirror, device and host
+    v = np.array([1.0, NaN, 4.0, NaN, NaN, 2.0, 8.0])
+    want = oracle.fill_spline(v)
+    assert_bits(uts.fillts(torch.as_tensor(v, device="cuda:0"), "spline").cpu().numpy(), want, "mirror device")
+    assert_bits(uts.fillSpline(v), want, "mirror host")
+
+
+@pytest.mark.gpu
+def test_gpu_spline_through_the_rdd_and_fused_entry_points(torch):
+    from sparkts import _native
+    from sparkts.timeseriesrdd import TimeSeriesRDD
+    lib = _native.lib()
+    rng = np.random.default_rng(9)
+    S, T, K = 40, 3000, 20
+    x = _panel(rng, S, T, 0.1)
+    x[3, :5] = NaN
+    ref, _ = _ref(x)
+    xd = torch.as_tensor(x, device="cuda:0")
+    # TimeSeriesRDD.fill("spline") (S/TimeSeriesRDD.scala:180-182)
+    rdd = TimeSeriesRDD(None, ["k%d" % i for i in range(S)], xd)
+    assert_bits(rdd.fill("spline").data.cpu().numpy(), ref, "rdd.fill")
+    # fill + autocorr: the filled panel, and the ACF of it within the ACF contract (1e-10)
+    filled, acf = rdd.fillAndAutocorr("spline", K)
+    assert_bits(filled.data.cpu().numpy(), ref, "fill_autocorr filled")
+    want = np.array([oracle.autocorr(r, K) for r in ref])
+    got = acf.cpu().numpy()
+    assert np.array_equal(np.isnan(got), np.isnan(want))
+    fin = ~np.isnan(want)
+    assert np.max(np.abs(got[fin] - want[fin]) / np.abs(want[fin])) <= 1e-10
+    # fill + lag matrix (filled returned, and not)
+    p = 4
+    lagm = torch.empty((S, (T - p) * p), dtype=torch.float64, device="cuda:0")
+    assert lib.sts_fill_lag_matrix(xd.data_ptr(), None, lagm.data_ptr(), S, T, T, T, 4, p, 0, None, None) == 0, \
+        lib.sts_last_error()
+    wl = np.stack([oracle.lag(r, p, False).T.ravel() for r in ref])   # column-major blocks
+    assert_bits(lagm.cpu().numpy(), wl, "fill_lag_matrix spline")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("method,lag", [("spline", 1), ("linear", 2), ("nearest", 1), ("previous", 40), ("next", 3)])
+def test_gpu_fill_diff_ewma_composition(torch, method, lag):
+    """fill -> differencesAtLag(filled, lag) (a fresh vector: the (ts, lag) form copies,
+    S/UnivariateTimeSeries.scala:384-386) -> EWMA add, for the methods and lags outside the fused
+    C2 kernel (fillPrevious, lag <= 32).  Round 5 differenced in place there, i.e. with the
+    reference's dest-eq-ts recurrence semantics: wrong for every such call."""
+    from sparkts import _native
+    lib = _native.lib()
+    rng = np.random.default_rng(lag * 7 + len(method))
+    S, T = 33, 700
+    x = _panel(rng, S, T, 0.1)
+    x[:, 0] = 100.0   # nearest: index 0 is never a source, keep every row fillable
+    sm = rng.uniform(0.05, 0.95, S)
+    want = np.empty_like(x)
+    for s in range(S):
+        f = oracle.fillts(x[s], method)
+        d = oracle.differences_at_lag(f, lag)
+        want[s] = oracle.ewma_add(d, sm[s])
+    xd = torch.as_tensor(x, device="cuda:0")
+    out = torch.empty_like(xd)
+    smd = torch.as_tensor(sm, device="cuda:0")
+    code = oracle.FILL_METHODS[method]
+    assert lib.sts_fill_diff_ewma(xd.data_ptr(), out.data_ptr(), S, T, T, T, code, lag, smd.data_ptr(), None,
+                                  None) == 0, lib.sts_last_error()
+    assert_bits(out.cpu().numpy(), want, "fill_diff_ewma %s lag %d" % (method, lag))
