@@ -151,6 +151,21 @@ def series(kind, level, sigma, T, seed):
         return level + sigma * (np.arange(T) / T * 10 + rng.uniform(-0.5, 0.5, T))
     if kind == "c4":
         return oracle.gen_ar_panel(seed, 1, T, 5)[0] * sigma + level
+    if kind.startswith("filled_"):
+        # README.md:57-61's own input: a NaN-riddled price walk after fill(method).
+        # NaN rate 5 / 20 / 60 % by seed, plus three long gaps (50-300 steps); step series for
+        # previous / next / nearest, linear ramps for linear
+        method = {"filled_prev": "previous", "filled_next": "next", "filled_near": "nearest",
+                  "filled_lin": "linear"}[kind]
+        x = level + np.cumsum(rng.standard_normal(T)) * sigma
+        x[rng.random(T) < (0.05, 0.2, 0.6)[seed % 3]] = np.nan
+        for _ in range(3):
+            g = int(rng.integers(50, 300))
+            a = int(rng.integers(1, max(2, T - g - 1)))
+            x[a:a + g] = np.nan
+        x[0] = level            # keep both ends valid: fills leave leading / trailing NaNs,
+        x[-1] = level + sigma   # and an AR fit of a NaN series is NaN
+        return oracle.fillts(x, method)
     raise ValueError(kind)
 
 
@@ -173,8 +188,18 @@ def run(case):
                 bmin=float(np.min(np.abs(ex[1:] if not no_int else ex))), **f)
 
 
-def cases(quick):
+def cases(quick, families="all"):
     out = []
+    if families == "filled":
+        for kind in ["filled_prev", "filled_next", "filled_near", "filled_lin"]:
+            for L in [0.0, 1.0, 1e1, 1e2, 1e4, 1e6]:
+                for sg in [1.0, 1e-2]:
+                    for T in ([390] if quick else [390, 2520]):
+                        for p in [1, 5, 8]:
+                            for ni in (False, True):
+                                for sd in (0, 1, 2):
+                                    out.append((kind, L, sg, T, p, ni, sd))
+        return out
     levels = [0.0, 1.0, 3.0, 1e1, 3e1, 1e2, 3e2, 1e3, 3e3, 1e4, 1e5, 1e6, 1e7]
     sigmas = [1.0, 1e-2]
     Ts = [300, 2520] if quick else [300, 2520, 6000]
@@ -198,8 +223,9 @@ if __name__ == "__main__":
     ap.add_argument("--quick", action="store_true")
     ap.add_argument("--out", default="-")
     ap.add_argument("--procs", type=int, default=7)
+    ap.add_argument("--families", default="all", choices=["all", "filled"])
     args = ap.parse_args()
-    cs = cases(args.quick)
+    cs = cases(args.quick, args.families)
     f = sys.stdout if args.out == "-" else open(args.out, "w")
     with Pool(args.procs) as pool:
         for r in pool.imap_unordered(run, cs, chunksize=2):

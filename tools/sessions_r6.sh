@@ -17,6 +17,11 @@ case "$SESSION" in
     timeout -k 10 600 python -u bench.py --percall > $O/percall.json 2> $O/percall.err || { tail -20 $O/percall.err; exit 1; }
     cat $O/percall.json
     ;;
+  arfilled)
+    # AR fit on filled series + the near-threshold rows
+    timeout -k 10 900 $PYT tests/test_ar_filled.py > $O/arfilled_pytest.log 2>&1 || { tail -40 $O/arfilled_pytest.log; exit 1; }
+    tail -2 $O/arfilled_pytest.log
+    ;;
   *)
     echo "unknown session $SESSION"; exit 2 ;;
 esac
