@@ -39,6 +39,7 @@
 
 #include <cstdint>
 
+#include "sts_dma.hpp"        // wave_lds_sync
 #include "sts_internal.hpp"   // kAcfEdge
 
 namespace sts {
@@ -260,6 +261,118 @@ __device__ __forceinline__ double acf_exact_lag(const double* F, int64_t T, int 
         v1 += d1 * d1;
         v2 += d2 * d2;
         cv += d1 * d2;
+    }
+    return cv / (__builtin_sqrt(v1) * __builtin_sqrt(v2));
+}
+
+// Rule 3's fallback on long series, streamed through LDS (round 6): acf_exact_lag's two passes
+// -- the same operations in the same order, so the same bits -- but F arrives in chunks of C
+// steps through the wave's own LDS buffers.  The whole wave loads the NEXT chunk with coalesced
+// 8-B loads (512 B per instruction) into registers before it sums the current one, so each
+// lane's dependent add chains wait on the FP64 pipe, not on HBM round trips (acf_exact_lag
+// issues its loads 8 steps ahead of each chain: ~2 x T / 8 HBM latencies, 107.7 ms for
+// 1 000 x 982 800 at K = 60).
+// Lane l computes lag i, L0 < i <= L0 + 64 (L0 = 64 b for lag block b), increasing with the lane
+// among the active lanes; !active lanes read inside the halo and add nothing.  bufa[C + 64]
+// holds the window F[L0 + j0 .. L0 + j0 + C + 64) (the lagged operand F[j + i]); for L0 > 0
+// (WIDE) bufb[C] holds F[j0 .. j0 + C) (the unlagged one), for L0 = 0 that is bufa itself.  Every
+// lane of the wave must call it (wave-uniform loop).  Sums start at +0.0 and so are never -0.0:
+// a masked step adds +0.0, the identity on them.
+template <int C, bool WIDE = false>
+__device__ double acf_exact_stream(const double* F, int64_t T, int i, bool active, double* bufa, int lane,
+                                   int L0 = 0, double* bufb = nullptr) {
+    static_assert(C % 64 == 0 && C >= 64, "chunk: whole wave rows");
+    constexpr int PL = C / 64;
+    const unsigned long long am = __ballot(active);
+    if (am == 0ull) return 0.0;
+    const int lf = __ffsll((long long)am) - 1, ll = 63 - __clzll(am);
+    const int64_t maxlen = T - __builtin_amdgcn_readlane(i, lf);   // the smallest active lag
+    const int64_t minlen = T - __builtin_amdgcn_readlane(i, ll);   // the largest
+    if (!WIDE) L0 = 0;
+    const double* FA = F + L0;
+    const int64_t TA = T - L0;                 // FA's length
+    const int ia = active ? i - L0 : 64;       // 1 .. 64
+    const int64_t len = active ? T - i : 0;
+    const double* pb = WIDE ? bufb : bufa;     // F[j0 + k] at pb[k]
+    double s1 = 0.0, s2 = 0.0, m1 = 0.0, m2 = 0.0, v1 = 0.0, v2 = 0.0, cv = 0.0;
+    for (int pass = 0; pass < 2; pass++) {
+        wave_lds_sync();   // the caller's (or the previous pass's) reads of the buffers are done
+        // bufa[0 .. C + 64) = FA[0 .. C + 64), bufb[0 .. C) = F[0 .. C) (0.0 past the end: never
+        // summed, j + i < T for j < len)
+#pragma unroll
+        for (int k = 0; k <= PL; k++) {
+            const int64_t t = (int64_t)k * 64 + lane;
+            bufa[t] = t < TA ? FA[t] : 0.0;
+            if (WIDE && k < PL) bufb[t] = t < T ? F[t] : 0.0;
+        }
+        for (int64_t j0 = 0; j0 < maxlen; j0 += C) {
+            double pf[PL], pg[WIDE ? PL : 1];
+#pragma unroll
+            for (int k = 0; k < PL; k++) {   // the next chunk's new steps, in flight meanwhile
+                const int64_t t = j0 + C + 64 + (int64_t)k * 64 + lane;
+                pf[k] = t < TA ? FA[t] : 0.0;
+                if (WIDE) {
+                    const int64_t u = j0 + C + (int64_t)k * 64 + lane;
+                    pg[k] = u < T ? F[u] : 0.0;
+                }
+            }
+            wave_lds_sync();
+            const double* pa = bufa + ia;   // F[j0 + i + k] at pa[k]
+            const bool full = j0 + C <= minlen;
+            // groups of 8 steps: 16 LDS reads, then the chains (a register double buffer of the
+            // next group's reads measured slower: its 16 moves per group cost VALU issue)
+            for (int k0 = 0; k0 < C; k0 += 8) {
+                double a[8], b[8];
+#pragma unroll
+                for (int q = 0; q < 8; q++) {
+                    a[q] = pa[k0 + q];
+                    b[q] = pb[k0 + q];
+                }
+                if (full) {
+                    if (pass == 0) {
+#pragma unroll
+                        for (int q = 0; q < 8; q++) {
+                            s1 += a[q];
+                            s2 += b[q];
+                        }
+                    } else {
+#pragma unroll
+                        for (int q = 0; q < 8; q++) {
+                            const double d1 = a[q] - m1, d2 = b[q] - m2;
+                            v1 += d1 * d1;
+                            v2 += d2 * d2;
+                            cv += d1 * d2;
+                        }
+                    }
+                } else {
+#pragma unroll
+                    for (int q = 0; q < 8; q++) {
+                        const bool in = j0 + k0 + q < len;
+                        if (pass == 0) {
+                            s1 += in ? a[q] : 0.0;
+                            s2 += in ? b[q] : 0.0;
+                        } else {
+                            const double d1 = a[q] - m1, d2 = b[q] - m2;
+                            v1 += in ? d1 * d1 : 0.0;
+                            v2 += in ? d2 * d2 : 0.0;
+                            cv += in ? d1 * d2 : 0.0;
+                        }
+                    }
+                }
+            }
+            wave_lds_sync();   // every lane's reads of this chunk are done
+            const double h = bufa[C + lane];   // the halo moves to the front ...
+            bufa[lane] = h;
+#pragma unroll
+            for (int k = 0; k < PL; k++) {     // ... the next steps behind it
+                bufa[64 + k * 64 + lane] = pf[k];
+                if (WIDE) bufb[k * 64 + lane] = pg[k];
+            }
+        }
+        if (pass == 0) {
+            m1 = s1 / (double)len;
+            m2 = s2 / (double)len;
+        }
     }
     return cv / (__builtin_sqrt(v1) * __builtin_sqrt(v2));
 }

@@ -141,7 +141,8 @@ __global__ __launch_bounds__(256) void acf_wide_finalize_kernel(const double* __
                                                                 int64_t ld, const double* __restrict__ shift, int K,
                                                                 int64_t nrange, int nblock,
                                                                 const double* __restrict__ part,
-                                                                double* __restrict__ acf) {
+                                                                double* __restrict__ acf,
+                                                                int32_t* __restrict__ exact) {
     const int64_t s = blockIdx.y;
     const int i = blockIdx.x * 256 + threadIdx.x + 1;
     if (s >= S || i > K) return;
@@ -165,8 +166,9 @@ __global__ __launch_bounds__(256) void acf_wide_finalize_kernel(const double* __
         bool sus;
         out = acf_combine_e(Pi, Sm, Qm, i, T, K, [&](int j) { return x[j] - c; },
                             [&](int j) { return x[T - 1 - j] - c; }, c, &sus);
-        // sts_acf.hpp rule 3: the wave's 64 lags take the reference's loop when any is suspect
-        if (__ballot(sus)) out = acf_exact_lag(x, T, i);
+        // sts_acf.hpp rule 3: a suspect lag flags the series; launch_acf_exact recomputes all its
+        // lags by the reference's loop
+        if (__ballot(sus) && (threadIdx.x & 63) == 0) exact[s] = 1;
     }
     acf[s * K + (i - 1)] = out;
 }
@@ -181,7 +183,7 @@ size_t acf_wide_partials(int64_t S, int64_t T, int K) {
 }
 
 hipError_t launch_acf_wide(const double* F, int64_t S, int64_t T, int64_t ld, const double* shift, int K,
-                           double* part, double* acf, hipStream_t st) {
+                           double* part, double* acf, int32_t* exact, hipStream_t st) {
     if (S <= 0 || K <= 0) return hipSuccess;
     const int64_t nrange = (T + kWideRange - 1) / kWideRange;
     const int nblock = (K + kWideLags - 1) / kWideLags;
@@ -198,15 +200,17 @@ hipError_t launch_acf_wide(const double* F, int64_t S, int64_t T, int64_t ld, co
             const int64_t n = (S - s0 < 65535) ? S - s0 : 65535;
             hipLaunchKernelGGL(acf_wide_finalize_kernel, dim3((unsigned)((K + 255) / 256), (unsigned)n), dim3(256), 0,
                                st, F + s0 * ld, n, T, ld, shift ? shift + s0 : nullptr, K, nrange, nblock,
-                               part ? part + s0 * nrange * nblock * kWideStride : nullptr, acf + s0 * K);
+                               part ? part + s0 * nrange * nblock * kWideStride : nullptr, acf + s0 * K, exact + s0);
             const hipError_t e = hipGetLastError();
             if (e != hipSuccess) return e;
         }
-        return hipSuccess;
+    } else {
+        hipLaunchKernelGGL(acf_wide_finalize_kernel, dim3((unsigned)((K + 255) / 256), (unsigned)S), dim3(256), 0, st, F,
+                           S, T, ld, shift, K, nrange, nblock, part, acf, exact);
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL(acf_wide_finalize_kernel, dim3((unsigned)((K + 255) / 256), (unsigned)S), dim3(256), 0, st, F, S,
-                       T, ld, shift, K, nrange, nblock, part, acf);
-    return hipGetLastError();
+    return launch_acf_exact(F, S, T, ld, K, exact, acf, st);
 }
 
 }  // namespace sts

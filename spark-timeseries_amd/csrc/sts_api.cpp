@@ -257,12 +257,16 @@ int run_tile(const double* in, double* out, double* lagmat, int64_t S, int64_t T
     const bool short_k = fuse && out && sts::short_ok(method, T, K) && !sts::ab_knob("STS_NO_SHORT");
     if (err && !one_seg) HIP_TRY(hipMemsetAsync(err, 0, (size_t)S * sizeof(int32_t), st), "hipMemsetAsync(err)");
     Scratch part(st);
+    int32_t* exact = nullptr;
     if (K > 0 && !fuse) {
-        // chunk partials, then (tile kernel) the per-series shifts
+        // chunk partials, then (tile kernel) the per-series shifts, then rule 3's per-series flags
         const size_t np = (size_t)(S * a.chunks_per_series) * sts::kPartStride;
-        hipError_t e = part.alloc((np + (seg ? 0 : (size_t)S)) * sizeof(double));
+        const size_t nsh = seg ? 0 : (size_t)S;
+        hipError_t e = part.alloc((np + nsh + ((size_t)S + 1) / 2) * sizeof(double));
         if (e != hipSuccess) return hip_fail(e, "hipMallocAsync(partials)");
         a.partials = static_cast<double*>(part.p);
+        exact = reinterpret_cast<int32_t*>(a.partials + np + nsh);
+        HIP_TRY(hipMemsetAsync(exact, 0, (size_t)S * sizeof(int32_t), st), "hipMemsetAsync(rule 3 flags)");
         if (!seg) {
             double* sh = a.partials + np;
             e = sts::launch_acf_shift(in, S, T, ld_in, method, sh, st);
@@ -286,8 +290,11 @@ int run_tile(const double* in, double* out, double* lagmat, int64_t S, int64_t T
         f.ldF = out ? ld_out : ld_in;
         f.parts_per_series = a.chunks_per_series;
         f.K = K;
+        f.exact = exact;
         e = sts::launch_acf_finalize(f, st);
         if (e != hipSuccess) return hip_fail(e, "acf finalize");
+        e = sts::launch_acf_exact(f.F, S, T, f.ldF, K, exact, acf, st);
+        if (e != hipSuccess) return hip_fail(e, "acf exact (rule 3)");
     }
     return STS_OK;
 }
@@ -464,11 +471,13 @@ int sts_fill_autocorr(const double* in, double* filled, int64_t S, int64_t T, in
         }
         Scratch sc(st);
         const size_t np = sts::acf_wide_partials(S, T, K);
-        hipError_t e = sc.alloc(((size_t)S + np) * sizeof(double));
+        hipError_t e = sc.alloc(((size_t)S + np + ((size_t)S + 1) / 2) * sizeof(double));
         if (e != hipSuccess) return hip_fail(e, "hipMallocAsync(acf partials)");
         double* shift = static_cast<double*>(sc.p);
+        int32_t* exact = reinterpret_cast<int32_t*>(shift + S + np);
+        HIP_TRY(hipMemsetAsync(exact, 0, (size_t)S * sizeof(int32_t), st), "hipMemsetAsync(rule 3 flags)");
         HIP_TRY(sts::launch_acf_shift(F, S, T, ldF, STS_FILL_NONE, shift, st), "acf shift");
-        HIP_TRY(timed(st, [&] { return sts::launch_acf_wide(F, S, T, ldF, shift, K, shift + S, acf, st); }),
+        HIP_TRY(timed(st, [&] { return sts::launch_acf_wide(F, S, T, ldF, shift, K, shift + S, acf, exact, st); }),
                 "autocorr (wide)");
         return es.finish("fill_autocorr");
     }

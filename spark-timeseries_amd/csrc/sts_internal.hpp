@@ -47,6 +47,8 @@ struct FinalizeArgs {
     double* acf;          // S x K
     int64_t S, T, ldF, parts_per_series;   // ACF partials per series (one per chunk)
     int K;
+    int32_t* exact;       // per series, zeroed by the caller: set where rule 3 (sts_acf.hpp) fires,
+                          // for launch_acf_exact to recompute that series by the reference's loop
 };
 
 // A/B experiment knobs (environment variables) exist only in the -DSTS_AB build
@@ -74,6 +76,10 @@ int validate(F&& f) {
 // launchers (return hipError_t of the launch)
 hipError_t launch_tile(int method, int tw, const TileArgs& a, hipStream_t st);
 hipError_t launch_acf_finalize(const FinalizeArgs& a, hipStream_t st);
+// rule 3's fallback for the series flagged in exact[S] (acf_finalize / the wide finalize): every
+// lag 1..K by the reference's two-pass loop, F streamed through LDS (sts_acf.hpp acf_exact_stream)
+hipError_t launch_acf_exact(const double* F, int64_t S, int64_t T, int64_t ldF, int K, const int32_t* exact,
+                            double* acf, hipStream_t st);
 // per-series robust ACF shift (sts_acf.hpp) for the tile kernel
 // method: the fill the series will take (STS_FILL_PREVIOUS reverses the shift's fallback)
 hipError_t launch_acf_shift(const double* in, int64_t S, int64_t T, int64_t ld, int method, double* shift,
@@ -83,7 +89,7 @@ hipError_t launch_acf_shift(const double* in, int64_t S, int64_t T, int64_t ld, 
 constexpr int kFusedMaxLags = 63;
 size_t acf_wide_partials(int64_t S, int64_t T, int K);
 hipError_t launch_acf_wide(const double* F, int64_t S, int64_t T, int64_t ld, const double* shift, int K, double* part,
-                           double* acf, hipStream_t st);
+                           double* acf, int32_t* exact, hipStream_t st);
 
 // Wave-private segment kernel (sts_seg.hip): tiles of kSegW steps, kSegTiles tiles per
 // wave.  TileArgs.tiles_per_series = ceil(T / kSegW), tiles_per_chunk = tiles per

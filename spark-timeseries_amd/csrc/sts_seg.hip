@@ -678,7 +678,10 @@ __global__ __launch_bounds__(256, 4) void seg_kernel(TileArgs a, int method) {
             if (__ballot(sus && lane < K)) {
                 __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
                 const double* F = cx.dst ? cx.dst : cx.src;
-                if (lane < K) r = acf_exact_lag(F, T, i);
+                // the ring is free now: F streams through it (sts_acf.hpp acf_exact_stream)
+                static_assert(kRing >= 512 + 64, "the exact fallback's chunk buffer");
+                const double e = acf_exact_stream<512>(F, T, i, lane < K && i < T, w.ring, lane);
+                if (lane < K) r = e;
             }
             if (lane < K) a.acf_fused[s * K + lane] = r;
         }

@@ -273,7 +273,11 @@ __global__ __launch_bounds__(64 * kShortWaves, 2) void short_fill_acf_kernel(Til
     // this wave stored (the LDS block is scratch by now): order the stores before the reads
     if (__ballot(lane < K && acf_suspect(r, sum1, sq1, sum2, sq2, v1, v2, N, c0))) {
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-        if (lane < K) r = acf_exact_lag(a.out + s * a.ld_out, T, lane + 1);
+        // F streams back through the (now free) block: the reference's loop, every sum from LDS
+        // (sts_acf.hpp acf_exact_stream; in this kernel, so the normal case pays no extra launch)
+        constexpr int CX = 64 * B - 64 < 512 ? 64 * B - 64 : 512;
+        const double e = acf_exact_stream<CX>(a.out + s * a.ld_out, T, lane + 1, lane < K, buf, lane);
+        if (lane < K) r = e;
     }
     if (lane < K) a.acf_fused[s * K + lane] = r;
 }

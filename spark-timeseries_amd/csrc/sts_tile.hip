@@ -949,10 +949,39 @@ __global__ __launch_bounds__(256) void acf_finalize_kernel(FinalizeArgs a) {
         bool sus;
         out = acf_combine(Pi, Sm, Qm, i, T, [&](int j) { return F[j] - c; },
                           [&](int j) { return F[T - 1 - j] - c; }, c, &sus);
-        // sts_acf.hpp rule 3: a series with any suspect lag takes the reference's loop (all lags)
-        if (__ballot(sus)) out = acf_exact_lag(F, T, i);
+        // sts_acf.hpp rule 3: a series with any suspect lag takes the reference's loop (all lags):
+        // flagged here, recomputed by acf_exact_kernel (F streamed through LDS)
+        if (__ballot(sus) && lane == 0) a.exact[s] = 1;
     }
     a.acf[s * K + lane] = out;
+}
+
+// Rule 3's fallback (sts_acf.hpp): one wave per (flagged series, block of 64 lags), every lag by
+// the reference's two-pass loop over F streamed through the wave's LDS chunk buffer.  Waves of
+// unflagged series exit at once (one flag load).
+// One wave per (series, 64-lag block), four per workgroup (so the four land on the CU's four
+// SIMDs: a flagged series' wave is one latency-bound chain per SIMD); waves of unflagged
+// series read their flag and end.  WIDE: the blocks past the first (numLags > 64) keep a second
+// chunk buffer for the unlagged operand.
+constexpr int kExactChunk = 512;
+template <bool WIDE>
+__global__ __launch_bounds__(256) void acf_exact_kernel(const double* __restrict__ F, int64_t S, int64_t T,
+                                                        int64_t ld, int K, int nblk, const int32_t* __restrict__ flags,
+                                                        double* __restrict__ acf) {
+    __shared__ double lds[4][kExactChunk + 64];
+    __shared__ double ldsb[4][WIDE ? kExactChunk : 1];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int nb = WIDE ? nblk - 1 : 1;
+    const int64_t u = (int64_t)blockIdx.x * 4 + wave;
+    const int64_t s = u / nb;
+    if (s >= S || !flags[s]) return;
+    const int b = WIDE ? 1 + (int)(u % nb) : 0;
+    const int i = b * 64 + lane + 1;
+    const bool active = i <= K && (int64_t)i < T;
+    const double r = WIDE ? acf_exact_stream<kExactChunk, true>(F + s * ld, T, i, active, lds[wave], lane, b * 64,
+                                                                ldsb[wave])
+                          : acf_exact_stream<kExactChunk>(F + s * ld, T, i, active, lds[wave], lane);
+    if (active) acf[s * K + (i - 1)] = r;
 }
 
 // One wave per series: the robust ACF shift (sts_acf.hpp) of every series, once per call,
@@ -1025,6 +1054,20 @@ hipError_t launch_acf_finalize(const FinalizeArgs& a, hipStream_t st) {
     if (a.S <= 0 || a.K <= 0) return hipSuccess;
     dim3 grid((unsigned)((a.S + 3) / 4)), block(256);
     hipLaunchKernelGGL(acf_finalize_kernel, grid, block, 0, st, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_acf_exact(const double* F, int64_t S, int64_t T, int64_t ldF, int K, const int32_t* exact,
+                            double* acf, hipStream_t st) {
+    if (S <= 0 || K <= 0 || T <= 0) return hipSuccess;
+    const int nblk = (K + 63) / 64;
+    if ((S * nblk + 3) / 4 > 0x7fffffffLL) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(acf_exact_kernel<false>, dim3((unsigned)((S + 3) / 4)), dim3(256), 0, st, F, S, T, ldF, K, nblk,
+                       exact, acf);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess || nblk == 1) return e;
+    hipLaunchKernelGGL(acf_exact_kernel<true>, dim3((unsigned)((S * (nblk - 1) + 3) / 4)), dim3(256), 0, st, F, S, T,
+                       ldF, K, nblk, exact, acf);
     return hipGetLastError();
 }
 

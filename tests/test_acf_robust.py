@@ -546,3 +546,35 @@ def test_gpu_autocorr_returns_tolerance_contract(torch, T, K, method):
     big = np.abs(ref) > 100.0 * floor
     assert big.mean() > 0.5
     assert rel_err(got[big], ref[big]) <= RTOL, rel_err(got[big], ref[big])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("T,K", [(300, 20), (2520, 20), (2520, 24), (5000, 60), (16384 + 77, 60), (70_001, 63),
+                                 (70_001, 1), (5000, 100), (70_001, 130), (982_800, 60)])
+def test_gpu_rule3_fallback_is_the_reference_bits(torch, T, K):
+    """Round 6: rule 3's fallback streams the series through LDS (sts_acf.hpp acf_exact_stream:
+    the short kernel's block, the segment kernel's ring, acf_exact_kernel after the tile and wide
+    finalizes).  On rows where it fires for the whole series -- non-dyadic constants with NaN
+    gaps, constant-but-one-end rows -- every lag is the reference's two-pass loop, so the result
+    must be the oracle's BITS (not merely 1e-10), across chunk boundaries (T = 70 001: 68 full
+    1 024-step chunks plus a masked tail), lag blocks (K = 100, 130: two and three 64-lag waves)
+    and every kernel the product dispatch picks."""
+    rng = np.random.default_rng(T + K)
+    rows = []
+    for c in (100.1, 1234.567, -0.3):
+        r = np.full(T, c)
+        r[rng.random(T) < 0.05] = np.nan
+        r[0] = c
+        r[-1] = c
+        rows.append(r)
+    r = np.full(T, 7.7)
+    r[-1] = 7.7 + 1e-9
+    rows.append(r)
+    x = np.array(rows)
+    filled, got = run_fill_acf(torch, x, "linear", K)
+    rf, ref, err = oracle.panel_fill_autocorr(x, "linear", K, threads=4)
+    assert (err == 0).all()
+    assert np.array_equal(filled.view(np.uint64), rf.view(np.uint64)), "fill not bit-exact"
+    same = (got.view(np.uint64) == ref.view(np.uint64)) | (np.isnan(got) & np.isnan(ref))
+    assert same.all(), "T=%d K=%d: %d lags differ from the reference's bits, first %s: %r vs %r" % (
+        T, K, (~same).sum(), np.argwhere(~same)[0], got[~same][0], ref[~same][0])

@@ -22,6 +22,22 @@ case "$SESSION" in
     timeout -k 10 900 $PYT tests/test_ar_filled.py > $O/arfilled_pytest.log 2>&1 || { tail -40 $O/arfilled_pytest.log; exit 1; }
     tail -2 $O/arfilled_pytest.log
     ;;
+  rule3)
+    # rule 3's fallback streamed through LDS: parity first, then the worst-case
+    # bench lines c1_rule3 / c3_rule3 and the normal c1 / c3 lines (the fallback must not cost them)
+    timeout -k 10 900 $PYT tests/test_acf_robust.py tests/test_acf_wide.py > $O/rule3_pytest1.log 2>&1 || { tail -40 $O/rule3_pytest1.log; exit 1; }
+    tail -2 $O/rule3_pytest1.log
+    timeout -k 10 900 $PYT tests/test_parity_gpu.py -k "acf or autocorr or rule3 or short or constant" > $O/rule3_pytest2.log 2>&1 || { tail -40 $O/rule3_pytest2.log; exit 1; }
+    tail -2 $O/rule3_pytest2.log
+    for w in c1_rule3 c3_rule3 c1; do
+      timeout -k 10 300 python -u bench.py --workload $w --steps 10 --warmup 3 --cpu-seconds 4 > $O/bench_$w.json 2> $O/bench_$w.err || { tail -20 $O/bench_$w.err; exit 1; }
+      python -c "import json,sys; d=json.load(open('$O/bench_$w.json')); r=d['roofline']; print('$w', round(d['ms_per_step'],3), r['avg_kernel_ms'], r['frac'], d['cpu_baseline']['sample_check'])"
+    done
+    ;;
+  latency)
+    # dependent-chain latency of FP64 VALU ops (the floor of the bit-exact sequential recurrences)
+    timeout -k 10 120 ./tools/ubench_latency > $O/ubench_latency.jsonl && cat $O/ubench_latency.jsonl
+    ;;
   *)
     echo "unknown session $SESSION"; exit 2 ;;
 esac
