@@ -64,6 +64,9 @@ WORKLOADS = {
     "wire_decode": (1_000_000, 390, 0.05, 10,
                     "Python wire format -> HBM panel (S/PythonConnector.scala:47-90): byte-swap decode of "
                     "1,000,000 records x 390 doubles already staged in HBM"),
+    "spline": (1_000_000, 390, 0.05, 2,
+               "fill('spline') (UnivariateTimeSeries.fillSpline, commons-math3 natural cubic spline, a1's fifth "
+               "method), 1,000,000 series x 390 steps (the C2 shape), 5 % NaN"),
     "c5": (1_250, 10_000_000, 0.30, 5,
            "C5 shard: fill('nearest') + lag(10, false), 1,250 series x 10,000,000 steps per GPU (N=8 -> C5's "
            "10k x 10M); lag matrices written into a reused scratch slab, 10 series per call"),
@@ -188,6 +191,9 @@ def main():
         elif args.workload in ("c2", "stage_c2"):
             raise_for_status(lib.sts_fill_diff_ewma(x.data_ptr(), out.data_ptr(), S, T, T, T, 3, 1, smooth.data_ptr(),
                                                     err.data_ptr(), sp), "fill_diff_ewma")
+        elif args.workload == "spline":
+            raise_for_status(lib.sts_fill(x.data_ptr(), out.data_ptr(), S, T, T, T, 4, err.data_ptr(), sp),
+                             "fill(spline)")
         elif args.workload == "c5":
             for b0 in range(0, S, LB):
                 nb = min(LB, S - b0)
@@ -254,6 +260,8 @@ def main():
               "c3_rule3": "sts::tile_kernel<4096,4,shifted> + acf_finalize_kernel with rule 3 firing on every series",
               "c1": "sts::short_fill_acf_kernel<40,20> (one wave per series in one-wave workgroups: series in by LDS-DMA, linear fill run by run in LDS, lag products as register FMAs, fused ACF finalize)",
               "c5": "sts::tile_kernel<4096,0> (fill nearest + lag-matrix columns)",
+              "spline": "sts::spline_fill_kernel (one lane per series: the natural spline's forward / backward "
+                        "sweeps in the reference's order, (mu, z) scratch rows, Horner evaluation)",
               "c2": "sts::recur_row_kernel<kFillDiffEwma,1,14,io,32> (fillPrevious -> differencesAtLag(1) -> EWMA add; whole rows through LDS, 32 lanes per series, bit-exact verified affine-scan EWMA)",
               "stage_c2": "sts::recur_row_kernel<kFillDiffEwma,1,14,io,32> (fillPrevious -> differencesAtLag(1) -> EWMA add; whole rows through LDS, 32 lanes per series)",
               "c4_levels": "sts::ar_fit_blk_kernel<5,40,4,dma> + sts::ar_qr_lane_kernel<5,true> (every series flagged: the reference's Householder-QR order, one series per lane, reflections replayed per row)",
@@ -349,7 +357,7 @@ def timed_region(step, steps, warmup, world, sync, reduce_device, on_start=None,
     return wall, elapsed
 
 
-FILL_OF = {"c3": "linear", "c1": "linear", "c1_rule3": "linear", "c3_rule3": "linear", "c2": "previous", "stage_c2": "previous", "c4": None, "c4_levels": None,
+FILL_OF = {"spline": "spline", "c3": "linear", "c1": "linear", "c1_rule3": "linear", "c3_rule3": "linear", "c2": "previous", "stage_c2": "previous", "c4": None, "c4_levels": None,
            "c5": "nearest",
            "ewma_fit": None, "garch_fit": None, "stats": None, "nan_instants": None, "to_instants": None,
            "wire_decode": None}
@@ -541,6 +549,8 @@ def cpu_baseline(args, S, T, K, seed, nan_p, out, acf, p_ar, smooth=None, gpar_r
             rf, racf, _ = oracle.panel_fill_autocorr(xs, "linear", K, threads=threads)
         elif args.workload == "c2":
             rf = oracle.panel_fill_diff_ewma(xs, 0.2, threads=threads)
+        elif args.workload == "spline":
+            rf, _ = oracle.panel_fill(xs, "spline", threads=threads)
         elif args.workload == "c5":
             xs[:, 1] = 1.0 + np.nan_to_num(xs[:, 1])
             rf, _ = oracle.panel_fill(xs, "nearest", threads=threads)

@@ -198,6 +198,9 @@ int sts_argarch_fit(const double* in, int64_t S, int64_t T, int64_t ld, double* 
  * (variance = m2 / n etc. are derived exactly as StatCounter does).  Bit-exact. */
 int sts_series_stats(const double* in, int64_t S, int64_t T, int64_t ld, double* stats,
                      void* stream);
+/* Memory access: the kernel reads whole 128-byte lines, so it may read up to 15
+ * doubles before in[0] and up to 15 after in[(S-1)*ld + T-1] -- always inside the 128-byte lines
+ * (hence the pages) that hold those two elements, never a line the panel does not touch. */
 
 /* ---- f3: TimeSeriesRDD.removeInstantsWithNaNs() (S/TimeSeriesRDD.scala:131-152) in three
  * steps, so partitions on different GPUs can combine their NaN flags in between (an

@@ -732,14 +732,27 @@ extern "C" int sts_debug_ar_stamps(unsigned long long* out16) {
 }
 #endif
 
-// scratch of the one-wave-per-series QR form (p > 8): slots of m x ldc doubles, at most
-// 2,048 slots and 1 GiB
-static int ar_qr_slots(const ArArgs& a, int64_t n) {
+// scratch of the one-wave-per-series QR form (p > 8): slots of m x ldc doubles.  The host cannot
+// see how many series the rule flags (normally none), and the wave kernel strides over its list,
+// so the slot count is bounded: one per SIMD (1 024), at most 512 MiB (up to 2 048
+// slots / 1 GiB were allocated per call before); a failed allocation retries with half the slots
+// rather than failing a fit whose QR phase may have nothing to do.
+static hipError_t alloc_qr_scratch(const ArArgs& a, int64_t n, double** scr, int* slots, hipStream_t st) {
     const size_t slot = ar_qr_wave_slot_elems(a.T, a.p, a.no_intercept) * sizeof(double);
-    int64_t k = (int64_t)((size_t(1) << 30) / (slot ? slot : 1));
-    if (k > 2048) k = 2048;
+    int64_t k = (int64_t)((size_t(512) << 20) / (slot ? slot : 1));
+    if (k > 1024) k = 1024;
     if (k > n) k = n;
-    return (int)(k < 1 ? 1 : k);
+    if (k < 1) k = 1;
+    for (;;) {
+        const hipError_t e = hipMallocAsync(reinterpret_cast<void**>(scr), (size_t)k * (slot ? slot : 8), st);
+        if (e == hipSuccess) {
+            *slots = (int)k;
+            return e;
+        }
+        (void)hipGetLastError();   // clear the failed allocation's error
+        if (k == 1) return e;
+        k /= 2;
+    }
 }
 
 static hipError_t launch_ar_fast(const ArArgs& a, hipStream_t st);
@@ -759,9 +772,7 @@ hipError_t launch_ar_fit(const ArArgs& a0, hipStream_t st) {
         double* scr = nullptr;
         int slots = 0;
         if (wave) {
-            slots = ar_qr_slots(a, a.S);
-            e = hipMallocAsync(reinterpret_cast<void**>(&scr),
-                               (size_t)slots * ar_qr_wave_slot_elems(a.T, a.p, 1) * sizeof(double), st);
+            e = alloc_qr_scratch(a, a.S, &scr, &slots, st);
             if (e != hipSuccess) return e;
         }
         e = launch_ar_qr(a, nullptr, nullptr, a.S, scr, slots, force_wave, st);
@@ -779,11 +790,7 @@ hipError_t launch_ar_fit(const ArArgs& a0, hipStream_t st) {
     if (e == hipSuccess) e = launch_ar_fast(a, st);
     double* scr = nullptr;
     int slots = 0;
-    if (e == hipSuccess && wave) {
-        slots = ar_qr_slots(a, a.S);
-        e = hipMallocAsync(reinterpret_cast<void**>(&scr),
-                           (size_t)slots * ar_qr_wave_slot_elems(a.T, a.p, 0) * sizeof(double), st);
-    }
+    if (e == hipSuccess && wave) e = alloc_qr_scratch(a, a.S, &scr, &slots, st);
     if (e == hipSuccess) e = launch_ar_qr(a, a.qr_list, a.qr_count, 0, scr, slots, force_wave, st);
     if (scr) (void)hipFreeAsync(scr, st);
     (void)hipFreeAsync(buf, st);

@@ -29,6 +29,8 @@
 
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 namespace sts {
 namespace {
 
@@ -156,10 +158,77 @@ __global__ __launch_bounds__(64) void ewma_fit_kernel(EwmaFitArgs a) {
 constexpr int kFitSpw = 32;
 constexpr int kFitCh = 64;
 
+#ifdef STS_AB
+// A/B: the wave's SPW rows held in LDS for the whole fit (one load, every
+// optimizer request served from LDS) instead of re-streamed per request.  LDS = SPW x (T + 1)
+// doubles per wave (T = 390: 50 KB for 16 rows, 100 KB for 32), so 3 / 1 waves per CU.
+template <int SPW>
+__global__ __launch_bounds__(64) void ewma_fit_res_kernel(EwmaFitArgs a) {
+    extern __shared__ double rows[];
+    const int lane = threadIdx.x;
+    const int64_t s0 = (int64_t)blockIdx.x * SPW;
+    const int64_t sl = s0 + lane;
+    const bool live = lane < SPW && sl < a.S;
+    const int ns = (a.S - s0 < SPW) ? (int)(a.S - s0) : SPW;
+    const int T = (int)a.T;
+    const int kRow = T + 1;
+    const double* base = a.in + s0 * a.ld;
+    for (int r = 0; r < ns; r++)   // each load instruction: 64 consecutive steps of one row
+        for (int t = lane; t < T; t += 64) rows[r * kRow + t] = base[r * a.ld + t];
+    __syncthreads();
+    EwmaOpt o;
+    o.pc = 0;
+    o.status = -1;
+    o.iter = 0;
+    o.evals = 0;
+    o.have_cur = 0;
+    o.cn = 0;
+    o.res_f = o.res_g = 0.0;
+    if (live) ewma_advance(o);
+    const double* myrow = rows + (live ? lane : 0) * kRow;
+    bool first = true;
+    for (;;) {
+        const bool pending = live && o.status < 0;
+        if (__ballot(pending) == 0) break;
+        if (pending) {
+            const double s = o.req, oms = 1.0 - s;
+            SseGrad g;
+            g.start(myrow[0]);
+            g.run(myrow, 1, T, s, oms);
+            o.res_f = g.sq;
+            o.res_g = 2 * g.dJ;
+            if (first && g.bad && T >= 2) {
+                o.status = STS_ERR_TOO_MANY_EVALUATIONS;
+            } else {
+                cache_insert(o);
+                ewma_advance(o);
+            }
+        }
+        first = false;
+    }
+    if (!live) return;
+    a.smoothing[sl] = (o.status == STS_OK) ? o.point : __builtin_nan("");
+    if (a.err) a.err[sl] = o.status;
+    if (a.evals) a.evals[sl] = o.evals;
+}
+#endif
+
 }  // namespace
 
 hipError_t launch_ewma_fit(const EwmaFitArgs& a, bool fit, hipStream_t st) {
     if (a.S <= 0) return hipSuccess;
+#ifdef STS_AB
+    if (const char* k = ab_knob("STS_EWMA_RES")) {   // 16 | 32 rows per wave held in LDS
+        const int spw = std::atoi(k) == 32 ? 32 : 16;
+        const size_t lds = (size_t)spw * (size_t)(a.T + 1) * sizeof(double);
+        if (fit && a.T >= 1 && lds <= 160 * 1024) {
+            dim3 g((unsigned)((a.S + spw - 1) / spw)), b(64);
+            if (spw == 32) hipLaunchKernelGGL(ewma_fit_res_kernel<32>, g, b, lds, st, a);
+            else hipLaunchKernelGGL(ewma_fit_res_kernel<16>, g, b, lds, st, a);
+            return hipGetLastError();
+        }
+    }
+#endif
     dim3 grid((unsigned)((a.S + kFitSpw - 1) / kFitSpw)), block(64);
     if (fit) hipLaunchKernelGGL((ewma_fit_kernel<kFitSpw, kFitCh, true>), grid, block, 0, st, a);
     else hipLaunchKernelGGL((ewma_fit_kernel<kFitSpw, kFitCh, false>), grid, block, 0, st, a);

@@ -38,6 +38,23 @@ case "$SESSION" in
     # dependent-chain latency of FP64 VALU ops (the floor of the bit-exact sequential recurrences)
     timeout -k 10 120 ./tools/ubench_latency > $O/ubench_latency.jsonl && cat $O/ubench_latency.jsonl
     ;;
+  ewmares)
+    # EWMA.fitModel: series block re-streamed per optimizer request (product) against the block held
+    # in LDS (A/B build, STS_EWMA_RES=16 | 32 rows per wave); same box, alternating, with the
+    # bench's sample check (smoothing bit-identical to the commons-math3 restatement)
+    AB=spark-timeseries_amd/build/libsts_hip_ab.so
+    for rep in 1 2; do
+      for V in base res16 res32; do
+        case $V in
+          base) E="" ;;
+          res16) E="STS_HIP_LIB=$AB STS_EWMA_RES=16" ;;
+          res32) E="STS_HIP_LIB=$AB STS_EWMA_RES=32" ;;
+        esac
+        env $E timeout -k 10 300 python -u bench.py --workload ewma_fit --steps 3 --warmup 1 --cpu-seconds 2 > $O/ewmares_$V.json 2> $O/ewmares_$V.err || { tail -20 $O/ewmares_$V.err; exit 1; }
+        python -c "import json; d=json.load(open('$O/ewmares_$V.json')); r=d['roofline']; print(json.dumps({'variant': '$V', 'rep': $rep, 'kernel_ms': r['avg_kernel_ms'], 'ms_per_step': d['ms_per_step'], 'check': d['cpu_baseline']['sample_check']}))" | tee -a $O/ewmares.jsonl
+      done
+    done
+    ;;
   *)
     echo "unknown session $SESSION"; exit 2 ;;
 esac
