@@ -95,9 +95,44 @@ int check_panel(const void* in, int64_t S, int64_t T, int64_t ld, const char* na
     return STS_OK;
 }
 
+// The calling thread's host-mapped status array for calls without a caller err array (round 6):
+// the kernels write it over PCIe and the call reads it after its stream synchronize, instead of a
+// stream-ordered allocation + memset + D2H copy (a one-series fill: 35 -> ~15 us,
+// tools/percall_parts.py).  Grown on demand up to kMappedErrMax entries, freed with the thread.
+constexpr int64_t kMappedErrMax = 1 << 16;
+struct MappedErr {
+    int32_t* host = nullptr;
+    int32_t* dev = nullptr;
+    int64_t cap = 0;
+    int32_t* get(int64_t n, int32_t** devp) {
+        if (n > cap) {
+            if (host) (void)hipHostFree(host);
+            host = dev = nullptr;
+            cap = 0;
+            void* p = nullptr;
+            if (hipHostMalloc(&p, (size_t)n * sizeof(int32_t), hipHostMallocMapped) != hipSuccess) return nullptr;
+            void* d = nullptr;
+            if (hipHostGetDevicePointer(&d, p, 0) != hipSuccess) {
+                (void)hipHostFree(p);
+                return nullptr;
+            }
+            host = static_cast<int32_t*>(p);
+            dev = static_cast<int32_t*>(d);
+            cap = n;
+        }
+        *devp = dev;
+        return host;
+    }
+    ~MappedErr() {
+        if (host) (void)hipHostFree(host);
+    }
+};
+thread_local MappedErr t_mapped_err;
+
 // err handling: caller array (async) or internal buffer checked synchronously
 struct ErrSink {
     int32_t* dev = nullptr;
+    int32_t* mapped = nullptr;   // host view of dev when dev is the thread's mapped array
     bool owned = false;
     Scratch scratch;
     int64_t S;
@@ -106,10 +141,15 @@ struct ErrSink {
     // itself (run_tile)
     int prepare(bool zero = true) {
         if (!dev) {
+            owned = true;
+            if (S > 0 && S <= kMappedErrMax) mapped = t_mapped_err.get(S, &dev);
+            if (mapped) {
+                std::memset(mapped, 0, (size_t)S * sizeof(int32_t));   // before any launch of this call
+                return STS_OK;
+            }
             hipError_t e = scratch.alloc((size_t)(S > 0 ? S : 1) * sizeof(int32_t));
             if (e != hipSuccess) return hip_fail(e, "hipMallocAsync(err)");
             dev = static_cast<int32_t*>(scratch.p);
-            owned = true;
         }
         if (S > 0 && zero) {
             hipError_t e = hipMemsetAsync(dev, 0, (size_t)S * sizeof(int32_t), scratch.st);
@@ -117,9 +157,21 @@ struct ErrSink {
         }
         return STS_OK;
     }
+    // a call that returns early (a failed launch) may still have kernels in flight that write
+    // the thread's mapped array: wait for them before the next call on this thread reuses it
+    ~ErrSink() {
+        if (mapped && !finished) (void)hipStreamSynchronize(scratch.st);
+    }
+    bool finished = false;
     // for the internal buffer: wait and turn the first failing series into a status
     int finish(const char* what) {
+        finished = true;
         if (!owned || S == 0) return STS_OK;
+        if (mapped) {
+            const hipError_t e = hipStreamSynchronize(scratch.st);
+            if (e != hipSuccess) return hip_fail(e, what);
+            return sts::series_status(mapped, S, what);
+        }
         std::vector<int32_t> h((size_t)S);
         hipError_t e = hipMemcpyAsync(h.data(), dev, (size_t)S * sizeof(int32_t), hipMemcpyDeviceToHost, scratch.st);
         if (e == hipSuccess) e = hipStreamSynchronize(scratch.st);

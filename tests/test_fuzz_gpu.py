@@ -302,3 +302,38 @@ def test_fuzz_host_entry_points(torch, case):
         r = oracle.ewma_add(oracle.differences_at_lag(oracle.fill_previous(x[s, :T]), 1), float(sm[s]))
         g = o2[s, :T]
         assert ((g.view(np.uint64) == r.view(np.uint64)) | (np.isnan(g) & np.isnan(r))).all(), (case, s, "c2_host")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", range(24 * SCALE))
+def test_fuzz_fill_spline(torch, case):
+    """fill("spline") (S/UnivariateTimeSeries.scala:268-297, round 6): random shapes, NaN rates with
+    long runs, levels and families -- the filled panel bit for bit against the commons-math3
+    restatement, the per-series status (NumberIsTooSmallException on < 3 points) identical, and
+    every other case through fill + autocorr (the ACF within the tolerance contract)."""
+    from sparkts import TimeSeriesRDD, _native
+    rng = np.random.default_rng(zlib.crc32(b"fuzz-spline-%d" % case))
+    T = int(np.exp(rng.uniform(np.log(2), np.log(40000))))
+    S = int(rng.integers(1, 12))
+    family = ["walk", "noise", "ar1", "steps"][int(rng.integers(0, 4))]
+    level = float(rng.choice([0.0, 100.0, 1e4, 1e6]))
+    x = fuzz_panel(rng, S, T, family, level, float(rng.choice([0.0, 0.02, 0.1, 0.4, 0.95])),
+                   bool(rng.integers(0, 2)))
+    rf, rerr = oracle.panel_fill(x, "spline")
+    xd = torch.as_tensor(x, device="cuda:0")
+    out = torch.empty_like(xd)
+    err = torch.full((S,), -1, dtype=torch.int32, device="cuda:0")
+    assert _native.lib().sts_fill(xd.data_ptr(), out.data_ptr(), S, T, T, T, 4, err.data_ptr(), None) == 0
+    torch.cuda.synchronize()
+    assert np.array_equal(err.cpu().numpy(), rerr), (case, err.cpu().numpy(), rerr)
+    f = out.cpu().numpy()
+    same = (f.view(np.uint64) == rf.view(np.uint64)) | (np.isnan(f) & np.isnan(rf))
+    assert same.all(), (case, T, family, int((~same).sum()))
+    if case % 2 == 0 and (rerr == 0).all() and T > 2:
+        K = int(rng.integers(1, max(2, min(61, T))))
+        filled, acf = TimeSeriesRDD(None, None, xd).fillAndAutocorr("spline", K)
+        rf2, racf, err2 = oracle.panel_fill_autocorr(x, "spline", K)
+        assert (err2 == 0).all()
+        got = acf.cpu().numpy()
+        for s in range(S):
+            assert within(got[s], racf[s], noise_floor(rf2[s], K)) <= 1.0, (case, s, T, K)
