@@ -657,7 +657,7 @@ def percall():
         return p
 
     rows = []
-    for T in (10, 100, 1000, 10_000, 100_000):
+    for T in (10, 100, 1000, 3000, 10_000, 30_000, 100_000):
         x = oracle.gen_panel(1, 1, T, 0.05)
         x[0, 0] = 1.0
         x[0, -1] = 2.0

@@ -110,7 +110,8 @@ struct MappedErr {
             host = dev = nullptr;
             cap = 0;
             void* p = nullptr;
-            if (hipHostMalloc(&p, (size_t)n * sizeof(int32_t), hipHostMallocMapped) != hipSuccess) return nullptr;
+            if (hipHostMalloc(&p, (size_t)n * sizeof(int32_t), hipHostMallocMapped | hipHostMallocPortable) != hipSuccess)
+                return nullptr;
             void* d = nullptr;
             if (hipHostGetDevicePointer(&d, p, 0) != hipSuccess) {
                 (void)hipHostFree(p);

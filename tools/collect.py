@@ -45,7 +45,8 @@ TRAFFIC_KERNELS = {"c3": "tile_kernel", "c1": "short_fill_acf_kernel", "c2": "re
                    # nan_instants16_kernel and gather_instants_kernel), per launch like bench.py's figure
                    "ewma_fit": "ewma_fit_kernel", "stats": "stats_fast_kernel", "nan_instants": "_instants",
                    "to_instants": "transpose16_kernel", "wire_decode": "wire_decode_rows_kernel",
-                   "garch_fit": "garch_fit_kernel", "stage_c2": "recur_row_kernel"}
+                   "garch_fit": "garch_fit_kernel", "stage_c2": "recur_row_kernel",
+                   "spline": "spline_fill_kernel"}
 
 
 def collect_fp64(tag, wl):
@@ -110,6 +111,12 @@ def main():
             print(json.dumps(rec))
     for wl in FP64_KERNELS:
         collect_fp64(tag, wl)
+    pc = os.path.join(OUT, "percall.log")   # bench.py --percall (tools/r5_session.sh percall)
+    if os.path.exists(pc):
+        lines = [ln for ln in open(pc) if ln.startswith("{")]
+        if lines:
+            with open(os.path.join(PROF, "%s_percall.json" % tag), "w") as f:
+                f.write(lines[-1])
 
 
 if __name__ == "__main__":

@@ -29,7 +29,8 @@ for s in ${STEPS:-artests}; do
     tests) step tests 1100 $PYT -m gpu tests ;;
     pytest) step pytest_sel ${TEST_SECS:-900} $PYT -m gpu $TEST_FILES ;;
     smoke) step smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()" ;;
-    c1|c2|c3|c4|c5|c4_levels|c1_rule3|c3_rule3|ewma_fit|garch_fit|stats|nan_instants|to_instants|wire_decode|stage_c2) step bench_$s 300 python -u bench.py --workload $s ;;
+    c1|c2|c3|c4|c5|c4_levels|c1_rule3|c3_rule3|ewma_fit|garch_fit|stats|nan_instants|to_instants|wire_decode|stage_c2|spline) step bench_$s 300 python -u bench.py --workload $s ;;
+    percall) step percall 300 python -u bench.py --percall ;;
     prof_*) W=${s#prof_}; step prof_$W 400 rocprofv3 --kernel-trace --stats -d $O/prof_$W -o run --output-format csv -- python -u bench.py --workload $W --no-cpu-baseline ;;
     fetch_*) W=${s#fetch_}; step pmc_fetch_$W 300 rocprofv3 --pmc FETCH_SIZE -d $O/pmc_fetch_$W -o run --output-format csv -- python -u bench.py --workload $W --steps 2 --warmup 0 --no-cpu-baseline ;;
     write_*) W=${s#write_}; step pmc_write_$W 300 rocprofv3 --pmc WRITE_SIZE -d $O/pmc_write_$W -o run --output-format csv -- python -u bench.py --workload $W --steps 2 --warmup 0 --no-cpu-baseline ;;
