@@ -260,3 +260,25 @@ def test_gpu_fill_diff_ewma_composition(torch, method, lag):
     assert lib.sts_fill_diff_ewma(xd.data_ptr(), out.data_ptr(), S, T, T, T, code, lag, smd.data_ptr(), None,
                                   None) == 0, lib.sts_last_error()
     assert_bits(out.cpu().numpy(), want, "fill_diff_ewma %s lag %d" % (method, lag))
+
+
+@pytest.mark.gpu
+def test_gpu_spline_long_series_across_launch_batches(torch):
+    """C3-scale lengths: T = 1 000 000 with 5 % NaN and gaps up to 10 000 steps, 140 series --
+    more than one launch batch of the (mu, z) scratch (2 GiB / (16 B x T) = 134 series per launch,
+    sts_spline.hip spline_batch): bit-exact, every batch."""
+    from sparkts import _native
+    rng = np.random.default_rng(1234)
+    S, T = 140, 1_000_000
+    x = 100.0 + np.cumsum(rng.standard_normal((S, T)), axis=1) * 0.01
+    x[rng.random((S, T)) < 0.05] = NaN
+    for s in range(0, S, 7):
+        a = int(rng.integers(1, T - 10_001))
+        x[s, a:a + int(rng.integers(100, 10_000))] = NaN
+    ref, rerr = oracle.panel_fill(x, "spline", threads=8)
+    assert (rerr == 0).all()
+    xd = torch.as_tensor(x, device="cuda:0")
+    out = torch.empty_like(xd)
+    assert _native.lib().sts_fill(xd.data_ptr(), out.data_ptr(), S, T, T, T, 4, None, None) == 0, \
+        _native.lib().sts_last_error()
+    assert_bits(out.cpu().numpy(), ref, "spline T = 1e6")
