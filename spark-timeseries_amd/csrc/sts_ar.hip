@@ -43,6 +43,17 @@ constexpr int kLd = kPMax + 2;   // row stride of the (p+1) x (p+1) Gram in LDS
 constexpr double kRuleRatio2 = 256.0;   // (|mean| / centred column rms)^2 < 16^2
 constexpr double kRuleKappa = 100.0;    // 1 / (scaled Cholesky pivot)^2 < 100
 constexpr double kRuleLevel = 100.0;    // |mean| / |c| < 100
+// Round 6: the register kernel skips its refinement pass when every scaled Cholesky pivot^2 of
+// the centred lag Gram exceeds 1 / kRefineKappa (nearly orthogonal lags, e.g. every C4 series:
+// 1 / pivot^2 ~ 1.1).  Calibration (tools/ar_flag_study.py families + the filled ones, 6 488
+// intercept fits, numpy emulation of the unrefined centred normal equations): wherever the AR
+// rule keeps a series AND 1 / pivot^2 < 4, the unrefined solution is within 8.8e-12
+// elementwise of the reference -- the reference's own distance to the exact solution there, the
+// refined one's too -- against 1.8e-9 without the pivot bound.
+#ifndef STS_AR_SKIP_REFINE
+#define STS_AR_SKIP_REFINE 1
+#endif
+constexpr double kRefineKappa = 4.0;
 
 // the intercept half of the rule on a finished fit
 __device__ __forceinline__ bool ar_rule_level(double c, double mu) {
@@ -356,7 +367,7 @@ template <int P>
 __device__ __forceinline__ bool ar_normal_chol(const double (&Pd)[P + 1], double sy, const double (&hd)[P],
                                                const double (&tl)[P], bool intercept, double ifm,
                                                double (&A)[P + 1][P + 1], double (&cs)[P + 1],
-                                               double (&phi)[P + 1], double mu2m, bool& illc) {
+                                               double (&phi)[P + 1], double mu2m, bool& illc, bool& wellc) {
 #pragma unroll
     for (int i = 1; i <= P; i++) {
 #pragma unroll
@@ -390,11 +401,13 @@ __device__ __forceinline__ bool ar_normal_chol(const double (&Pd)[P + 1], double
     for (int j = 1; j <= P; j++) dg[j] = A[j][j];
     bool ok = true;
     illc = false;
+    wellc = true;
 #pragma unroll
     for (int j = 1; j <= P; j++) {
         const double djj = A[j][j];
         ok = ok && (djj > 0.0);
         illc = illc || !(mu2m < kRuleRatio2 * dg[j]) || !(djj * kRuleKappa > dg[j]);
+        wellc = wellc && (djj * kRefineKappa > dg[j]);
         const double l = __builtin_sqrt(djj);
         A[j][j] = l;
 #pragma unroll
@@ -551,8 +564,8 @@ __global__ __launch_bounds__(64 * NWV, STS_AR_WAVES_PER_EU) void ar_fit_blk_kern
     const double ifm = 1.0 / fm;   // the fit is a 1e-10-tolerance path: multiply, no division chains
     const bool bad = __builtin_isnan(sy) || __builtin_isnan(part);
     double A[P + 1][P + 1], cs[P + 1], phi[P + 1];
-    bool illc;
-    const bool ok = ar_normal_chol<P>(Pd, sy, hd, tl, intercept, ifm, A, cs, phi, mu * mu * fm, illc);
+    bool illc, wellc;
+    const bool ok = ar_normal_chol<P>(Pd, sy, hd, tl, intercept, ifm, A, cs, phi, mu * mu * fm, illc, wellc);
     auto Lu = [&](int i, int k) -> double { return A[i][k]; };
     // reciprocals of L's diagonal once: the two solves' substitutions are chains of P steps,
     // and a division per step was ~10 instructions of dependent latency
@@ -585,6 +598,14 @@ __global__ __launch_bounds__(64 * NWV, STS_AR_WAVES_PER_EU) void ar_fit_blk_kern
         for (int k = 1; k <= P; k++) sc -= phi[k] * cs[k];
         cpr = intercept ? sc * ifm : 0.0;
         AR_STAMP(3);
+        if (STS_AR_SKIP_REFINE && wellc && !illc) {
+            // nearly orthogonal lags: the unrefined solution already sits at the reference's own
+            // distance from the exact one (kRefineKappa); un-shift and skip the residual pass
+            double sphi = 0.0;
+#pragma unroll
+            for (int k = 1; k <= P; k++) sphi += phi[k];
+            cpr = intercept ? cpr + mu * (1.0 - sphi) : 0.0;
+        } else {
 
         // ---- refinement: exact residual pass e_t = Y_t - c' - sum_k phi_k Y_{t-k},
         //      rows t = P .. T-1 of the lag design ----
@@ -645,6 +666,7 @@ __global__ __launch_bounds__(64 * NWV, STS_AR_WAVES_PER_EU) void ar_fit_blk_kern
         }
         // un-shift: y = x - mu  =>  c = c' + mu * (1 - sum phi)
         cpr = intercept ? (cpr + dc * ifm) + mu * (1.0 - sphi) : 0.0;
+        }
         AR_STAMP(5);
     } else {
         cpr = __builtin_nan("");

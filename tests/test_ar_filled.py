@@ -304,3 +304,35 @@ def test_gpu_ar_fit_filled_fuzz(torch, seed):
             if no_int:
                 got, ref = got[1:], ref[1:]
             assert elementwise(got, ref) <= ELEM_TOL, (seed, case, method, T, p, no_int, s)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("p", [2, 5, 8])
+def test_gpu_ar_fit_around_the_refinement_bound(torch, p):
+    """Round 6: the register AR kernel skips its refinement pass when every scaled Cholesky pivot^2
+    exceeds 1 / 4 (sts_ar.hip kRefineKappa).  AR(1) series at phi around sqrt(3) / 2 put
+    1 / pivot^2 = 1 / (1 - rho^2) on both sides of 4 (the lags of an AR(1) have no partial
+    correlation past the first); levels keep the AR rule quiet.  Device vs oracle <= 1e-10
+    elementwise on both sides, fit and fused residuals."""
+    from sparkts.models import Autoregression
+    T = 2520
+    rows = []
+    for phi in (0.80, 0.85, 0.86, 0.866, 0.87, 0.88, 0.90):
+        for seed in range(3):
+            rng = np.random.default_rng(seed * 100 + int(phi * 1000))
+            e = rng.standard_normal(T)
+            y = np.empty(T)
+            y[0] = e[0]
+            for t in range(1, T):
+                y[t] = phi * y[t - 1] + e[t]
+            rows.append(10.0 + y)
+    x = np.array(rows)
+    m, resid = Autoregression.fitModelAndRemove(torch.as_tensor(x, device="cuda:0"), p)
+    c, coef, res = m.c.cpu().numpy(), m.coefficients.cpu().numpy(), resid.cpu().numpy()
+    kappas = []
+    for s in range(x.shape[0]):
+        rc, rcoef = oracle.ar_fit(x[s], p)
+        assert elementwise(np.r_[c[s], coef[s]], np.r_[rc, rcoef]) <= ELEM_TOL, (p, s)
+        assert same_bits(res[s], oracle.ar_remove(x[s], c[s], coef[s])), ("residuals", s)
+        kappas.append(rule_stats(x[s], p, rc)[1])
+    assert min(kappas) < 4.0 < max(kappas)   # both sides of the bound are exercised

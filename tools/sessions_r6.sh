@@ -55,6 +55,22 @@ case "$SESSION" in
       done
     done
     ;;
+  arskip)
+    # C4: the register AR kernel skipping its refinement pass on nearly orthogonal lags (product)
+    # against the same sources with -DSTS_AR_SKIP_REFINE=0 (var_norefskip); AR parity first
+    timeout -k 10 900 $PYT tests/test_ar_price_levels.py tests/test_ar_filled.py > $O/arskip_pytest1.log 2>&1 || { tail -40 $O/arskip_pytest1.log; exit 1; }
+    tail -1 $O/arskip_pytest1.log
+    timeout -k 10 900 $PYT tests/test_parity_gpu.py tests/test_fuzz_gpu.py tests/test_garch.py -k "ar or AR or arima or argarch" > $O/arskip_pytest2.log 2>&1 || { tail -40 $O/arskip_pytest2.log; exit 1; }
+    tail -1 $O/arskip_pytest2.log
+    V=spark-timeseries_amd/build/var_norefskip/libsts_hip.so
+    for rep in 1 2 3; do
+      for L in skip norefskip; do
+        if [ $L = norefskip ]; then E="STS_HIP_LIB=$V"; else E=""; fi
+        env $E timeout -k 10 200 python -u bench.py --workload c4 --steps 20 --warmup 5 --cpu-seconds 2 > $O/arskip_$L.json 2>/dev/null || exit 1
+        python -c "import json; d=json.load(open('$O/arskip_$L.json')); r=d['roofline']; print(json.dumps({'lib': '$L', 'rep': $rep, 'kernel_ms': r['avg_kernel_ms'], 'frac': r['frac'], 'check': d['cpu_baseline']['sample_check']}))" | tee -a $O/arskip.jsonl
+      done
+    done
+    ;;
   *)
     echo "unknown session $SESSION"; exit 2 ;;
 esac
