@@ -308,6 +308,10 @@ int run_tile(const double* in, double* out, double* lagmat, int64_t S, int64_t T
     // (sts_short.hip; its rule-3 fallback re-reads the filled series from out); STS_NO_SHORT keeps
     // the segment kernel (A/B build)
     const bool short_k = fuse && out && sts::short_ok(method, T, K) && !sts::ab_knob("STS_NO_SHORT");
+    // two series per workgroup on one LDS block (sts_short.hip short_pair_kernel); STS_SHORT_PAIR=0/1
+    // picks the form on the A/B build
+    const char* pair_env = sts::ab_knob("STS_SHORT_PAIR");
+    const bool short_pair = pair_env ? pair_env[0] == '1' : sts::kShortPairDefault;
     if (err && !one_seg) HIP_TRY(hipMemsetAsync(err, 0, (size_t)S * sizeof(int32_t), st), "hipMemsetAsync(err)");
     Scratch part(st);
     int32_t* exact = nullptr;
@@ -328,7 +332,7 @@ int run_tile(const double* in, double* out, double* lagmat, int64_t S, int64_t T
         }
     }
     prof_mark(st);
-    hipError_t e = short_k ? sts::launch_short(method, a, st)
+    hipError_t e = short_k ? sts::launch_short(method, a, st, short_pair)
                    : seg   ? sts::launch_segment(method, a, st)
                            : sts::launch_tile(method, tw, a, st);
     prof_mark(st);

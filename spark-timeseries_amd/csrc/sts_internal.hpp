@@ -22,6 +22,8 @@ constexpr int kPartSum = 64, kPartSq = 65, kPartShift = 66;
 // autocorr head / tail length handled per lag by the finalize (sts_acf.hpp); K <= kAcfEdge
 // on the fused paths, and series shorter than 2 kAcfEdge take the direct two-pass finalize
 constexpr int kAcfEdge = 64;
+// short fused fill + ACF: the two-series-per-block form (sts_short.hip short_pair_kernel) by default
+constexpr bool kShortPairDefault = false;
 
 struct TileArgs {
     const double* in;
@@ -101,7 +103,7 @@ hipError_t launch_segment(int method, const TileArgs& a, hipStream_t st);
 // fill('linear') + fused ACF with the whole series in one wave's registers (sts_short.hip):
 // short_ok() says whether a one-segment, fused-ACF seg call may take it instead
 bool short_ok(int method, int64_t T, int K);
-hipError_t launch_short(int method, const TileArgs& a, hipStream_t st);
+hipError_t launch_short(int method, const TileArgs& a, hipStream_t st, bool pair);
 
 // fillts "spline" (sts_spline.hip): series per launch for the (mu, z) scratch rows (16 B per
 // step), and the batched launches over S series (scratch: spline_batch(S, T) x T double2)

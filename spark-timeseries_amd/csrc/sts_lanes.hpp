@@ -37,6 +37,21 @@ __device__ __forceinline__ double row_sum_dpp(double v) {
     v = v + dpp_d<0x124>(v);
     return v + dpp_d<0x128>(v);
 }
+// sum over the wave into lane 63 only, no SGPRs: row_sum_dpp, then DPP row_bcast:15 (rows 1 / 3
+// add lane 15 / 47) and row_bcast:31 (rows 2 / 3 add lane 31): lane 63 = (r2 + r3) + (r0 + r1),
+// wave_sum_dpp's bits (a + b = b + a exactly)
+template <int CTRL, int ROWS>
+__device__ __forceinline__ double dpp_rows_d(double v) {
+    const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)(unsigned)u, CTRL, ROWS, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(unsigned)(u >> 32), CTRL, ROWS, 0xf, false);
+    return __builtin_bit_cast(double, ((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
+}
+__device__ __forceinline__ double wave_sum_to_63(double v) {
+    v = row_sum_dpp(v);
+    v = v + dpp_rows_d<0x142, 0xa>(v);
+    return v + dpp_rows_d<0x143, 0xc>(v);
+}
 // lane l - 1's value (wave_shr:1; lane 0 gets 0)
 __device__ __forceinline__ double lane_prev(double v) { return dpp_d<0x138>(v); }
 // lane l + 1's value (wave_shl:1; lane 63 gets 0)

@@ -22,6 +22,8 @@
 // Tolerance as every ACF path: 1e-10 relative to the oracle; the fill is bit-exact.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <atomic>
 #include <cstdint>
 
 #include "sts.h"
@@ -39,6 +41,10 @@ namespace {
                             // ends (C1: 0.1003-0.1012 ms vs 0.1036-0.1051 for 2, 0.108 for 4)
 #endif
 constexpr int kShortWaves = STS_SHORT_WAVES;
+
+#ifndef STS_SHORT_TRIM
+#define STS_SHORT_TRIM 1   // fewer VALU per series: bounds as masks / a c0-filled tail (round 6)
+#endif
 
 #ifndef STS_SHORT_DIAG
 #define STS_SHORT_DIAG 0   // timing-only cost models (tools/variant.sh): 1 no ACF, 2 no fill,
@@ -73,47 +79,54 @@ __device__ __forceinline__ double shift_from_masks(const double* buf, unsigned l
     return median_of_lanes(v, true, lane);
 }
 
-template <int B, int KM, int M>
-__global__ __launch_bounds__(64 * kShortWaves, 2) void short_fill_acf_kernel(TileArgs a) {
+// ---- the pieces both kernels share ----
+
+// the series into the LDS block by LDS-DMA (T even, 16-B aligned rows: whole 16-B pieces);
+// returns the lane's validity mask (bit j: step t0 + j is inside the series and valid)
+template <int B>
+__device__ __forceinline__ unsigned long long short_load(double* buf, const double* src, int T, int lane, int t0) {
+    const unsigned lb = lds_addr(buf);
+#pragma unroll
+    for (int i = 0; i < B / 2; i++) {
+        const int u = 2 * (i * 64 + lane);
+        // past the series end: a copy of its last pair (T even), never read as data
+        glds16(src + (STS_SHORT_TRIM ? (u < T - 2 ? u : T - 2) : (u < T ? u : 0)), lb + i * 1024);
+    }
+    dma_wait();
+    wave_lds_sync();
+    unsigned long long vm = 0ull;
+    if (STS_SHORT_TRIM) {   // the bound as one mask instead of a test per step
+#pragma unroll
+        for (int j = 0; j < B / 2; j++) {
+            const double2 v = *reinterpret_cast<const double2*>(buf + t0 + 2 * j);
+            if (!__builtin_isnan(v.x)) vm |= 1ull << (2 * j);
+            if (!__builtin_isnan(v.y)) vm |= 1ull << (2 * j + 1);
+        }
+        const int n = T - t0;   // steps of this block inside the series
+        vm &= n >= 64 ? ~0ull : n <= 0 ? 0ull : (1ull << n) - 1ull;
+    } else {
+#pragma unroll
+        for (int j = 0; j < B / 2; j++) {
+            const double2 v = *reinterpret_cast<const double2*>(buf + t0 + 2 * j);
+            if (t0 + 2 * j < T && !__builtin_isnan(v.x)) vm |= 1ull << (2 * j);
+            if (t0 + 2 * j + 1 < T && !__builtin_isnan(v.y)) vm |= 1ull << (2 * j + 1);
+        }
+    }
+    return vm;
+}
+
+// The fill, run by run into the LDS block (a lane walks only its own runs).  A run is a
+// maximal NaN stretch with valid ends L (or none, -1) and R (or none, T):
+//   linear   (S/UnivariateTimeSeries.scala:247-266): both ends needed, r[t] = r[t-1] +
+//            (x_R - x_L) / (R - L), sequentially from L;
+//   previous (:194-204) x_L;  next (:214-224) x_R;
+//   nearest  (:156-184) x_L while t - L < R - t, else x_R (ties to R), one end enough;
+//            index 0 is never rewritten and never an end; no end at all throws.
+// Returns fillNearest's "Input is all NaNs!" (no valid step after index 0).
+template <int B, int M>
+__device__ __forceinline__ bool short_fill(double* buf, unsigned long long vm, int T, int lane, int t0) {
     static_assert(M == STS_FILL_LINEAR || M == STS_FILL_PREVIOUS || M == STS_FILL_NEXT || M == STS_FILL_NEAREST,
                   "fill method");
-    constexpr int BUFD = 64 * B;   // doubles per wave block: the whole series
-    __shared__ __attribute__((aligned(16))) double buf_mem[kShortWaves * BUFD];
-    const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int64_t s = (int64_t)blockIdx.x * kShortWaves + wave;   // (an XCD-contiguous remap: 0.1025-0.1029 vs 0.1028-0.1030 ms, round 4)
-    if (s >= a.S) return;
-    double* buf = buf_mem + wave * BUFD;
-    const int T = (int)a.T;
-    const int t0 = lane * B;
-    const double* src = a.in + s * a.ld_in;
-
-    // ---- the series into the LDS block (T even, 16-B aligned rows: whole 16-B pieces) ----
-    {
-        const unsigned lb = lds_addr(buf);
-#pragma unroll
-        for (int i = 0; i < B / 2; i++) {
-            const int u = 2 * (i * 64 + lane);
-            glds16(src + (u < T ? u : 0), lb + i * 1024);
-        }
-        dma_wait();
-        wave_lds_sync();
-    }
-    unsigned long long vm = 0ull;   // bit j: step t0 + j is inside the series and valid
-#pragma unroll
-    for (int j = 0; j < B / 2; j++) {
-        const double2 v = *reinterpret_cast<const double2*>(buf + t0 + 2 * j);
-        if (t0 + 2 * j < T && !__builtin_isnan(v.x)) vm |= 1ull << (2 * j);
-        if (t0 + 2 * j + 1 < T && !__builtin_isnan(v.y)) vm |= 1ull << (2 * j + 1);
-    }
-
-    // ---- the fill, run by run into the LDS block (a lane walks only its own runs).  A run is a
-    //      maximal NaN stretch with valid ends L (or none, -1) and R (or none, T):
-    //      linear   (S/UnivariateTimeSeries.scala:247-266): both ends needed, r[t] = r[t-1] +
-    //               (x_R - x_L) / (R - L), sequentially from L;
-    //      previous (:194-204) x_L;  next (:214-224) x_R;
-    //      nearest  (:156-184) x_L while t - L < R - t, else x_R (ties to R), one end enough;
-    //               index 0 is never rewritten and never an end; no end at all throws. ----
     // fillNearest's index 0 is not a valid end: out of its mask (the shift keeps using vm)
     const unsigned long long vf = (M == STS_FILL_NEAREST && lane == 0) ? vm & ~1ull : vm;
     const int fv = vf ? t0 + __builtin_ctzll(vf) : T;          // first valid step of the block
@@ -127,7 +140,6 @@ __global__ __launch_bounds__(64 * kShortWaves, 2) void short_fill_acf_kernel(Til
     const int Lc = below ? lvs : -1;   // last valid step before the block (-1: none)
     const int Rc = above ? fvs : T;    // first valid step after the block (T: none)
     const int tend = (t0 + B < T) ? t0 + B : T;   // end of this block inside the series
-    // fillNearest over a series with no valid step after index 0: "Input is all NaNs!"
     const bool all_nan = (M == STS_FILL_NEAREST) && hv == 0ull && T >= 2;
     // steps [q0, q1) of a run with ends L, R
     auto fill_run = [&](int q0, int q1, int L, int R) {
@@ -172,17 +184,61 @@ __global__ __launch_bounds__(64 * kShortWaves, 2) void short_fill_acf_kernel(Til
             fill_run(t, R < tend ? R : tend, t - 1, R);
         }
     }
-    wave_lds_sync();   // the LDS block now holds the filled series
+    return all_nan;
+}
 
-    // ---- filled series out: coalesced 1-KB stores from the block ----
-    if (a.out) {
-        double* dst = a.out + s * a.ld_out;
+// the filled series out of the block: coalesced 1-KB stores
+template <int B>
+__device__ __forceinline__ void short_store(double* dst, const double* buf, int T, int lane) {
 #pragma unroll
-        for (int i = 0; i < B / 2; i++) {
-            const int u = 2 * (i * 64 + lane);
-            if (u < T) store_pair16<true>(dst + u, buf + u);   // nt stores: C1 0.0926 vs 0.1030 ms (nt loads too: 0.098)
-        }
+    for (int i = 0; i < B / 2; i++) {
+        const int u = 2 * (i * 64 + lane);
+        if (u < T) store_pair16<true>(dst + u, buf + u);   // nt stores: C1 0.0926 vs 0.1030 ms (nt loads too: 0.098)
     }
+}
+
+// Finalize per lag i = lane + 1 (sts_acf.hpp acf_combine's sums, regrouped): slice 1 = y[i..64)
+// of the head + the whole tail + the middle, slice 2 = the whole head + z[i..64) of the tail +
+// the middle; every partial is a sum of its own terms (suffix scans over the lanes, no "total
+// minus head").  Pi: lag i's lag product, Sm / Qm: the middle sums, yh = y(lane), zt =
+// y(T - 1 - lane).  `suspect`: sts_acf.hpp rule 3 for this lane's lag.
+__device__ __forceinline__ double short_finalize(double Pi, double Sm, double Qm, double yh, double zt, double c0,
+                                                 int T, int lane, bool& suspect) {
+    // suffix sums from lane .. 63 by DPP (round 5: the ds_bpermute scan it replaces was ~1/3 of the
+    // finalize's latency)
+    const double ys = suffix_sum_dpp(yh, lane), yq = suffix_sum_dpp(yh * yh, lane);
+    const double zs = suffix_sum_dpp(zt, lane), zq = suffix_sum_dpp(zt * zt, lane);
+    const double Yall = lane_bcast(ys, 0), YQall = lane_bcast(yq, 0), Zall = lane_bcast(zs, 0),
+                 ZQall = lane_bcast(zq, 0);
+    // lag i = lane + 1 wants the suffixes from position i: lane i's (none for i = 64)
+    const double ysi = lane_next(ys), yqi = lane_next(yq), zsi = lane_next(zs), zqi = lane_next(zq);
+    const double sum1 = (Sm + Zall) + ysi, sq1 = (Qm + ZQall) + yqi;
+    const double sum2 = (Sm + Yall) + zsi, sq2 = (Qm + YQall) + zqi;
+    const double N = (double)(T - (lane + 1));
+    const double v1 = sq1 - sum1 * sum1 / N;
+    const double v2 = sq2 - sum2 * sum2 / N;
+    const double cv = Pi - sum1 * sum2 / N;
+    const double r = cv / (__builtin_sqrt(v1) * __builtin_sqrt(v2));   // :89
+    suspect = acf_suspect(r, sum1, sq1, sum2, sq2, v1, v2, N, c0);
+    return r;
+}
+
+template <int B, int KM, int M>
+__global__ __launch_bounds__(64 * kShortWaves, 2) void short_fill_acf_kernel(TileArgs a) {
+    constexpr int BUFD = 64 * B;   // doubles per wave block: the whole series
+    __shared__ __attribute__((aligned(16))) double buf_mem[kShortWaves * BUFD];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int64_t s = (int64_t)blockIdx.x * kShortWaves + wave;   // (an XCD-contiguous remap: 0.1025-0.1029 vs 0.1028-0.1030 ms, round 4)
+    if (s >= a.S) return;
+    double* buf = buf_mem + wave * BUFD;
+    const int T = (int)a.T;
+    const int t0 = lane * B;
+
+    const unsigned long long vm = short_load<B>(buf, a.in + s * a.ld_in, T, lane, t0);
+    const bool all_nan = short_fill<B, M>(buf, vm, T, lane, t0);
+    wave_lds_sync();   // the LDS block now holds the filled series
+    if (a.out) short_store<B>(a.out + s * a.ld_out, buf, T, lane);
     if (a.err && lane == 0) a.err[s] = all_nan ? STS_ERR_ALL_NAN : STS_OK;
     const int K = a.K;
     if (K <= 0 || a.acf_fused == nullptr || STS_SHORT_DIAG == 1) return;
@@ -191,11 +247,24 @@ __global__ __launch_bounds__(64 * kShortWaves, 2) void short_fill_acf_kernel(Til
 
     // ---- ACF: y = F - c, lag products P_d = sum_t y_t y_{t-d}, middle sums ----
     double x[B];
+    if (STS_SHORT_TRIM) {
+        // the block past the series end holds c0, so y there is c0 - c0 = 0 without a select per
+        // step (a non-finite c0 makes every y NaN anyway)
+        for (int t = T + lane; t < BUFD; t += 64) buf[t] = c0;
+        wave_lds_sync();
 #pragma unroll
-    for (int j = 0; j < B / 2; j++) {
-        const double2 v = *reinterpret_cast<const double2*>(buf + t0 + 2 * j);
-        x[2 * j] = (t0 + 2 * j < T) ? v.x - c0 : 0.0;
-        x[2 * j + 1] = (t0 + 2 * j + 1 < T) ? v.y - c0 : 0.0;
+        for (int j = 0; j < B / 2; j++) {
+            const double2 v = *reinterpret_cast<const double2*>(buf + t0 + 2 * j);
+            x[2 * j] = v.x - c0;
+            x[2 * j + 1] = v.y - c0;
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < B / 2; j++) {
+            const double2 v = *reinterpret_cast<const double2*>(buf + t0 + 2 * j);
+            x[2 * j] = (t0 + 2 * j < T) ? v.x - c0 : 0.0;
+            x[2 * j + 1] = (t0 + 2 * j + 1 < T) ? v.y - c0 : 0.0;
+        }
     }
     // the head y(0..63) and the tail y(T-1-j), one per lane (T >= 128: disjoint)
     const double yh = buf[lane] - c0, zt = buf[T - 1 - lane] - c0;
@@ -250,28 +319,11 @@ __global__ __launch_bounds__(64 * kShortWaves, 2) void short_fill_acf_kernel(Til
         if (lane < K) a.acf_fused[s * K + lane] = Pi + Sm + Qm;
         return;
     }
-    // ---- finalize per lag i = lane + 1 (sts_acf.hpp acf_combine's sums, regrouped): slice 1
-    //      = y[i..64) of the head + the whole tail + the middle, slice 2 = the whole head +
-    //      z[i..64) of the tail + the middle; every partial is a sum of its own terms (suffix
-    //      scans over the lanes, no "total minus head") ----
-    // suffix sums from lane .. 63 by DPP (round 5: the ds_bpermute scan it replaces was ~1/3 of the
-    // finalize's latency)
-    const double ys = suffix_sum_dpp(yh, lane), yq = suffix_sum_dpp(yh * yh, lane);
-    const double zs = suffix_sum_dpp(zt, lane), zq = suffix_sum_dpp(zt * zt, lane);
-    const double Yall = lane_bcast(ys, 0), YQall = lane_bcast(yq, 0), Zall = lane_bcast(zs, 0),
-                 ZQall = lane_bcast(zq, 0);
-    // lag i = lane + 1 wants the suffixes from position i: lane i's (none for i = 64)
-    const double ysi = lane_next(ys), yqi = lane_next(yq), zsi = lane_next(zs), zqi = lane_next(zq);
-    const double sum1 = (Sm + Zall) + ysi, sq1 = (Qm + ZQall) + yqi;
-    const double sum2 = (Sm + Yall) + zsi, sq2 = (Qm + YQall) + zqi;
-    const double N = (double)(T - (lane + 1));
-    const double v1 = sq1 - sum1 * sum1 / N;
-    const double v2 = sq2 - sum2 * sum2 / N;
-    const double cv = Pi - sum1 * sum2 / N;
-    double r = cv / (__builtin_sqrt(v1) * __builtin_sqrt(v2));   // :89
+    bool sus;
+    double r = short_finalize(Pi, Sm, Qm, yh, zt, c0, T, lane, sus);
     // sts_acf.hpp rule 3: a suspect series takes the reference's loop over the filled series
     // this wave stored (the LDS block is scratch by now): order the stores before the reads
-    if (__ballot(lane < K && acf_suspect(r, sum1, sq1, sum2, sq2, v1, v2, N, c0))) {
+    if (__ballot(lane < K && sus)) {
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
         // F streams back through the (now free) block: the reference's loop, every sum from LDS
         // (sts_acf.hpp acf_exact_stream; in this kernel, so the normal case pays no extra launch)
@@ -280,6 +332,131 @@ __global__ __launch_bounds__(64 * kShortWaves, 2) void short_fill_acf_kernel(Til
         if (lane < K) r = e;
     }
     if (lane < K) a.acf_fused[s * K + lane] = r;
+}
+
+// LDS barrier of the two waves of a pair workgroup (LDS ordering only: the block changes hands;
+// global stores stay in flight)
+__device__ __forceinline__ void pair_lds_barrier() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+// Round 6: two waves per workgroup on ONE LDS block, ping-pong.  The one-wave
+// kernel above holds its 20-KB block through the whole ACF although the block is only needed
+// until y is in registers.  Here the workgroup is persistent over the series g, g + G, g + 2G, ...
+// (G workgroups) and its two waves alternate: in phase p the block's owner (wave p % 2) streams
+// series slot p in, fills it, stores it and takes y into registers, while the other wave runs the
+// lag products and the finalize of slot p - 1 from its registers; an LDS barrier ends the phase.
+// So each block is always streaming, and a CU holds 8 blocks with 16 waves -- which needs <= 128
+// VGPRs: y stays resident (2B VGPRs), the lag products run in passes of <= 12 lags with the
+// previous lane's steps fetched one at a time (no rolling window), and the wave sums go by DPP
+// (no LDS scratch: the block belongs to the partner).  Rule 3 runs after the loop, when the block
+// is free (half per wave), for the slots a wave recorded (the 64 first; later ones read global
+// memory directly, sts_acf.hpp acf_exact_lag: the same bits).
+#ifndef STS_PAIR_LAGS
+#define STS_PAIR_LAGS 8   // lags per pass of the pair kernel's lag products
+#endif
+constexpr int kPairLags = STS_PAIR_LAGS;
+
+template <int B, int KM, int M>
+__global__ __launch_bounds__(128, 4) void short_pair_kernel(TileArgs a) {
+    constexpr int BUFD = 64 * B;
+    __shared__ __attribute__((aligned(16))) double buf[BUFD];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int64_t G = gridDim.x, g = blockIdx.x;
+    const int64_t nslots = g < a.S ? (a.S - g + G - 1) / G : 0;
+    const int T = (int)a.T;
+    const int t0 = lane * B;
+    const int K = a.K;
+    const bool acf = K > 0 && a.acf_fused != nullptr;
+    static_assert(KM <= B, "the lag partners reach one lane back only");
+    double x[B];
+    double yh = 0.0, zt = 0.0, c0 = 0.0;
+    unsigned long long sus_slots = 0ull;   // bit j: this wave's slot 2j + wave needs rule 3
+    for (int64_t p = 0; p <= nslots; p++) {
+        // per-phase opaque copies: the per-step predicates and addresses derived from them are
+        // recomputed in each phase instead of hoisted out of the loop (and spilled)
+        int lane_q = lane, T_q = T;
+        asm volatile("" : "+v"(lane_q));
+        asm volatile("" : "+s"(T_q));
+        const int lane = lane_q, T = T_q, t0 = lane * B;
+        if ((int)(p & 1) == wave) {
+            if (p < nslots) {   // ---- the block's owner: series in, fill, out, y -> registers ----
+                const int64_t s = g + p * G;
+                const unsigned long long vm = short_load<B>(buf, a.in + s * a.ld_in, T, lane, t0);
+                const bool all_nan = short_fill<B, M>(buf, vm, T, lane, t0);
+                wave_lds_sync();
+                if (a.out) short_store<B>(a.out + s * a.ld_out, buf, T, lane);
+                if (a.err && lane == 0) a.err[s] = all_nan ? STS_ERR_ALL_NAN : STS_OK;
+                if (acf) c0 = shift_from_masks<B>(buf, vm, T, lane, M == STS_FILL_PREVIOUS);
+            }
+            // y into registers on EVERY path through this branch (past the last slot: whatever the
+            // block holds, never used), so the previous slot's y is dead during the fill instead of
+            // carried around the loop
+#pragma unroll
+            for (int j = 0; j < B / 2; j++) {
+                const double2 v = *reinterpret_cast<const double2*>(buf + t0 + 2 * j);
+                x[2 * j] = (t0 + 2 * j < T) ? v.x - c0 : 0.0;
+                x[2 * j + 1] = (t0 + 2 * j + 1 < T) ? v.y - c0 : 0.0;
+            }
+            yh = buf[lane] - c0;
+            zt = buf[T - 1 - lane] - c0;
+        } else if (p >= 1 && acf && STS_SHORT_DIAG != 1) {   // ---- the other wave: slot p - 1's ACF from registers ----
+            const int64_t s = g + (p - 1) * G;
+            constexpr int NP = (KM + kPairLags - 1) / kPairLags, LP = (KM + NP - 1) / NP;
+            double Pi = 0.0, sm = 0.0, qm = 0.0;
+#pragma unroll
+            for (int pass = 0; pass < NP; pass++) {
+                const int d0 = 1 + pass * LP;   // lags d0 .. d0 + LP - 1 (past KM: zero, never read)
+                double P[LP];
+#pragma unroll
+                for (int q = 0; q < LP; q++) P[q] = 0.0;
+                // partners in the previous lane's block: y(t0 - m), one at a time (lane 0: 0)
+#pragma unroll
+                for (int m = 1; m < d0 + LP && m <= KM; m++) {
+                    const double pv = lane_prev(x[B - m]);
+#pragma unroll
+                    for (int q = 0; q < LP; q++)
+                        if (d0 + q >= m && d0 + q <= KM) P[q] = __builtin_fma(x[d0 + q - m], pv, P[q]);
+                }
+#pragma unroll
+                for (int j = 0; j < B; j++) {
+                    if (pass == 0 && acf_mid(t0 + j, T)) {
+                        sm += x[j];
+                        qm = __builtin_fma(x[j], x[j], qm);
+                    }
+#pragma unroll
+                    for (int q = 0; q < LP; q++)
+                        if (j >= d0 + q && d0 + q <= KM && STS_SHORT_DIAG != 5) P[q] = __builtin_fma(x[j], x[j - d0 - q], P[q]);
+                }
+                // wave sums into lane 63 (DPP only), then lag d's to lane d - 1
+#pragma unroll
+                for (int q = 0; q < LP && d0 + q <= KM; q++) {
+                    const double tot = lane_bcast(wave_sum_to_63(P[q]), 63);
+                    if (lane == d0 + q - 1) Pi = tot;
+                }
+            }
+            const double Sm = lane_bcast(wave_sum_to_63(sm), 63), Qm = lane_bcast(wave_sum_to_63(qm), 63);
+            bool sus;
+            double r = short_finalize(Pi, Sm, Qm, yh, zt, c0, T, lane, sus);
+            if (__ballot(lane < K && sus)) sus_slots |= 1ull << ((p - 1) >> 1);   // < 64: the launcher caps nslots
+            if (lane < K) a.acf_fused[s * K + lane] = r;
+        }
+        pair_lds_barrier();   // the block changes hands
+    }
+    // ---- rule 3 (sts_acf.hpp) for the recorded slots: the reference's loop over the filled series
+    //      this wave stored, streamed through its half of the (now free) block ----
+    if (sus_slots) __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    while (sus_slots) {
+        const int j = __builtin_ctzll(sus_slots);
+        sus_slots &= sus_slots - 1ull;
+        const int64_t s = g + (2 * (int64_t)j + wave) * G;
+        constexpr int CX = 32 * B - 64 < 512 ? 32 * B - 64 : 512;
+        const double e = acf_exact_stream<CX>(a.out + s * a.ld_out, T, lane + 1, lane < K, buf + wave * (BUFD / 2), lane);
+        if (lane < K) a.acf_fused[s * K + lane] = e;
+    }
 }
 
 }  // namespace
@@ -292,19 +469,39 @@ bool short_ok(int method, int64_t T, int K) {
            T > 2 * (int64_t)K;
 }
 
+// compute units of the current device (cached per device; 256 on MI355X)
+int cu_count() {
+    static std::atomic<int> cache[64];
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0) dev = 0;
+    const int slot = dev < 64 ? dev : 63;
+    int n = cache[slot].load(std::memory_order_relaxed);
+    if (n <= 0) {
+        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+        cache[slot].store(n, std::memory_order_relaxed);
+    }
+    return n;
+}
+
 template <int M>
-hipError_t launch_short_m(const TileArgs& a, hipStream_t st) {
+hipError_t launch_short_m(const TileArgs& a, hipStream_t st, bool pair) {
     if (a.S <= 0) return hipSuccess;
-    const int64_t nblk = (a.S + kShortWaves - 1) / kShortWaves;
+    // the pair form is persistent: two series per workgroup and 8 workgroups (LDS blocks) per CU at most
+    // (>= S / 128 workgroups: a wave's rule-3 record holds 64 slots)
+    const int64_t nblk = pair ? std::max<int64_t>(std::min<int64_t>((a.S + 1) / 2, 8 * (int64_t)cu_count()), (a.S + 127) / 128)
+                              : (a.S + kShortWaves - 1) / kShortWaves;
     if (nblk > 0x7fffffffLL) return hipErrorInvalidValue;
-    dim3 g((unsigned)nblk), b(64 * kShortWaves);
+    dim3 g((unsigned)nblk), b(pair ? 128 : 64 * kShortWaves);
     const int64_t need = (a.T + 63) / 64;
     // the lag window (KM >= K, a multiple of 4) reaches back KM steps: blocks of >= KM steps
     const int KM = (a.K + 3) / 4 * 4 < 8 ? 8 : (a.K + 3) / 4 * 4;
     const int64_t nb = need < KM ? KM : need;
     const int B = nb <= 8 ? 8 : nb <= 16 ? 16 : nb <= 24 ? 24 : nb <= 32 ? 32 : 40;
-#define STS_SHORT_K(BB, KK) \
-    case KK: hipLaunchKernelGGL((short_fill_acf_kernel<BB, (KK <= BB ? KK : BB), M>), g, b, 0, st, a); break;
+#define STS_SHORT_K(BB, KK)                                                                        \
+    case KK:                                                                                       \
+        if (pair) hipLaunchKernelGGL((short_pair_kernel<BB, (KK <= BB ? KK : BB), M>), g, b, 0, st, a); \
+        else hipLaunchKernelGGL((short_fill_acf_kernel<BB, (KK <= BB ? KK : BB), M>), g, b, 0, st, a);  \
+        break;
 #define STS_SHORT(BB)                                                                              \
     case BB:                                                                                       \
         switch (KM) {                                                                              \
@@ -322,12 +519,12 @@ hipError_t launch_short_m(const TileArgs& a, hipStream_t st) {
     return hipGetLastError();
 }
 
-hipError_t launch_short(int method, const TileArgs& a, hipStream_t st) {
+hipError_t launch_short(int method, const TileArgs& a, hipStream_t st, bool pair) {
     switch (method) {
-    case STS_FILL_LINEAR: return launch_short_m<STS_FILL_LINEAR>(a, st);
-    case STS_FILL_PREVIOUS: return launch_short_m<STS_FILL_PREVIOUS>(a, st);
-    case STS_FILL_NEXT: return launch_short_m<STS_FILL_NEXT>(a, st);
-    case STS_FILL_NEAREST: return launch_short_m<STS_FILL_NEAREST>(a, st);
+    case STS_FILL_LINEAR: return launch_short_m<STS_FILL_LINEAR>(a, st, pair);
+    case STS_FILL_PREVIOUS: return launch_short_m<STS_FILL_PREVIOUS>(a, st, pair);
+    case STS_FILL_NEXT: return launch_short_m<STS_FILL_NEXT>(a, st, pair);
+    case STS_FILL_NEAREST: return launch_short_m<STS_FILL_NEAREST>(a, st, pair);
     default: return hipErrorInvalidValue;
     }
 }

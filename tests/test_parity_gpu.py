@@ -327,6 +327,8 @@ KNOB_VARIANTS = {
     "tile": {"STS_TILE_KERNEL": "tile"},
     "seg": {"STS_TILE_KERNEL": "seg", "STS_NO_SHORT": "1"},
     "short": {"STS_TILE_KERNEL": "seg"},                              # linear, K <= 24, T <= 2560: sts_short.hip
+    "short1": {"STS_TILE_KERNEL": "seg", "STS_SHORT_PAIR": "0"},      # its one-series-per-block form
+    "short2": {"STS_TILE_KERNEL": "seg", "STS_SHORT_PAIR": "1"},      # two series per block (round 6)
     "tile2048": {"STS_TILE_KERNEL": "tile", "STS_TILE_W": "2048"},    # 2-wave workgroups, 2048-step tiles
     "tilec4": {"STS_TILE_KERNEL": "tile", "STS_TILES_PER_CHUNK": "4"},  # 4 tiles per workgroup
     "seg3": {"STS_TILE_KERNEL": "seg", "STS_SEG_TILES": "3"},          # multi-segment partials + finalize
@@ -418,11 +420,12 @@ def test_short_fill_acf(torch, monkeypatch, method, K):
     rng = np.random.default_rng(1000 + K + 100 * code)
 
     def run(lib, x, T):
+        S = x.shape[0]
         xd = dev(torch, x)
         out = torch.empty_like(xd)
-        acf = torch.empty((16, K), dtype=torch.float64, device="cuda:0")
-        e = torch.full((16,), 99, dtype=torch.int32, device="cuda:0")
-        assert lib.sts_fill_autocorr(xd.data_ptr(), out.data_ptr(), 16, T, T, T, code, K, acf.data_ptr(),
+        acf = torch.empty((S, K), dtype=torch.float64, device="cuda:0")
+        e = torch.full((S,), 99, dtype=torch.int32, device="cuda:0")
+        assert lib.sts_fill_autocorr(xd.data_ptr(), out.data_ptr(), S, T, T, T, code, K, acf.data_ptr(),
                                      e.data_ptr(), torch.cuda.current_stream().cuda_stream) == 0
         torch.cuda.synchronize()
         return host(out), host(acf), host(e)
@@ -461,6 +464,17 @@ def test_short_fill_acf(torch, monkeypatch, method, K):
         assert np.array_equal(seg_e, err)
         assert_bits(seg_f[ok], rf[ok], "seg fill T=%d" % T)
         assert_rel(got_a[ok], seg_a[ok], what="short vs seg %s T=%d K=%d" % (method, T, K))
+        # both forms of the short kernel (one series per LDS block / two per block: round 6),
+        # also on an odd panel (the second wave of the last pair has no series)
+        for pair in ("0", "1"):
+            monkeypatch.setenv("STS_SHORT_PAIR", pair)
+            for rows in (slice(0, 16), slice(0, 15), slice(15, 16)):
+                pf, pa, pe = run(_native.load_variant(_native.AB_LIB_PATH), x[rows], T)
+                okr = ok[rows]
+                assert np.array_equal(pe, err[rows]), (pair, rows)
+                assert_bits(pf[okr], rf[rows][okr], "pair=%s fill T=%d" % (pair, T))
+                assert_rel(pa[okr], racf[rows][okr], what="pair=%s acf %s T=%d K=%d" % (pair, method, T, K))
+            monkeypatch.delenv("STS_SHORT_PAIR")
 
 
 def test_fill_autocorr_c3_length(torch):

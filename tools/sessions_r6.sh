@@ -71,6 +71,58 @@ case "$SESSION" in
       done
     done
     ;;
+  pair)
+    # C1: the short kernel with two series per LDS block (STS_SHORT_PAIR on the A/B
+    # build): parity through the pair form first, then C1 / c1_rule3 alternating the two forms
+    AB=spark-timeseries_amd/build/libsts_hip_ab.so
+    timeout -k 10 900 $PYT tests/test_parity_gpu.py -k "short or fused or both_kernels" > $O/pair_pytest1.log 2>&1 || { tail -40 $O/pair_pytest1.log; exit 1; }
+    tail -1 $O/pair_pytest1.log
+    STS_SHORT_PAIR=1 timeout -k 10 900 $PYT --sts-lib $AB tests/test_acf_robust.py tests/test_parity_gpu.py -k "product or returns or short or autocorr or acf" > $O/pair_pytest2.log 2>&1 || { tail -40 $O/pair_pytest2.log; exit 1; }
+    tail -1 $O/pair_pytest2.log
+    # forms: 0 / 1 = STS_SHORT_PAIR on the A/B build; any other name = build/var_<name> (tools/variant.sh
+    # with -DSTS_AB) under STS_SHORT_PAIR=1
+    for rep in 1 2 3; do
+      for P in 0 1 $PAIR_VARS; do
+        L=$AB; PP=$P
+        case $P in 0|1) ;; *) L=spark-timeseries_amd/build/var_$P/libsts_hip.so; PP=1 ;; esac
+        for w in c1 ${PAIR_WL-c1_rule3}; do
+          STS_SHORT_PAIR=$PP STS_HIP_LIB=$L timeout -k 10 200 python -u bench.py --workload $w --steps 20 --warmup 5 --cpu-seconds 2 > $O/pair_${w}_$P.json 2>/dev/null || exit 1
+          python -c "import json; d=json.load(open('$O/pair_${w}_$P.json')); r=d['roofline']; print(json.dumps({'workload': '$w', 'form': '$P', 'rep': $rep, 'kernel_ms': r['avg_kernel_ms'], 'frac': r['frac'], 'ms_per_step': d['ms_per_step'], 'check': d['cpu_baseline']['sample_check']}))" | tee -a $O/pair.jsonl
+        done
+      done
+    done
+    ;;
+  c1sq)
+    # SQ counters of the C1 short kernel, both forms (STS_SHORT_PAIR on the A/B build), two passes each
+    AB=spark-timeseries_amd/build/libsts_hip_ab.so
+    export TMPDIR=/tmp
+    for P in 0 1; do
+      i=0
+      for grp in "SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY GRBM_GUI_ACTIVE" \
+                 "SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR GRBM_GUI_ACTIVE"; do
+        i=$((i+1))
+        STS_SHORT_PAIR=$P STS_HIP_LIB=$AB timeout -s KILL 120 rocprofv3 --pmc $grp -d $O/c1sq_${P}_$i -o run --output-format csv -- \
+            python -u bench.py --workload c1 --steps 3 --warmup 1 --no-cpu-baseline > $O/c1sq_${P}_$i.out 2>&1 || { tail -5 $O/c1sq_${P}_$i.out; exit 1; }
+      done
+    done
+    python tools/c1_sq.py $O/c1_sq.json $O
+    ;;
+  trim)
+    # C1: the one-wave short kernel with fewer VALU per series (STS_SHORT_TRIM, product) against
+    # var_notrim (-DSTS_SHORT_TRIM=0); the short-kernel parity first
+    timeout -k 10 900 $PYT tests/test_parity_gpu.py -k "short or fused or both_kernels or c1" > $O/trim_pytest.log 2>&1 || { tail -40 $O/trim_pytest.log; exit 1; }
+    tail -1 $O/trim_pytest.log
+    timeout -k 10 900 $PYT tests/test_acf_robust.py -k "product or returns or short" > $O/trim_pytest2.log 2>&1 || { tail -40 $O/trim_pytest2.log; exit 1; }
+    tail -1 $O/trim_pytest2.log
+    V=spark-timeseries_amd/build/var_notrim/libsts_hip.so
+    for rep in 1 2 3; do
+      for L in trim notrim; do
+        if [ $L = notrim ]; then E="STS_HIP_LIB=$V"; else E=""; fi
+        env $E timeout -k 10 200 python -u bench.py --workload c1 --steps 20 --warmup 5 --cpu-seconds 2 > $O/trim_$L.json 2>/dev/null || exit 1
+        python -c "import json; d=json.load(open('$O/trim_$L.json')); r=d['roofline']; print(json.dumps({'lib': '$L', 'rep': $rep, 'kernel_ms': r['avg_kernel_ms'], 'frac': r['frac'], 'check': d['cpu_baseline']['sample_check']}))" | tee -a $O/trim.jsonl
+      done
+    done
+    ;;
   *)
     echo "unknown session $SESSION"; exit 2 ;;
 esac
