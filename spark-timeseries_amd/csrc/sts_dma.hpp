@@ -36,6 +36,21 @@ __device__ __forceinline__ void glds16(const double* gsrc, unsigned lds_byte_add
                      : "memory");
 }
 
+// the same from a wave-uniform base (SGPR pair) plus a per-lane byte offset (VGPR): no 64-bit
+// address arithmetic per instruction
+__device__ __forceinline__ void glds16_s(const double* sbase, unsigned voff, unsigned lds_byte_addr) {
+    unsigned keep;
+    lds_byte_addr = __builtin_amdgcn_readfirstlane(lds_byte_addr);
+    // (readfirstlane returns int: through unsigned, or the low half sign-extends into the high one)
+    const unsigned long long b =
+        (unsigned long long)(unsigned)__builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)sbase) |
+        ((unsigned long long)(unsigned)__builtin_amdgcn_readfirstlane((unsigned)((uintptr_t)sbase >> 32)) << 32);
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(voff), "s"(b), "s"(lds_byte_addr)
+                 : "memory");
+}
+
 // one 16-B store of a staged result pair (NT: non-temporal)
 template <bool NT = false>
 __device__ __forceinline__ void store_pair16(double* p, const double* lds_src) {

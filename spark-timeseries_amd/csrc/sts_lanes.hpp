@@ -7,11 +7,14 @@ namespace sts {
 
 // ds_bpermute (what __shfl / __shfl_xor compile to) costs an LDS round trip (~100+ cycles);
 // DPP covers the in-row steps and the one-lane shift, v_readlane broadcasts from a known lane.
+// Every lane is written: bound_ctrl makes a lane whose source is out of range (wave_shr's lane
+// 0, row_shl past the row end) read 0, so no old value -- and no v_mov to zero it first (round 6:
+// one VALU per DPP move; the C1 short kernel's ~350 such moves per series)
 template <int CTRL>
 __device__ __forceinline__ double dpp_d(double v) {
     const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
-    const int lo = __builtin_amdgcn_update_dpp(0, (int)(unsigned)u, CTRL, 0xf, 0xf, false);
-    const int hi = __builtin_amdgcn_update_dpp(0, (int)(unsigned)(u >> 32), CTRL, 0xf, 0xf, false);
+    const int lo = __builtin_amdgcn_mov_dpp((int)(unsigned)u, CTRL, 0xf, 0xf, true);
+    const int hi = __builtin_amdgcn_mov_dpp((int)(unsigned)(u >> 32), CTRL, 0xf, 0xf, true);
     return __builtin_bit_cast(double, ((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
 }
 __device__ __forceinline__ double lane_bcast(double v, int l) {

@@ -245,8 +245,9 @@ __global__ __launch_bounds__(64) void recur_kernel(RecurArgs a) {
 template <int CTRL>
 __device__ __forceinline__ double dpp_shift(double v) {   // row_shr:k (0x110 + k) or wave_shr:1 (0x138); lanes without a source get 0
     const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
-    const int lo = __builtin_amdgcn_update_dpp(0, (int)(unsigned)u, CTRL, 0xf, 0xf, false);
-    const int hi = __builtin_amdgcn_update_dpp(0, (int)(unsigned)(u >> 32), CTRL, 0xf, 0xf, false);
+    // bound_ctrl: a lane without a source reads 0, so no old value to zero first (round 6)
+    const int lo = __builtin_amdgcn_mov_dpp((int)(unsigned)u, CTRL, 0xf, 0xf, true);
+    const int hi = __builtin_amdgcn_mov_dpp((int)(unsigned)(u >> 32), CTRL, 0xf, 0xf, true);
     return __builtin_bit_cast(double, ((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
 }
 __device__ __forceinline__ unsigned long long dbits(double v) { return __builtin_bit_cast(unsigned long long, v); }

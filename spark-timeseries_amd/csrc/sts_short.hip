@@ -43,7 +43,8 @@ namespace {
 constexpr int kShortWaves = STS_SHORT_WAVES;
 
 #ifndef STS_SHORT_TRIM
-#define STS_SHORT_TRIM 1   // fewer VALU per series: bounds as masks / a c0-filled tail (round 6)
+#define STS_SHORT_TRIM 2   // fewer VALU per series (round 6): 1 = bounds as masks, a c0-filled tail;
+                           // 2 = + the middle sums under scalar lane masks, scalar-based DMA
 #endif
 
 #ifndef STS_SHORT_DIAG
@@ -51,6 +52,16 @@ constexpr int kShortWaves = STS_SHORT_WAVES;
                            // 3 no per-lag finalize, 4 no robust shift, 5 no lag products;
                            // wrong results
 #endif
+
+// v in the lanes of the wave-uniform mask m, +0.0 elsewhere (v_cndmask on the SGPR pair: no
+// per-lane compare)
+__device__ __forceinline__ double lanes_keep(double v, unsigned long long m) {
+    const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
+    unsigned lo, hi;
+    asm("v_cndmask_b32_e64 %0, 0, %1, %2" : "=v"(lo) : "v"((unsigned)u), "s"(m));
+    asm("v_cndmask_b32_e64 %0, 0, %1, %2" : "=v"(hi) : "v"((unsigned)(u >> 32)), "s"(m));
+    return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
+}
 
 // robust_shift (sts_acf.hpp) from the lanes' validity masks: lane l's sample is the first
 // valid RAW step of [l T / 64, (l + 1) T / 64) -- a range of < B steps, so inside the blocks
@@ -89,13 +100,33 @@ __device__ __forceinline__ unsigned long long short_load(double* buf, const doub
 #pragma unroll
     for (int i = 0; i < B / 2; i++) {
         const int u = 2 * (i * 64 + lane);
-        // past the series end: a copy of its last pair (T even), never read as data
-        glds16(src + (STS_SHORT_TRIM ? (u < T - 2 ? u : T - 2) : (u < T ? u : 0)), lb + i * 1024);
+        if (STS_SHORT_TRIM >= 2 && (i + 1) * 128 <= T)   // a whole piece: scalar base + the lane's 16 B, no VALU
+            glds16_s(src + i * 128, 16u * (unsigned)lane, lb + i * 1024);
+        else   // past the series end: a copy of its last pair (T even), never read as data
+            glds16(src + (STS_SHORT_TRIM ? (u < T - 2 ? u : T - 2) : (u < T ? u : 0)), lb + i * 1024);
     }
     dma_wait();
     wave_lds_sync();
     unsigned long long vm = 0ull;
-    if (STS_SHORT_TRIM) {   // the bound as one mask instead of a test per step
+    if (STS_SHORT_TRIM >= 2) {
+        // bits shifted in from the top step down: acc = 2 acc + (v ordered), one compare and one
+        // add-with-carry per step (the low word holds steps 0..31, the high word 32..B-1)
+        unsigned wlo = 0u, whi = 0u;
+#pragma unroll
+        for (int j = B / 2 - 1; j >= 0; j--) {
+            const double2 v = *reinterpret_cast<const double2*>(buf + t0 + 2 * j);
+            if (2 * j >= 32) {
+                asm volatile("v_cmp_o_f64 vcc, %1, %1\n\tv_addc_co_u32 %0, vcc, %0, %0, vcc" : "+v"(whi) : "v"(v.y) : "vcc");
+                asm volatile("v_cmp_o_f64 vcc, %1, %1\n\tv_addc_co_u32 %0, vcc, %0, %0, vcc" : "+v"(whi) : "v"(v.x) : "vcc");
+            } else {
+                asm volatile("v_cmp_o_f64 vcc, %1, %1\n\tv_addc_co_u32 %0, vcc, %0, %0, vcc" : "+v"(wlo) : "v"(v.y) : "vcc");
+                asm volatile("v_cmp_o_f64 vcc, %1, %1\n\tv_addc_co_u32 %0, vcc, %0, %0, vcc" : "+v"(wlo) : "v"(v.x) : "vcc");
+            }
+        }
+        vm = ((unsigned long long)whi << 32) | wlo;
+        const int n = T - t0;   // steps of this block inside the series
+        vm &= n >= 64 ? ~0ull : n <= 0 ? 0ull : (1ull << n) - 1ull;
+    } else if (STS_SHORT_TRIM) {   // the bound as one mask instead of a test per step
 #pragma unroll
         for (int j = 0; j < B / 2; j++) {
             const double2 v = *reinterpret_cast<const double2*>(buf + t0 + 2 * j);
@@ -275,11 +306,30 @@ __global__ __launch_bounds__(64 * kShortWaves, 2) void short_fill_acf_kernel(Til
     double P[KM + 1];
 #pragma unroll
     for (int d = 0; d <= KM; d++) P[d] = 0.0;
-    double sm = 0.0, qm = 0.0;
+    double sm = 0.0, qm = 0.0, sm2 = 0.0, qm2 = 0.0;
+    // the middle's last step T - kAcfEdge - 1 sits in lane mid_l at offset mid_o: steps j <= mid_o
+    // of lanes <= mid_l are below the tail, steps j > mid_o only of lanes < mid_l (wave-uniform)
+    const int mid_l = (T - kAcfEdge - 1) / B, mid_o = T - kAcfEdge - 1 - mid_l * B;
+    const unsigned long long mid_m1 = mid_l >= 63 ? ~0ull : (2ull << mid_l) - 1ull;
+    const unsigned long long mid_m0 = (1ull << mid_l) - 1ull;
 #pragma unroll
     for (int j = 0; j < B; j++) {
         const double yj = x[j];
-        if (acf_mid(t0 + j, T)) {
+        if (STS_SHORT_TRIM >= 2) {
+            // rule 2's middle [kAcfEdge, T - kAcfEdge) holds step t0 + j for the lanes l in [lo, hi):
+            // a wave-uniform lane mask per j (scalar work), one masked copy of y for both sums, and
+            // two chains (even / odd j) for the latency
+            const int lo = j >= kAcfEdge ? 0 : (kAcfEdge - j + B - 1) / B;   // a constant after unrolling
+            const unsigned long long mm = (j <= mid_o ? mid_m1 : mid_m0) & ~((1ull << lo) - 1ull);
+            const double ym = lanes_keep(yj, mm);
+            if (j & 1) {
+                sm2 += ym;
+                qm2 = __builtin_fma(ym, ym, qm2);
+            } else {
+                sm += ym;
+                qm = __builtin_fma(ym, ym, qm);
+            }
+        } else if (acf_mid(t0 + j, T)) {
             sm += yj;
             qm = __builtin_fma(yj, yj, qm);
         }
@@ -300,6 +350,10 @@ __global__ __launch_bounds__(64 * kShortWaves, 2) void short_fill_acf_kernel(Til
     for (int d = 1; d <= KM; d++) {
         const double v = row_sum_dpp(P[d]);
         if (row_lead) scr[4 * d + row] = v;
+    }
+    if (STS_SHORT_TRIM >= 2) {
+        sm += sm2;
+        qm += qm2;
     }
     {
         const double v0 = row_sum_dpp(sm), v1 = row_sum_dpp(qm);

@@ -123,6 +123,21 @@ case "$SESSION" in
       done
     done
     ;;
+  dpp)
+    # DPP moves without an old value (bound_ctrl): the whole GPU suite, then same-box A/B of the
+    # product against var_head (the previous tree) on the workloads whose kernels use the helpers
+    timeout -k 10 1500 python -u -m pytest -x -q --timeout 300 --timeout-method thread -p no:cacheprovider -m gpu tests > $O/dpp_pytest.log 2>&1 || { tail -40 $O/dpp_pytest.log; exit 1; }
+    tail -1 $O/dpp_pytest.log
+    for rep in 1 2 3; do
+      for w in ${DPP_WL:-c1 c2 c4}; do
+        for L in new ${DPP_LIBS:-head}; do
+          if [ $L = new ]; then E=""; else E="STS_HIP_LIB=spark-timeseries_amd/build/var_$L/libsts_hip.so"; fi
+          env $E timeout -k 10 200 python -u bench.py --workload $w --steps 20 --warmup 5 --cpu-seconds 2 > $O/dpp_${w}_$L.json 2>/dev/null || exit 1
+          python -c "import json; d=json.load(open('$O/dpp_${w}_$L.json')); r=d['roofline']; print(json.dumps({'workload': '$w', 'lib': '$L', 'rep': $rep, 'kernel_ms': r['avg_kernel_ms'], 'frac': r['frac'], 'check': d['cpu_baseline']['sample_check']}))" | tee -a $O/dpp.jsonl
+        done
+      done
+    done
+    ;;
   *)
     echo "unknown session $SESSION"; exit 2 ;;
 esac
