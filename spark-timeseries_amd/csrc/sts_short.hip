@@ -43,8 +43,9 @@ namespace {
 constexpr int kShortWaves = STS_SHORT_WAVES;
 
 #ifndef STS_SHORT_TRIM
-#define STS_SHORT_TRIM 2   // fewer VALU per series (round 6): 1 = bounds as masks, a c0-filled tail;
-                           // 2 = + the middle sums under scalar lane masks, scalar-based DMA
+#define STS_SHORT_TRIM 3   // fewer VALU per series (round 6): 1 = bounds as masks, a c0-filled tail;
+                           // 2 = + the middle sums under scalar lane masks, scalar-based DMA,
+                           // validity bits by add-with-carry; 3 = + the wave sums through LDS rows
 #endif
 
 #ifndef STS_SHORT_DIAG
@@ -344,31 +345,67 @@ __global__ __launch_bounds__(64 * kShortWaves, 2) void short_fill_acf_kernel(Til
     //      (lane d - 1 collects lag d), added in wave_sum_dpp's order ----
     wave_lds_sync();   // every read of the filled block is done: it becomes scratch
     double* scr = buf;
-    const int row = lane >> 4;
-    const bool row_lead = (lane & 15) == 0;
-#pragma unroll
-    for (int d = 1; d <= KM; d++) {
-        const double v = row_sum_dpp(P[d]);
-        if (row_lead) scr[4 * d + row] = v;
-    }
     if (STS_SHORT_TRIM >= 2) {
         sm += sm2;
         qm += qm2;
     }
-    {
-        const double v0 = row_sum_dpp(sm), v1 = row_sum_dpp(qm);
-        if (row_lead) {
-            scr[row] = v0;
-            scr[4 * (KM + 1) + row] = v1;
+    double Pi, Sm, Qm;
+    // the V = KM + 2 quantities (0: sm, d: P_d, KM + 1: qm) of every lane as LDS rows of RS
+    // doubles (RS odd: conflict-free writes), then lane (v, q) sums quantity v over the q-th of
+    // G lane groups and a second pass adds the G partials -- ~V + G adds per lane where the DPP
+    // row sums cost 12 VALU per quantity (round 6)
+    constexpr int V = KM + 2, RS = V | 1, G = 64 / V, LG = (64 + G - 1) / G;
+    if (STS_SHORT_TRIM >= 3 && 64 * RS + G * V <= BUFD) {
+#pragma unroll
+        for (int v = 0; v < V; v++) scr[lane * RS + v] = v == 0 ? sm : v == KM + 1 ? qm : P[v];
+        wave_lds_sync();
+        double* part = scr + 64 * RS;
+        if (lane < G * V) {
+            const int v = lane % V, q = lane / V;
+            const double* col = scr + q * LG * RS + v;
+            double a0 = 0.0, a1 = 0.0;
+#pragma unroll
+            for (int k = 0; k < LG; k += 2) {
+                if (q * LG + k < 64) a0 += col[k * RS];
+                if (k + 1 < LG && q * LG + k + 1 < 64) a1 += col[(k + 1) * RS];
+            }
+            part[q * V + v] = a0 + a1;
         }
+        wave_lds_sync();
+        const int li = (lane < KM) ? lane + 1 : KM;
+        Pi = part[li];
+        Sm = part[0];
+        Qm = part[KM + 1];
+#pragma unroll
+        for (int q = 1; q < G; q++) {
+            Pi += part[q * V + li];
+            Sm += part[q * V];
+            Qm += part[q * V + KM + 1];
+        }
+    } else {
+        const int row = lane >> 4;
+        const bool row_lead = (lane & 15) == 0;
+#pragma unroll
+        for (int d = 1; d <= KM; d++) {
+            const double v = row_sum_dpp(P[d]);
+            if (row_lead) scr[4 * d + row] = v;
+        }
+        {
+            const double v0 = row_sum_dpp(sm), v1 = row_sum_dpp(qm);
+            if (row_lead) {
+                scr[row] = v0;
+                scr[4 * (KM + 1) + row] = v1;
+            }
+        }
+        wave_lds_sync();
+        const int li = (lane < KM) ? lane + 1 : KM;
+        const double4 pr = *reinterpret_cast<const double4*>(scr + 4 * li);
+        Pi = (pr.x + pr.y) + (pr.z + pr.w);
+        const double4 sr = *reinterpret_cast<const double4*>(scr);
+        const double4 qr = *reinterpret_cast<const double4*>(scr + 4 * (KM + 1));
+        Sm = (sr.x + sr.y) + (sr.z + sr.w);
+        Qm = (qr.x + qr.y) + (qr.z + qr.w);
     }
-    wave_lds_sync();
-    const int li = (lane < KM) ? lane + 1 : KM;
-    const double4 pr = *reinterpret_cast<const double4*>(scr + 4 * li);
-    const double Pi = (pr.x + pr.y) + (pr.z + pr.w);
-    const double4 sr = *reinterpret_cast<const double4*>(scr);
-    const double4 qr = *reinterpret_cast<const double4*>(scr + 4 * (KM + 1));
-    const double Sm = (sr.x + sr.y) + (sr.z + sr.w), Qm = (qr.x + qr.y) + (qr.z + qr.w);
     if (STS_SHORT_DIAG == 3) {
         if (lane < K) a.acf_fused[s * K + lane] = Pi + Sm + Qm;
         return;
