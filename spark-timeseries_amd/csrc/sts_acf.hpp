@@ -211,6 +211,30 @@ __device__ __forceinline__ bool acf_suspect(double r, double sum1, double sq1, d
     return e_ours + e_ref > __builtin_fmax(1e-11 * ar, eps * rn);
 }
 
+// The same test at a fraction of its VALU (round 6, the issue-bound short kernel): hardware
+// reciprocal / reciprocal-square-root approximations instead of IEEE divisions and square
+// roots (~40 instead of ~200 instructions).  Their error (far below 1e-6 relative) is covered
+// by the 1.001 factor on the estimate, so this flags every series acf_suspect flags (a
+// superset within 0.1 % of the threshold, which then takes the reference's own loop).
+__device__ __forceinline__ bool acf_suspect_fast(double r, double sum1, double sq1, double sum2, double sq2,
+                                                 double v1, double v2, double N, double c) {
+    if (!(__builtin_isfinite(sum1) && __builtin_isfinite(sq1) && __builtin_isfinite(sum2) && __builtin_isfinite(sq2)))
+        return false;
+    if (!(v1 > 0.0) || !(v2 > 0.0) || !__builtin_isfinite(r)) return true;
+    constexpr double eps = 0x1p-52;
+    const double iv1 = __builtin_amdgcn_rcp(v1), iv2 = __builtin_amdgcn_rcp(v2), iN = __builtin_amdgcn_rcp(N);
+    const double R1 = sq1 * iv1, R2 = sq2 * iv2, ar = __builtin_fabs(r);
+    const double rn = N * __builtin_amdgcn_rsq(N);                      // sqrt(N)
+    const double G = __builtin_fmax(rn * 0.125, 16.0);
+    const double R12 = R1 * R2;
+    const double e_ours = eps * G * (R12 * __builtin_amdgcn_rsq(R12) + ar * 0.5 * (R1 + R2));
+    const double m1 = sq1 * iN, m2 = sq2 * iN;
+    const double d1 = 0x1p-55 * N * (__builtin_fabs(c) + m1 * __builtin_amdgcn_rsq(m1));
+    const double d2 = 0x1p-55 * N * (__builtin_fabs(c) + m2 * __builtin_amdgcn_rsq(m2));
+    const double e_ref = N * d1 * d2 * __builtin_amdgcn_rsq(v1 * v2) + ar * 0.5 * (N * d1 * d1 * iv1 + N * d2 * d2 * iv2);
+    return (e_ours + e_ref) * 1.001 > __builtin_fmax(1e-11 * ar, eps * rn);
+}
+
 // The reference's autocorr of lag i (1 <= i < T) over F (S/UnivariateTimeSeries.scala:71-89,
 // Breeze mean = left-to-right sum / count): means first, then the centred sums, every sum
 // sequential in the reference's order (-ffp-contract=off): the reference's bits.  One lane per

@@ -43,9 +43,10 @@ namespace {
 constexpr int kShortWaves = STS_SHORT_WAVES;
 
 #ifndef STS_SHORT_TRIM
-#define STS_SHORT_TRIM 3   // fewer VALU per series (round 6): 1 = bounds as masks, a c0-filled tail;
+#define STS_SHORT_TRIM 4   // fewer VALU per series (round 6): 1 = bounds as masks, a c0-filled tail;
                            // 2 = + the middle sums under scalar lane masks, scalar-based DMA,
-                           // validity bits by add-with-carry; 3 = + the wave sums through LDS rows
+                           // validity bits by add-with-carry; 3 = + the wave sums through LDS rows;
+                           // 4 = + rule 3's test on hardware reciprocals (acf_suspect_fast)
 #endif
 
 #ifndef STS_SHORT_DIAG
@@ -251,7 +252,8 @@ __device__ __forceinline__ double short_finalize(double Pi, double Sm, double Qm
     const double v2 = sq2 - sum2 * sum2 / N;
     const double cv = Pi - sum1 * sum2 / N;
     const double r = cv / (__builtin_sqrt(v1) * __builtin_sqrt(v2));   // :89
-    suspect = acf_suspect(r, sum1, sq1, sum2, sq2, v1, v2, N, c0);
+    suspect = STS_SHORT_TRIM >= 4 ? acf_suspect_fast(r, sum1, sq1, sum2, sq2, v1, v2, N, c0)
+                                  : acf_suspect(r, sum1, sq1, sum2, sq2, v1, v2, N, c0);
     return r;
 }
 
