@@ -43,10 +43,11 @@ namespace {
 constexpr int kShortWaves = STS_SHORT_WAVES;
 
 #ifndef STS_SHORT_TRIM
-#define STS_SHORT_TRIM 4   // fewer VALU per series (round 6): 1 = bounds as masks, a c0-filled tail;
+#define STS_SHORT_TRIM 5   // fewer VALU per series (round 6): 1 = bounds as masks, a c0-filled tail;
                            // 2 = + the middle sums under scalar lane masks, scalar-based DMA,
                            // validity bits by add-with-carry; 3 = + the wave sums through LDS rows;
-                           // 4 = + rule 3's test on hardware reciprocals (acf_suspect_fast)
+                           // 4 = + rule 3's test on hardware reciprocals (acf_suspect_fast);
+                           // 5 = + the store pass's LDS reads batched
 #endif
 
 #ifndef STS_SHORT_DIAG
@@ -223,6 +224,20 @@ __device__ __forceinline__ bool short_fill(double* buf, unsigned long long vm, i
 // the filled series out of the block: coalesced 1-KB stores
 template <int B>
 __device__ __forceinline__ void short_store(double* dst, const double* buf, int T, int lane) {
+    if (STS_SHORT_TRIM >= 5) {
+        // every piece read first (the block holds 64 B doubles: no bound on the reads), then the
+        // stores: one LDS wait instead of one per store behind its exec-masked branch
+        typedef double d2_t __attribute__((ext_vector_type(2)));
+        d2_t v[B / 2];
+#pragma unroll
+        for (int i = 0; i < B / 2; i++) v[i] = *reinterpret_cast<const d2_t*>(buf + 2 * (i * 64 + lane));
+#pragma unroll
+        for (int i = 0; i < B / 2; i++) {
+            const int u = 2 * (i * 64 + lane);
+            if ((i + 1) * 128 <= T || u < T) __builtin_nontemporal_store(v[i], reinterpret_cast<d2_t*>(dst + u));
+        }
+        return;
+    }
 #pragma unroll
     for (int i = 0; i < B / 2; i++) {
         const int u = 2 * (i * 64 + lane);
