@@ -26,6 +26,7 @@
 // IEEE divisions) per knot per lane; the launcher batches series so the scratch stays bounded.
 #include <hip/hip_runtime.h>
 
+#include "sts_dma.hpp"
 #include "sts_internal.hpp"
 
 namespace {
@@ -146,6 +147,186 @@ __global__ __launch_bounds__(kBlock) void spline_fill_kernel(const double* __res
     }
 }
 
+#ifndef STS_SPLINE_LDS
+#define STS_SPLINE_LDS 1   // round 6: the rows' reads and the (mu, z) scratch through LDS (below)
+#endif
+
+// Round 6: the same two sweeps, the same arithmetic in the same order (bit-identical), with the
+// memory access reorganised.  spline_fill_kernel's lanes read their own rows 8 B at a time --
+// each load instruction touches 64 cache lines, one per lane -- and that, not the FP64 chain,
+// bounded it (16.6 ms for 1 M x 390 against a chain floor below 1 ms).  Here a one-wave
+// workgroup owns 64 series and walks them in chunks of kLc steps: the chunk of all 64 rows
+// arrives by coalesced 16-B loads (4 lanes per row: 16 rows per instruction), is written to an
+// LDS tile [row][kLc + 1], and each lane reads its row from there; the next chunk's loads are in
+// flight meanwhile.  The forward sweep stores knot i's (mu, z) at the step of knot i + 1 (the
+// knot being read when they are formed, so always inside the current chunk) into LDS tiles that
+// leave as coalesced 16-B stores; the backward sweep reads them back the same way and carries
+// them from knot i + 1 to knot i.  The outputs are still written per lane.
+constexpr int kLc = 8;             // steps per chunk
+constexpr int kLp = kLc + 1;       // LDS row pitch in doubles (odd: conflict-free row reads)
+
+__global__ __launch_bounds__(64) void spline_lds_kernel(const double* __restrict__ in, double* __restrict__ out,
+                                                        double2* __restrict__ scratch, int64_t S, int64_t T,
+                                                        int64_t ld_in, int64_t ld_out, int32_t* __restrict__ err) {
+    __shared__ double R[64 * kLp];    // raw chunk
+    __shared__ double MU[64 * kLp];   // scratch chunk: mu ...
+    __shared__ double Z[64 * kLp];    // ... and z
+    const int lane = threadIdx.x;
+    const int64_t s0 = (int64_t)blockIdx.x * 64;
+    const int nrows = (int)(S - s0 < 64 ? S - s0 : 64);
+    const int64_t s = s0 + lane;
+    const bool live = lane < nrows;
+    // coalesced chunk loads: lane L takes row 16 i + L / 4, steps 2 (L % 4) .. + 1 of the chunk
+    const int lr = lane >> 2, lp = (lane & 3) * 2;
+    auto load_raw = [&](int64_t t0, double2 (&v)[4]) {
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const int row = 16 * i + lr;
+            const int64_t t = t0 + lp;
+            if (row < nrows && t < T) {
+                const double* src = in + (s0 + row) * ld_in + t;
+                if (t + 1 < T) v[i] = *reinterpret_cast<const double2*>(src);   // rows 16-B aligned, t even
+                else v[i] = make_double2(src[0], 0.0);
+            } else {
+                v[i] = make_double2(0.0, 0.0);
+            }
+        }
+    };
+    auto put_raw = [&](const double2 (&v)[4]) {
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const int row = 16 * i + lr;
+            R[row * kLp + lp] = v[i].x;
+            R[row * kLp + lp + 1] = v[i].y;
+        }
+    };
+    // scratch chunk moves: lane L takes row 8 i + L / 8, step L % 8
+    const int sr = lane >> 3, sk = lane & 7;
+    auto sc_at = [&](int row, int64_t t) { return scratch + (s0 + row) * T + t; };
+
+    // ---- forward sweep ----
+    int64_t cnt = 0, xa = 0, xb = 0, first = 0;
+    double ya = 0.0, yb = 0.0, mu_prev = 0.0, z_prev = 0.0;
+    double2 nv[4];
+    load_raw(0, nv);
+    for (int64_t t0 = 0; t0 < T; t0 += kLc) {
+        sts::wave_lds_sync();   // the previous chunk's tiles are read / stored
+        put_raw(nv);
+        sts::wave_lds_sync();
+        if (t0 + kLc < T) load_raw(t0 + kLc, nv);   // next chunk in flight
+        bool wrote = false;
+#pragma unroll
+        for (int k = 0; k < kLc; k++) {
+            const double yv = R[lane * kLp + k];
+            const int64_t t = t0 + k;
+            if (!live || t >= T || yv != yv) continue;
+            if (cnt == 0) {
+                first = t;
+                xb = t;
+                yb = yv;
+            } else if (cnt == 1) {
+                MU[lane * kLp + k] = 0.0;   // knot 0's (mu, z) = (0, 0), at knot 1's step
+                Z[lane * kLp + k] = 0.0;
+                wrote = true;
+                xa = xb;
+                ya = yb;
+                xb = t;
+                yb = yv;
+            } else {
+                const double xi1 = (double)t, xi = (double)xb, xim1 = (double)xa;
+                const double hm1 = xi - xim1;
+                const double hi = xi1 - xi;
+                const double span = xi1 - xim1;
+                const double g = 2.0 * span - hm1 * mu_prev;
+                const double mu = hi / g;
+                const double z = (3.0 * (yv * hm1 - yb * span + ya * hi) / (hm1 * hi) - hm1 * z_prev) / g;
+                MU[lane * kLp + k] = mu;   // knot xb's, at step t
+                Z[lane * kLp + k] = z;
+                wrote = true;
+                mu_prev = mu;
+                z_prev = z;
+                xa = xb;
+                ya = yb;
+                xb = t;
+                yb = yv;
+            }
+            cnt++;
+        }
+        if (__ballot(wrote)) {   // the chunk's (mu, z) out (steps without a knot carry stale values, never read)
+            sts::wave_lds_sync();
+#pragma unroll
+            for (int i = 0; i < 8; i++) {
+                const int row = 8 * i + sr;
+                const int64_t t = t0 + sk;
+                if (row < nrows && t < T) *sc_at(row, t) = make_double2(MU[row * kLp + sk], Z[row * kLp + sk]);
+            }
+        }
+    }
+    const bool ok = cnt >= 3;
+    if (live && err) err[s] = ok ? STS_OK : STS_ERR_TOO_FEW_POINTS;
+
+    // ---- backward sweep ----
+    double* o = out + s * ld_out;
+    const int64_t lo = ok ? first : T;
+    const int64_t hi = ok ? xb : T;
+    double c_next = 0.0, y_next = yb, mu_p = 0.0, z_p = 0.0;   // (mu, z) of the knot left of x_next
+    int64_t x_next = hi;
+    const int64_t tlast = ((T - 1) / kLc) * kLc;
+    double2 ns[8];
+    auto load_sc = [&](int64_t t0, double2 (&q)[8]) {
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            const int row = 8 * i + sr;
+            const int64_t t = t0 + sk;
+            q[i] = (row < nrows && t < T) ? *sc_at(row, t) : make_double2(0.0, 0.0);
+        }
+    };
+    load_raw(tlast, nv);
+    load_sc(tlast, ns);
+    for (int64_t t0 = tlast; t0 >= 0; t0 -= kLc) {
+        sts::wave_lds_sync();
+        put_raw(nv);
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            const int row = 8 * i + sr;
+            MU[row * kLp + sk] = ns[i].x;
+            Z[row * kLp + sk] = ns[i].y;
+        }
+        sts::wave_lds_sync();
+        if (t0 > 0) {
+            load_raw(t0 - kLc, nv);
+            load_sc(t0 - kLc, ns);
+        }
+        if (!live) continue;
+#pragma unroll
+        for (int k = kLc - 1; k >= 0; k--) {
+            const int64_t t = t0 + k;
+            if (t >= T) continue;
+            const double yv = R[lane * kLp + k];
+            if (t >= hi || t < lo) {
+                o[t] = yv;
+                if (t == hi) {   // the last knot: its left neighbour's (mu, z)
+                    mu_p = MU[lane * kLp + k];
+                    z_p = Z[lane * kLp + k];
+                }
+                continue;
+            }
+            if (yv != yv) continue;
+            const double c = z_p - mu_p * c_next;
+            const double xt = (double)t;
+            const double h = (double)x_next - xt;
+            const double b = (y_next - yv) / h - h * (c_next + 2.0 * c) / 3.0;
+            const double d = (c_next - c) / (3.0 * h);
+            for (int64_t p = t; p < x_next; p++) o[p] = poly_value(yv, b, c, d, (double)p - xt);
+            c_next = c;
+            y_next = yv;
+            x_next = t;
+            mu_p = MU[lane * kLp + k];
+            z_p = Z[lane * kLp + k];
+        }
+    }
+}
+
 }  // namespace
 
 namespace sts {
@@ -161,9 +342,15 @@ hipError_t launch_spline(const double* in, double* out, int64_t S, int64_t T, in
     if (S <= 0 || T <= 0) return hipSuccess;
     for (int64_t s0 = 0; s0 < S; s0 += batch) {
         const int64_t n = S - s0 < batch ? S - s0 : batch;
-        dim3 g((unsigned)((n + kBlock - 1) / kBlock)), b(kBlock);
-        hipLaunchKernelGGL(spline_fill_kernel, g, b, 0, st, in + s0 * ld_in, out + s0 * ld_out,
-                           reinterpret_cast<double2*>(scratch), n, T, ld_in, ld_out, err ? err + s0 : nullptr);
+        if (STS_SPLINE_LDS && !(ld_in & 1) && !(reinterpret_cast<uintptr_t>(in) & 15)) {   // 16-B row pieces
+            dim3 g((unsigned)((n + 63) / 64)), b(64);
+            hipLaunchKernelGGL(spline_lds_kernel, g, b, 0, st, in + s0 * ld_in, out + s0 * ld_out,
+                               reinterpret_cast<double2*>(scratch), n, T, ld_in, ld_out, err ? err + s0 : nullptr);
+        } else {
+            dim3 g((unsigned)((n + kBlock - 1) / kBlock)), b(kBlock);
+            hipLaunchKernelGGL(spline_fill_kernel, g, b, 0, st, in + s0 * ld_in, out + s0 * ld_out,
+                               reinterpret_cast<double2*>(scratch), n, T, ld_in, ld_out, err ? err + s0 : nullptr);
+        }
         const hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }

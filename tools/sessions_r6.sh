@@ -138,6 +138,20 @@ case "$SESSION" in
       done
     done
     ;;
+  splds)
+    # fill("spline") with the rows and the (mu, z) scratch through LDS (STS_SPLINE_LDS, product) against
+    # var_splold (-DSTS_SPLINE_LDS=0); the spline tests first
+    timeout -k 10 900 $PYT tests/test_spline.py tests/test_fuzz_gpu.py tests/test_parity_gpu.py -k "spline or unsupported or fill_diff_ewma" > $O/splds_pytest.log 2>&1 || { tail -40 $O/splds_pytest.log; exit 1; }
+    tail -1 $O/splds_pytest.log
+    V=spark-timeseries_amd/build/var_splold/libsts_hip.so
+    for rep in 1 2 3; do
+      for L in lds old; do
+        if [ $L = old ]; then E="STS_HIP_LIB=$V"; else E=""; fi
+        env $E timeout -k 10 300 python -u bench.py --workload spline --steps 5 --warmup 2 --cpu-seconds 2 > $O/splds_$L.json 2>/dev/null || exit 1
+        python -c "import json; d=json.load(open('$O/splds_$L.json')); r=d['roofline']; print(json.dumps({'lib': '$L', 'rep': $rep, 'ms_per_step': d['ms_per_step'], 'kernel_ms': r['avg_kernel_ms'], 'frac': r['frac'], 'check': d['cpu_baseline']['sample_check']}))" | tee -a $O/splds.jsonl
+      done
+    done
+    ;;
   *)
     echo "unknown session $SESSION"; exit 2 ;;
 esac
