@@ -168,7 +168,8 @@ constexpr int kLp = kLc + 1;       // LDS row pitch in doubles (odd: conflict-fr
 __global__ __launch_bounds__(64) void spline_lds_kernel(const double* __restrict__ in, double* __restrict__ out,
                                                         double2* __restrict__ scratch, int64_t S, int64_t T,
                                                         int64_t ld_in, int64_t ld_out, int32_t* __restrict__ err) {
-    __shared__ double R[64 * kLp];    // raw chunk
+    __shared__ double RB[2 * 64 * kLp];   // raw chunk tiles (the backward sweep's outputs in place)
+    double* const R = RB;
     __shared__ double MU[64 * kLp];   // scratch chunk: mu ...
     __shared__ double Z[64 * kLp];    // ... and z
     const int lane = threadIdx.x;
@@ -204,88 +205,103 @@ __global__ __launch_bounds__(64) void spline_lds_kernel(const double* __restrict
     const int sr = lane >> 3, sk = lane & 7;
     auto sc_at = [&](int row, int64_t t) { return scratch + (s0 + row) * T + t; };
 
-    // ---- forward sweep ----
-    int64_t cnt = 0, xa = 0, xb = 0, first = 0;
+    // ---- forward sweep: per step straight-line code (32-bit step indices, selects instead of
+    //      branches; a lane forms (mu, z) at every step and keeps them only at its knots) ----
+    const int Ti = (int)T;
+    int cnt = 0, xa = 0, xb = 0, first = 0;
     double ya = 0.0, yb = 0.0, mu_prev = 0.0, z_prev = 0.0;
     double2 nv[4];
     load_raw(0, nv);
-    for (int64_t t0 = 0; t0 < T; t0 += kLc) {
+    for (int t0 = 0; t0 < Ti; t0 += kLc) {
         sts::wave_lds_sync();   // the previous chunk's tiles are read / stored
         put_raw(nv);
         sts::wave_lds_sync();
-        if (t0 + kLc < T) load_raw(t0 + kLc, nv);   // next chunk in flight
-        bool wrote = false;
+        if (t0 + kLc < Ti) load_raw(t0 + kLc, nv);   // next chunk in flight
 #pragma unroll
         for (int k = 0; k < kLc; k++) {
             const double yv = R[lane * kLp + k];
-            const int64_t t = t0 + k;
-            if (!live || t >= T || yv != yv) continue;
-            if (cnt == 0) {
-                first = t;
+            const int t = t0 + k;
+            const bool knot = live && t < Ti && yv == yv;
+            const double xi1 = (double)t, xi = (double)xb, xim1 = (double)xa;
+            const double hm1 = xi - xim1;
+            const double hi = xi1 - xi;
+            const double span = xi1 - xim1;
+            const double g = 2.0 * span - hm1 * mu_prev;
+            const double mu = hi / g;
+            const double z = (3.0 * (yv * hm1 - yb * span + ya * hi) / (hm1 * hi) - hm1 * z_prev) / g;
+            // knot 1 stores knot 0's (0, 0), knot i + 1 knot i's (mu, z); other steps' slots are never read
+            const bool full = cnt >= 2;
+            MU[lane * kLp + k] = full ? mu : 0.0;
+            Z[lane * kLp + k] = full ? z : 0.0;
+            if (knot) {
+                if (full) {
+                    mu_prev = mu;
+                    z_prev = z;
+                }
+                if (cnt == 0) first = t;
+                if (cnt >= 1) {
+                    xa = xb;
+                    ya = yb;
+                }
                 xb = t;
                 yb = yv;
-            } else if (cnt == 1) {
-                MU[lane * kLp + k] = 0.0;   // knot 0's (mu, z) = (0, 0), at knot 1's step
-                Z[lane * kLp + k] = 0.0;
-                wrote = true;
-                xa = xb;
-                ya = yb;
-                xb = t;
-                yb = yv;
-            } else {
-                const double xi1 = (double)t, xi = (double)xb, xim1 = (double)xa;
-                const double hm1 = xi - xim1;
-                const double hi = xi1 - xi;
-                const double span = xi1 - xim1;
-                const double g = 2.0 * span - hm1 * mu_prev;
-                const double mu = hi / g;
-                const double z = (3.0 * (yv * hm1 - yb * span + ya * hi) / (hm1 * hi) - hm1 * z_prev) / g;
-                MU[lane * kLp + k] = mu;   // knot xb's, at step t
-                Z[lane * kLp + k] = z;
-                wrote = true;
-                mu_prev = mu;
-                z_prev = z;
-                xa = xb;
-                ya = yb;
-                xb = t;
-                yb = yv;
+                cnt++;
             }
-            cnt++;
         }
-        if (__ballot(wrote)) {   // the chunk's (mu, z) out (steps without a knot carry stale values, never read)
-            sts::wave_lds_sync();
+        sts::wave_lds_sync();   // the chunk's (mu, z) out
 #pragma unroll
-            for (int i = 0; i < 8; i++) {
-                const int row = 8 * i + sr;
-                const int64_t t = t0 + sk;
-                if (row < nrows && t < T) *sc_at(row, t) = make_double2(MU[row * kLp + sk], Z[row * kLp + sk]);
-            }
+        for (int i = 0; i < 8; i++) {
+            const int row = 8 * i + sr;
+            const int t = t0 + sk;
+            if (row < nrows && t < Ti) *sc_at(row, t) = make_double2(MU[row * kLp + sk], Z[row * kLp + sk]);
         }
     }
     const bool ok = cnt >= 3;
     if (live && err) err[s] = ok ? STS_OK : STS_ERR_TOO_FEW_POINTS;
 
-    // ---- backward sweep ----
+    // ---- backward sweep.  The outputs go into the raw tile in place (a step's raw value is read
+    //      before its output is written) and leave as coalesced 16-B stores one chunk late, so a
+    //      knot's gap steps in the chunk to its right still land in LDS; gap steps further right
+    //      (gaps longer than a chunk) are stored directly, after the earlier stores completed ----
     double* o = out + s * ld_out;
-    const int64_t lo = ok ? first : T;
-    const int64_t hi = ok ? xb : T;
+    const int lo = ok ? first : Ti;
+    const int hi = ok ? xb : Ti;
     double c_next = 0.0, y_next = yb, mu_p = 0.0, z_p = 0.0;   // (mu, z) of the knot left of x_next
-    int64_t x_next = hi;
-    const int64_t tlast = ((T - 1) / kLc) * kLc;
+    int x_next = hi;
+    const int tlast = ((Ti - 1) / kLc) * kLc;
     double2 ns[8];
-    auto load_sc = [&](int64_t t0, double2 (&q)[8]) {
+    auto load_sc = [&](int t0, double2 (&q)[8]) {
 #pragma unroll
         for (int i = 0; i < 8; i++) {
             const int row = 8 * i + sr;
-            const int64_t t = t0 + sk;
-            q[i] = (row < nrows && t < T) ? *sc_at(row, t) : make_double2(0.0, 0.0);
+            const int t = t0 + sk;
+            q[i] = (row < nrows && t < Ti) ? *sc_at(row, t) : make_double2(0.0, 0.0);
+        }
+    };
+    auto flush = [&](int tc, const double* tile) {   // chunk [tc, tc + kLc) of the 64 rows out
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const int row = 16 * i + lr;
+            const int t = tc + lp;
+            if (row < nrows && t < Ti) {
+                double* dst = out + (s0 + row) * ld_out + t;
+                if (t + 1 < Ti) *reinterpret_cast<double2*>(dst) = make_double2(tile[row * kLp + lp], tile[row * kLp + lp + 1]);
+                else dst[0] = tile[row * kLp + lp];
+            }
         }
     };
     load_raw(tlast, nv);
     load_sc(tlast, ns);
-    for (int64_t t0 = tlast; t0 >= 0; t0 -= kLc) {
+    for (int t0 = tlast; t0 >= 0; t0 -= kLc) {
+        double* Rc = RB + ((t0 / kLc) & 1) * (64 * kLp);         // this chunk's tile
+        double* Rr = RB + (((t0 / kLc) & 1) ^ 1) * (64 * kLp);   // the chunk to its right (not yet out)
         sts::wave_lds_sync();
-        put_raw(nv);
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const int row = 16 * i + lr;
+            Rc[row * kLp + lp] = nv[i].x;
+            Rc[row * kLp + lp + 1] = nv[i].y;
+        }
 #pragma unroll
         for (int i = 0; i < 8; i++) {
             const int row = 8 * i + sr;
@@ -297,34 +313,50 @@ __global__ __launch_bounds__(64) void spline_lds_kernel(const double* __restrict
             load_raw(t0 - kLc, nv);
             load_sc(t0 - kLc, ns);
         }
-        if (!live) continue;
 #pragma unroll
         for (int k = kLc - 1; k >= 0; k--) {
-            const int64_t t = t0 + k;
-            if (t >= T) continue;
-            const double yv = R[lane * kLp + k];
-            if (t >= hi || t < lo) {
-                o[t] = yv;
-                if (t == hi) {   // the last knot: its left neighbour's (mu, z)
-                    mu_p = MU[lane * kLp + k];
-                    z_p = Z[lane * kLp + k];
-                }
-                continue;
-            }
-            if (yv != yv) continue;
+            const int t = t0 + k;
+            const double yv = Rc[lane * kLp + k];
+            const double mu_here = MU[lane * kLp + k], z_here = Z[lane * kLp + k];
+            const bool in_t = live && t < Ti;
+            const bool raw = t >= hi || t < lo;                       // keeps its raw value
+            const bool knot = in_t && !raw && yv == yv;
             const double c = z_p - mu_p * c_next;
             const double xt = (double)t;
             const double h = (double)x_next - xt;
             const double b = (y_next - yv) / h - h * (c_next + 2.0 * c) / 3.0;
             const double d = (c_next - c) / (3.0 * h);
-            for (int64_t p = t; p < x_next; p++) o[p] = poly_value(yv, b, c, d, (double)p - xt);
-            c_next = c;
-            y_next = yv;
-            x_next = t;
-            mu_p = MU[lane * kLp + k];
-            z_p = Z[lane * kLp + k];
+            // PolynomialFunction({yv, b, c, d}).value(arg): Horner over the untrimmed coefficients
+            // equals the trimmed form (a zero leading coefficient contributes +0.0 exactly), except
+            // all-zero b, c, d, where the trimmed form returns yv itself (its sign of zero)
+            const bool deg0 = b == 0.0 && c == 0.0 && d == 0.0;
+            if (knot) Rc[lane * kLp + k] = deg0 ? yv : ((0.0 * d + c) * 0.0 + b) * 0.0 + yv;
+            if (in_t && t == hi) {   // the last knot: its left neighbour's (mu, z)
+                mu_p = mu_here;
+                z_p = z_here;
+            }
+            if (knot) {
+                // a gap past the right chunk: those chunks are out already -- wait for their stores
+                // before storing over them (once per such knot)
+                if (x_next > t0 + 2 * kLc) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                for (int p = t + 1; p < x_next; p++) {   // the NaN steps up to the next knot
+                    const double arg = (double)p - xt;
+                    const double v = deg0 ? yv : ((arg * d + c) * arg + b) * arg + yv;
+                    if (p < t0 + kLc) Rc[lane * kLp + (p - t0)] = v;
+                    else if (p < t0 + 2 * kLc) Rr[lane * kLp + (p - t0 - kLc)] = v;
+                    else o[p] = v;
+                }
+                c_next = c;
+                y_next = yv;
+                x_next = t;
+                mu_p = mu_here;
+                z_p = z_here;
+            }
         }
+        sts::wave_lds_sync();
+        if (t0 + kLc < Ti) flush(t0 + kLc, Rr);   // the right chunk is final now
     }
+    flush(0, RB);
 }
 
 }  // namespace
@@ -342,7 +374,8 @@ hipError_t launch_spline(const double* in, double* out, int64_t S, int64_t T, in
     if (S <= 0 || T <= 0) return hipSuccess;
     for (int64_t s0 = 0; s0 < S; s0 += batch) {
         const int64_t n = S - s0 < batch ? S - s0 : batch;
-        if (STS_SPLINE_LDS && !(ld_in & 1) && !(reinterpret_cast<uintptr_t>(in) & 15)) {   // 16-B row pieces
+        if (STS_SPLINE_LDS && !(ld_in & 1) && !(ld_out & 1) && !(reinterpret_cast<uintptr_t>(in) & 15) &&
+            !(reinterpret_cast<uintptr_t>(out) & 15) && T < (int64_t(1) << 30)) {   // 16-B row pieces, 32-bit steps
             dim3 g((unsigned)((n + 63) / 64)), b(64);
             hipLaunchKernelGGL(spline_lds_kernel, g, b, 0, st, in + s0 * ld_in, out + s0 * ld_out,
                                reinterpret_cast<double2*>(scratch), n, T, ld_in, ld_out, err ? err + s0 : nullptr);

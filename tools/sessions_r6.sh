@@ -152,6 +152,28 @@ case "$SESSION" in
       done
     done
     ;;
+  splsq)
+    # SQ counters of the spline kernel (one pass of 8 SQ counters)
+    export TMPDIR=/tmp
+    timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVE_CYCLES SQ_WAIT_ANY GRBM_GUI_ACTIVE \
+        -d $O/splsq_1 -o run --output-format csv -- python -u bench.py --workload spline --steps 1 --warmup 0 --no-cpu-baseline > $O/splsq_1.out 2>&1 || { tail -5 $O/splsq_1.out; exit 1; }
+    timeout -s KILL 120 rocprofv3 --pmc SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_WAIT_INST_ANY SQ_INST_CYCLES_VMEM SQ_BUSY_CYCLES SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_ADD_F64 GRBM_GUI_ACTIVE \
+        -d $O/splsq_2 -o run --output-format csv -- python -u bench.py --workload spline --steps 1 --warmup 0 --no-cpu-baseline > $O/splsq_2.out 2>&1 || { tail -5 $O/splsq_2.out; exit 1; }
+    python - <<'PY'
+import csv, glob, collections, json
+d = collections.defaultdict(list)
+for f in glob.glob("gpurun_out/r6/splsq_*/**/*counter_collection.csv", recursive=True):
+    per = collections.defaultdict(dict)
+    for r in csv.DictReader(open(f)):
+        if "spline" not in r["Kernel_Name"]:
+            continue
+        k = int(r["Dispatch_Id"]); per[k][r["Counter_Name"]] = per[k].get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+    for c in per.values():
+        for k, v in c.items():
+            d[k].append(v)
+print(json.dumps({k: sum(v) / len(v) for k, v in sorted(d.items())}, indent=1))
+PY
+    ;;
   *)
     echo "unknown session $SESSION"; exit 2 ;;
 esac
