@@ -162,7 +162,14 @@ __global__ __launch_bounds__(kBlock) void spline_fill_kernel(const double* __res
 // knot being read when they are formed, so always inside the current chunk) into LDS tiles that
 // leave as coalesced 16-B stores; the backward sweep reads them back the same way and carries
 // them from knot i + 1 to knot i.  The outputs are still written per lane.
-constexpr int kLc = 8;             // steps per chunk
+#ifndef STS_SPLINE_LC
+#define STS_SPLINE_LC 8   // 8: 190 VGPRs, 18 KB of LDS, 8 waves per CU; 4 (122 VGPRs, 10 KB, 16 waves) measured slower
+#endif
+constexpr int kLc = STS_SPLINE_LC;  // steps per chunk (4 or 8)
+constexpr int kRl = kLc / 2;        // lanes per row in a raw chunk move (16 B each)
+constexpr int kRi = kRl;            // raw move instructions per chunk (64 / kRl rows each)
+constexpr int kSi = kLc;            // scratch move instructions per chunk (kLc lanes per row, 64 / kLc rows each)
+static_assert(kLc == 4 || kLc == 8, "chunk");
 constexpr int kLp = kLc + 1;       // LDS row pitch in doubles (odd: conflict-free row reads)
 
 __global__ __launch_bounds__(64) void spline_lds_kernel(const double* __restrict__ in, double* __restrict__ out,
@@ -178,11 +185,11 @@ __global__ __launch_bounds__(64) void spline_lds_kernel(const double* __restrict
     const int64_t s = s0 + lane;
     const bool live = lane < nrows;
     // coalesced chunk loads: lane L takes row 16 i + L / 4, steps 2 (L % 4) .. + 1 of the chunk
-    const int lr = lane >> 2, lp = (lane & 3) * 2;
-    auto load_raw = [&](int64_t t0, double2 (&v)[4]) {
+    const int lr = lane / kRl, lp = (lane % kRl) * 2;
+    auto load_raw = [&](int64_t t0, double2 (&v)[kRi]) {
 #pragma unroll
-        for (int i = 0; i < 4; i++) {
-            const int row = 16 * i + lr;
+        for (int i = 0; i < kRi; i++) {
+            const int row = (64 / kRl) * i + lr;
             const int64_t t = t0 + lp;
             if (row < nrows && t < T) {
                 const double* src = in + (s0 + row) * ld_in + t;
@@ -193,16 +200,16 @@ __global__ __launch_bounds__(64) void spline_lds_kernel(const double* __restrict
             }
         }
     };
-    auto put_raw = [&](const double2 (&v)[4]) {
+    auto put_raw = [&](const double2 (&v)[kRi]) {
 #pragma unroll
-        for (int i = 0; i < 4; i++) {
-            const int row = 16 * i + lr;
+        for (int i = 0; i < kRi; i++) {
+            const int row = (64 / kRl) * i + lr;
             R[row * kLp + lp] = v[i].x;
             R[row * kLp + lp + 1] = v[i].y;
         }
     };
     // scratch chunk moves: lane L takes row 8 i + L / 8, step L % 8
-    const int sr = lane >> 3, sk = lane & 7;
+    const int sr = lane / kLc, sk = lane % kLc;
     auto sc_at = [&](int row, int64_t t) { return scratch + (s0 + row) * T + t; };
 
     // ---- forward sweep: per step straight-line code (32-bit step indices, selects instead of
@@ -210,7 +217,7 @@ __global__ __launch_bounds__(64) void spline_lds_kernel(const double* __restrict
     const int Ti = (int)T;
     int cnt = 0, xa = 0, xb = 0, first = 0;
     double ya = 0.0, yb = 0.0, mu_prev = 0.0, z_prev = 0.0;
-    double2 nv[4];
+    double2 nv[kRi];
     load_raw(0, nv);
     for (int t0 = 0; t0 < Ti; t0 += kLc) {
         sts::wave_lds_sync();   // the previous chunk's tiles are read / stored
@@ -250,8 +257,8 @@ __global__ __launch_bounds__(64) void spline_lds_kernel(const double* __restrict
         }
         sts::wave_lds_sync();   // the chunk's (mu, z) out
 #pragma unroll
-        for (int i = 0; i < 8; i++) {
-            const int row = 8 * i + sr;
+        for (int i = 0; i < kSi; i++) {
+            const int row = (64 / kLc) * i + sr;
             const int t = t0 + sk;
             if (row < nrows && t < Ti) *sc_at(row, t) = make_double2(MU[row * kLp + sk], Z[row * kLp + sk]);
         }
@@ -269,19 +276,19 @@ __global__ __launch_bounds__(64) void spline_lds_kernel(const double* __restrict
     double c_next = 0.0, y_next = yb, mu_p = 0.0, z_p = 0.0;   // (mu, z) of the knot left of x_next
     int x_next = hi;
     const int tlast = ((Ti - 1) / kLc) * kLc;
-    double2 ns[8];
-    auto load_sc = [&](int t0, double2 (&q)[8]) {
+    double2 ns[kSi];
+    auto load_sc = [&](int t0, double2 (&q)[kSi]) {
 #pragma unroll
-        for (int i = 0; i < 8; i++) {
-            const int row = 8 * i + sr;
+        for (int i = 0; i < kSi; i++) {
+            const int row = (64 / kLc) * i + sr;
             const int t = t0 + sk;
             q[i] = (row < nrows && t < Ti) ? *sc_at(row, t) : make_double2(0.0, 0.0);
         }
     };
     auto flush = [&](int tc, const double* tile) {   // chunk [tc, tc + kLc) of the 64 rows out
 #pragma unroll
-        for (int i = 0; i < 4; i++) {
-            const int row = 16 * i + lr;
+        for (int i = 0; i < kRi; i++) {
+            const int row = (64 / kRl) * i + lr;
             const int t = tc + lp;
             if (row < nrows && t < Ti) {
                 double* dst = out + (s0 + row) * ld_out + t;
@@ -297,14 +304,14 @@ __global__ __launch_bounds__(64) void spline_lds_kernel(const double* __restrict
         double* Rr = RB + (((t0 / kLc) & 1) ^ 1) * (64 * kLp);   // the chunk to its right (not yet out)
         sts::wave_lds_sync();
 #pragma unroll
-        for (int i = 0; i < 4; i++) {
-            const int row = 16 * i + lr;
+        for (int i = 0; i < kRi; i++) {
+            const int row = (64 / kRl) * i + lr;
             Rc[row * kLp + lp] = nv[i].x;
             Rc[row * kLp + lp + 1] = nv[i].y;
         }
 #pragma unroll
-        for (int i = 0; i < 8; i++) {
-            const int row = 8 * i + sr;
+        for (int i = 0; i < kSi; i++) {
+            const int row = (64 / kLc) * i + sr;
             MU[row * kLp + sk] = ns[i].x;
             Z[row * kLp + sk] = ns[i].y;
         }
