@@ -174,6 +174,16 @@ for f in glob.glob("gpurun_out/r6/splsq_*/**/*counter_collection.csv", recursive
 print(json.dumps({k: sum(v) / len(v) for k, v in sorted(d.items())}, indent=1))
 PY
     ;;
+  overlap)
+    # the fill's HBM stream and the lag products' FP64 MFMAs from different waves: alone and together
+    timeout -k 10 120 ./tools/ubench_overlap 8 4 12288 2048 > $O/overlap.jsonl && cat $O/overlap.jsonl
+    timeout -k 10 120 ./tools/ubench_overlap 8 4 12288 512 > $O/overlap_fewB.jsonl && cat $O/overlap_fewB.jsonl
+    ;;
+  overlap2)
+    # the C3 proportions: an HBM stream of ~20 ms beside MFMA work of ~15-20 ms, MFMA from 2 / 4 waves per SIMD
+    timeout -k 10 200 ./tools/ubench_overlap 8 8 49152 512 > $O/overlap2_w2.jsonl && cat $O/overlap2_w2.jsonl
+    timeout -k 10 200 ./tools/ubench_overlap 8 8 24576 1024 > $O/overlap2_w4.jsonl && cat $O/overlap2_w4.jsonl
+    ;;
   *)
     echo "unknown session $SESSION"; exit 2 ;;
 esac
