@@ -256,12 +256,13 @@ def main():
     if args.workload == "nan_instants":  # flag pass reads everything; the gather reads + writes kept values
         bytes_per_step = 8.0 * S * T + 16.0 * S * n_keep
     kernel = {"c3": "sts::tile_kernel<4096,4,shifted> (fill linear + ACF partials, FP64 MFMA)",
-              "c1_rule3": "sts::short_fill_acf_kernel<40,20> with rule 3 firing on every series (acf_exact_lag per lag)",
+              "c1_rule3": "sts::short_fill_acf_kernel<40,20> with rule 3 firing on every series (the reference's two-pass loop per lag, streamed through the LDS block: acf_exact_stream)",
               "c3_rule3": "sts::tile_kernel<4096,4,shifted> + acf_finalize_kernel with rule 3 firing on every series",
-              "c1": "sts::short_fill_acf_kernel<40,20> (one wave per series in one-wave workgroups: series in by LDS-DMA, linear fill run by run in LDS, lag products as register FMAs, fused ACF finalize)",
+              "c1": "sts::short_fill_acf_kernel<40,20> (one wave per series in one-wave workgroups: series in by LDS-DMA, linear fill run by run in LDS, lag products as register FMAs, wave sums through LDS rows, fused ACF finalize; issue-bound, so trimmed to ~2 400 VALU per series)",
               "c5": "sts::tile_kernel<4096,0> (fill nearest + lag-matrix columns)",
-              "spline": "sts::spline_fill_kernel (one lane per series: the natural spline's forward / backward "
-                        "sweeps in the reference's order, (mu, z) scratch rows, Horner evaluation)",
+              "spline": "sts::spline_lds_kernel (one lane per series: the natural spline's forward / backward "
+                        "sweeps in the reference's order; rows, (mu, z) scratch and outputs moved through LDS tiles "
+                        "as coalesced 16-B pieces, Horner evaluation)",
               "c2": "sts::recur_row_kernel<kFillDiffEwma,1,14,io,32> (fillPrevious -> differencesAtLag(1) -> EWMA add; whole rows through LDS, 32 lanes per series, bit-exact verified affine-scan EWMA)",
               "stage_c2": "sts::recur_row_kernel<kFillDiffEwma,1,14,io,32> (fillPrevious -> differencesAtLag(1) -> EWMA add; whole rows through LDS, 32 lanes per series)",
               "c4_levels": "sts::ar_fit_blk_kernel<5,40,4,dma> + sts::ar_qr_lane_kernel<5,true> (every series flagged: the reference's Householder-QR order, one series per lane, reflections replayed per row)",
