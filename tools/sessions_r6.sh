@@ -184,6 +184,12 @@ PY
     timeout -k 10 200 ./tools/ubench_overlap 8 8 49152 512 > $O/overlap2_w2.jsonl && cat $O/overlap2_w2.jsonl
     timeout -k 10 200 ./tools/ubench_overlap 8 8 24576 1024 > $O/overlap2_w4.jsonl && cat $O/overlap2_w4.jsonl
     ;;
+  overlap3)
+    # the same with the MFMA waves' shader clock recorded (s_memtime against the 100-MHz wall clock)
+    timeout -k 10 200 ./tools/ubench_overlap 8 8 49152 512 > $O/overlap3_w2.jsonl && cat $O/overlap3_w2.jsonl
+    timeout -k 10 200 ./tools/ubench_overlap 8 8 24576 1024 > $O/overlap3_w4.jsonl && cat $O/overlap3_w4.jsonl
+    timeout -k 10 200 ./tools/ubench_overlap 8 8 12288 2048 > $O/overlap3_w8.jsonl && cat $O/overlap3_w8.jsonl
+    ;;
   *)
     echo "unknown session $SESSION"; exit 2 ;;
 esac
