@@ -190,6 +190,11 @@ PY
     timeout -k 10 200 ./tools/ubench_overlap 8 8 24576 1024 > $O/overlap3_w4.jsonl && cat $O/overlap3_w4.jsonl
     timeout -k 10 200 ./tools/ubench_overlap 8 8 12288 2048 > $O/overlap3_w8.jsonl && cat $O/overlap3_w8.jsonl
     ;;
+  overlap4)
+    # launch order swapped (the copy's waves resident first), and a lighter MFMA load
+    timeout -k 10 200 ./tools/ubench_overlap 8 8 49152 512 1 > $O/overlap4_w2_copyfirst.jsonl && cat $O/overlap4_w2_copyfirst.jsonl
+    timeout -k 10 200 ./tools/ubench_overlap 8 8 12288 512 1 > $O/overlap4_w2_light_copyfirst.jsonl && cat $O/overlap4_w2_light_copyfirst.jsonl
+    ;;
   *)
     echo "unknown session $SESSION"; exit 2 ;;
 esac

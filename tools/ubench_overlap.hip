@@ -72,6 +72,7 @@ int main(int argc, char** argv) {
     const int copies = argc > 2 ? atoi(argv[2]) : 4;            // copy passes per launch set
     const int iters = argc > 3 ? atoi(argv[3]) : 4096;          // MFMA groups of 4 per wave
     const int blocksB = argc > 4 ? atoi(argv[4]) : 256 * 8;     // MFMA workgroups (4 waves each)
+    const int copy_first = argc > 5 ? atoi(argv[5]) : 0;        // together: launch order
     const long n = bytes / 16;
     d2 *in, *out;
     double* sink;
@@ -122,8 +123,13 @@ int main(int argc, char** argv) {
         CK(hipDeviceSynchronize());
         CK(hipEventRecord(e0, sb));
         CK(hipStreamWaitEvent(sa, e0, 0));
-        runB(sb);
-        runA(sa);
+        if (copy_first) {
+            runA(sa);
+            runB(sb);
+        } else {
+            runB(sb);
+            runA(sa);
+        }
         CK(hipEventRecord(ea, sa));
         CK(hipEventRecord(eb, sb));
         CK(hipEventSynchronize(ea));
