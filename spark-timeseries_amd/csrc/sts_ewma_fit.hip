@@ -73,7 +73,7 @@ template <int SPW, int CH, bool FIT>
 __global__ __launch_bounds__(64) void ewma_fit_kernel(EwmaFitArgs a) {
     constexpr int kRow = CH + 1;
     constexpr int NLD = SPW * CH / 64;
-    static_assert(SPW * CH % 64 == 0 && CH % 64 == 0, "chunk shape");
+    static_assert(SPW * CH % 64 == 0 && 64 % (64 * 64 / (SPW * CH) > 0 ? 1 : 1) == 0 && (CH % 64 == 0 || 64 % CH == 0), "chunk shape");
     __shared__ double tile[SPW * kRow];
     const int lane = threadIdx.x;
     const int64_t s0 = (int64_t)blockIdx.x * SPW;
@@ -155,8 +155,14 @@ __global__ __launch_bounds__(64) void ewma_fit_kernel(EwmaFitArgs a) {
     }
 }
 
-constexpr int kFitSpw = 32;
-constexpr int kFitCh = 64;
+#ifndef STS_EWMA_SPW
+#define STS_EWMA_SPW 32   // series per wave (lanes that run the pass)
+#endif
+#ifndef STS_EWMA_CH
+#define STS_EWMA_CH 64    // steps per LDS chunk
+#endif
+constexpr int kFitSpw = STS_EWMA_SPW;
+constexpr int kFitCh = STS_EWMA_CH;
 
 #ifdef STS_AB
 // A/B: the wave's SPW rows held in LDS for the whole fit (one load, every

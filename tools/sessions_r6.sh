@@ -195,6 +195,20 @@ PY
     timeout -k 10 200 ./tools/ubench_overlap 8 8 49152 512 1 > $O/overlap4_w2_copyfirst.jsonl && cat $O/overlap4_w2_copyfirst.jsonl
     timeout -k 10 200 ./tools/ubench_overlap 8 8 12288 512 1 > $O/overlap4_w2_light_copyfirst.jsonl && cat $O/overlap4_w2_light_copyfirst.jsonl
     ;;
+  ew)
+    # EWMA.fitModel with 64 series per wave in 32-step chunks (var_ew6432) against the product's 32 x 64;
+    # the EWMA parity first, on the variant
+    V=spark-timeseries_amd/build/var_ew6432/libsts_hip.so
+    timeout -k 10 900 $PYT --sts-lib $V tests/test_parity_gpu.py tests/test_fuzz_gpu.py tests/test_ewma_state_machine.py -k "ewma or EWMA" > $O/ew_pytest.log 2>&1 || { tail -40 $O/ew_pytest.log; exit 1; }
+    tail -1 $O/ew_pytest.log
+    for rep in 1 2 3; do
+      for L in prod ew6432; do
+        if [ $L = prod ]; then E=""; else E="STS_HIP_LIB=$V"; fi
+        env $E timeout -k 10 200 python -u bench.py --workload ewma_fit --steps 5 --warmup 2 --cpu-seconds 2 > $O/ew_$L.json 2>/dev/null || exit 1
+        python -c "import json; d=json.load(open('$O/ew_$L.json')); r=d['roofline']; print(json.dumps({'lib': '$L', 'rep': $rep, 'kernel_ms': r['avg_kernel_ms'], 'check': d['cpu_baseline']['sample_check']}))" | tee -a $O/ew.jsonl
+      done
+    done
+    ;;
   *)
     echo "unknown session $SESSION"; exit 2 ;;
 esac
