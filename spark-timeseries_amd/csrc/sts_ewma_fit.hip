@@ -73,7 +73,7 @@ template <int SPW, int CH, bool FIT>
 __global__ __launch_bounds__(64) void ewma_fit_kernel(EwmaFitArgs a) {
     constexpr int kRow = CH + 1;
     constexpr int NLD = SPW * CH / 64;
-    static_assert(SPW * CH % 64 == 0 && 64 % (64 * 64 / (SPW * CH) > 0 ? 1 : 1) == 0 && (CH % 64 == 0 || 64 % CH == 0), "chunk shape");
+    static_assert(SPW * CH % 64 == 0 && (CH % 64 == 0 || 64 % CH == 0), "chunk shape: whole load instructions");
     __shared__ double tile[SPW * kRow];
     const int lane = threadIdx.x;
     const int64_t s0 = (int64_t)blockIdx.x * SPW;
