@@ -209,6 +209,16 @@ PY
       done
     done
     ;;
+  c3sleep)
+    # C3: the MFMA phase with an s_sleep after each chunk's MFMAs (lower MFMA duty per wave) against the product
+    for rep in 1 2 3; do
+      for L in prod ${C3_VARS:-sleep1 sleep2}; do
+        if [ $L = prod ]; then E=""; else E="STS_HIP_LIB=spark-timeseries_amd/build/var_$L/libsts_hip.so"; fi
+        env $E timeout -k 10 300 python -u bench.py --workload c3 --steps 5 --warmup 2 --no-cpu-baseline > $O/c3s_$L.json 2>/dev/null || exit 1
+        python -c "import json; d=json.load(open('$O/c3s_$L.json')); r=d['roofline']; print(json.dumps({'lib': '$L', 'rep': $rep, 'kernel_ms': r['avg_kernel_ms'], 'frac': r['frac']}))" | tee -a $O/c3s.jsonl
+      done
+    done
+    ;;
   *)
     echo "unknown session $SESSION"; exit 2 ;;
 esac
