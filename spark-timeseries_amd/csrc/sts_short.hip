@@ -50,6 +50,10 @@ constexpr int kShortWaves = STS_SHORT_WAVES;
                            // 5 = + the store pass's LDS reads batched
 #endif
 
+#ifndef STS_SHORT_COMPACT
+#define STS_SHORT_COMPACT 0   // the fill's in-block runs as one wave-wide list (A/B)
+#endif
+
 #ifndef STS_SHORT_DIAG
 #define STS_SHORT_DIAG 0   // timing-only cost models (tools/variant.sh): 1 no ACF, 2 no fill,
                            // 3 no per-lag finalize, 4 no robust shift, 5 no lag products;
@@ -209,13 +213,48 @@ __device__ __forceinline__ bool short_fill(double* buf, unsigned long long vm, i
         // runs that start inside the block: step t NaN, t - 1 valid
         const unsigned long long inT = (tend - t0 >= 64) ? ~0ull : ((1ull << (tend > t0 ? tend - t0 : 0)) - 1ull);
         unsigned long long rs = ~vf & (vf << 1) & inT;
-        while (rs) {
-            const int j = __builtin_ctzll(rs);
-            rs &= rs - 1ull;
-            const int t = t0 + j;
-            const unsigned long long hi = (j + 1 < 64) ? vf >> (j + 1) : 0ull;
-            const int R = hi ? t + 1 + __builtin_ctzll(hi) : Rc;
-            fill_run(t, R < tend ? R : tend, t - 1, R);
+        if (STS_SHORT_COMPACT) {
+            // the wave's runs as one list, 64 at a time (a lane-by-lane loop runs as many rounds as
+            // the lane with the most runs): run g is the k-th run of the largest lane l with
+            // excl(l) <= g, excl = the runs of the lanes below (bit-sliced: nr <= B < 64)
+            const int nr = __popcll(rs);
+            int excl = 0, total = 0;
+#pragma unroll
+            for (int b = 0; b < 6; b++) {
+                const unsigned long long m = __ballot((nr >> b) & 1);
+                excl += (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u)) << b;
+                total += __popcll(m) << b;
+            }
+            for (int base = 0; base < total; base += 64) {
+                const int g = base + lane;
+                int lo = 0;   // every lane searches (bpermute sources must be active)
+#pragma unroll
+                for (int st = 32; st >= 1; st >>= 1)
+                    if (__shfl(excl, lo + st) <= g) lo += st;
+                const int k = g - __shfl(excl, lo);
+                const unsigned long long rso = __shfl(rs, lo), vfo = __shfl(vf, lo);
+                const int Rco = __shfl(Rc, lo);
+                if (g < total) {
+                    unsigned long long m = rso;
+                    for (int i = 0; i < k; i++) m &= m - 1ull;
+                    const int j = __builtin_ctzll(m);
+                    const int to = lo * B;
+                    const int t = to + j;
+                    const int tendo = (to + B < T) ? to + B : T;
+                    const unsigned long long hi = (j + 1 < 64) ? vfo >> (j + 1) : 0ull;
+                    const int R = hi ? t + 1 + __builtin_ctzll(hi) : Rco;
+                    fill_run(t, R < tendo ? R : tendo, t - 1, R);
+                }
+            }
+        } else {
+            while (rs) {
+                const int j = __builtin_ctzll(rs);
+                rs &= rs - 1ull;
+                const int t = t0 + j;
+                const unsigned long long hi = (j + 1 < 64) ? vf >> (j + 1) : 0ull;
+                const int R = hi ? t + 1 + __builtin_ctzll(hi) : Rc;
+                fill_run(t, R < tend ? R : tend, t - 1, R);
+            }
         }
     }
     return all_nan;

@@ -219,6 +219,19 @@ PY
       done
     done
     ;;
+  compact)
+    # C1: the fill's in-block runs as one wave-wide list (var_compact, -DSTS_SHORT_COMPACT=1) against the product
+    V=spark-timeseries_amd/build/var_compact/libsts_hip.so
+    timeout -k 10 900 $PYT --sts-lib $V tests/test_parity_gpu.py tests/test_acf_robust.py tests/test_fuzz_gpu.py -k "short or fused or autocorr or acf or fill" > $O/compact_pytest.log 2>&1 || { tail -40 $O/compact_pytest.log; exit 1; }
+    tail -1 $O/compact_pytest.log
+    for rep in 1 2 3; do
+      for L in prod compact; do
+        if [ $L = prod ]; then E=""; else E="STS_HIP_LIB=$V"; fi
+        env $E timeout -k 10 200 python -u bench.py --workload c1 --steps 20 --warmup 5 --cpu-seconds 2 > $O/compact_$L.json 2>/dev/null || exit 1
+        python -c "import json; d=json.load(open('$O/compact_$L.json')); r=d['roofline']; print(json.dumps({'lib': '$L', 'rep': $rep, 'kernel_ms': r['avg_kernel_ms'], 'frac': r['frac'], 'check': d['cpu_baseline']['sample_check']}))" | tee -a $O/compact.jsonl
+      done
+    done
+    ;;
   *)
     echo "unknown session $SESSION"; exit 2 ;;
 esac
