@@ -232,6 +232,28 @@ PY
       done
     done
     ;;
+  splsq2)
+    # the spline kernel's waiting time: instruction fetch and the I-cache
+    export TMPDIR=/tmp
+    timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_IFETCH SQ_WAIT_ANY SQ_INSTS_LDS SQ_ACTIVE_INST_ANY \
+        -d $O/splsq2_1 -o run --output-format csv -- python -u bench.py --workload spline --steps 1 --warmup 0 --no-cpu-baseline > $O/splsq2_1.out 2>&1 || { tail -5 $O/splsq2_1.out; exit 1; }
+    timeout -s KILL 120 rocprofv3 --pmc SQC_ICACHE_HITS SQC_ICACHE_MISSES SQC_ICACHE_REQ GRBM_GUI_ACTIVE \
+        -d $O/splsq2_2 -o run --output-format csv -- python -u bench.py --workload spline --steps 1 --warmup 0 --no-cpu-baseline > $O/splsq2_2.out 2>&1 || { tail -5 $O/splsq2_2.out; exit 1; }
+    python - <<'PY'
+import csv, glob, collections, json
+d = collections.defaultdict(list)
+for f in glob.glob("gpurun_out/r6/splsq2_*/**/*counter_collection.csv", recursive=True):
+    per = collections.defaultdict(dict)
+    for r in csv.DictReader(open(f)):
+        if "spline" not in r["Kernel_Name"]:
+            continue
+        k = int(r["Dispatch_Id"]); per[k][r["Counter_Name"]] = per[k].get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+    for c in per.values():
+        for k, v in c.items():
+            d[k].append(v)
+print(json.dumps({k: sum(v) / len(v) for k, v in sorted(d.items())}, indent=1))
+PY
+    ;;
   *)
     echo "unknown session $SESSION"; exit 2 ;;
 esac
